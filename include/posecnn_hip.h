@@ -1,0 +1,175 @@
+/*
+ * posecnn_hip.h — C-ABI of libposecnn_hip.so, the MI355X (gfx950) replacement
+ * for the native launchers behind PoseCNN's custom ops.
+ *
+ * Conventions
+ *  - every pointer is a DEVICE pointer unless the name ends in _host;
+ *  - `stream` is a hipStream_t passed as void* (NULL = legacy default stream);
+ *  - nothing allocates: temporaries live in a caller-provided `workspace` whose
+ *    size the matching *_workspace_size() query returns;
+ *  - nothing synchronises: variable-length results (RoI rows) are written into
+ *    capacity-sized buffers with a device-side row count, so a whole
+ *    vote -> RoI pool -> FC -> loss step can be captured in a hipGraph;
+ *  - return value 0 = PCNN_OK, otherwise a PCNN_E* code (never exit()).
+ *
+ * Reference seam replaced (mrlooi/PoseCNN): the TF OpKernel::Compute methods
+ * call C++ launchers with raw device pointers + an Eigen::GpuDevice stream.
+ */
+#ifndef POSECNN_HIP_H
+#define POSECNN_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PCNN_OK 0
+#define PCNN_EINVAL 1    /* bad shape / argument (reference: OP_REQUIRES InvalidArgument) */
+#define PCNN_EHIP 2      /* HIP launch error (reference: fprintf + exit(-1)) */
+#define PCNN_ECAPACITY 3 /* workspace or output capacity too small */
+
+#define PCNN_MAX_ROI 128 /* hough_voting_gpu_op.cu.cc:14 */
+
+int pcnn_abi_version(void);
+const char* pcnn_strerror(int code);
+
+/* ---------------------------------------------------------------------------
+ * Hough voting (Houghvotinggpu).
+ * Replaces HoughVotingLaucher (lib/hough_voting_gpu_layer/hough_voting_gpu_op.cu.cc:615-799)
+ * called per image from HoughvotinggpuOp<GPU>::Compute (hough_voting_gpu_op.cc:321-429).
+ *  label  (B,H,W) int32          vertex (B,H,W,3C) f32      extents (C,3) f32
+ *  meta   (B,num_meta) f32       gt (num_gt,13) f32 [b,cls,0,0,0,0,qw,qx,qy,qz,tx,ty,tz]
+ *  outputs, capacity `cap` rows (reference MAX_ROI*9 = 1152):
+ *    top_box (cap,7) [b,cls,x1,y1,x2,y2,score]  top_pose (cap,7) [qw,qx,qy,qz,tx,ty,tz]
+ *    top_target/top_weight (cap,4C)              top_domain (cap) int32
+ *    num_rois (2) int32: [0] = rows emitted, [1] = max(rows, 1) (the op's
+ *    output row count; row 0 is the all-zero dummy when rows == 0,
+ *    hough_voting_gpu_op.cc:382-383)
+ *  batch_base   added to the batch column (image-sharded runs, global image index)
+ *  global_batch index_size = PCNN_MAX_ROI / global_batch (cu.cc:734)
+ *  inlier_thr = 0.9, label_thr = 500 in the reference (hough_voting_gpu_op.cc:356-357)
+ *  vote_thr <= 0: single instance per class (argmax); > 0: Hough-space NMS.
+ *  debug_counts (optional, may be NULL): (B, C-1, H, W) int32 vote counts per
+ *    present-class slot (slot order = ascending class id), the reference hough_space.
+ * ------------------------------------------------------------------------- */
+size_t pcnn_hough_voting_workspace_size(int B, int H, int W, int C, int skip_pixels, float vote_thr);
+
+int pcnn_hough_voting(const int32_t* label, const float* vertex, const float* extents, const float* meta,
+                      int num_meta, const float* gt, int num_gt, int B, int H, int W, int C, int batch_base,
+                      int global_batch, int is_train, float inlier_thr, int label_thr, float vote_thr,
+                      float per_thr, int skip_pixels, float* top_box, float* top_pose, float* top_target,
+                      float* top_weight, int32_t* top_domain, int32_t* num_rois, int cap, int32_t* debug_counts,
+                      void* workspace, size_t workspace_bytes, void* stream);
+
+/* HoughvotinggpuGrad (hough_voting_gpu_op.cc:440-484; set_gradients cu.cc:608-612):
+ * zero gradients for label (B,H,W) and vertex (B,H,W,3C). Either may be NULL. */
+int pcnn_hough_voting_grad(float* grad_label, float* grad_vertex, int B, int H, int W, int C, void* stream);
+
+/* Diagnostic counters of the last pcnn_hough_voting call on `workspace`:
+ * copies [0] = count mismatches between the interval vote and the exact
+ * per-voter re-check at emitted maxima (must be 0), [1] = NMS candidate
+ * overflows, [2..3] reserved. Synchronous (reads device memory). */
+int pcnn_hough_voting_diag(const void* workspace, int B, int H, int W, int C, int skip_pixels, float vote_thr,
+                           int32_t* diag_host4, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * RoI max pooling (RoiPool / RoiPoolGrad).
+ * Replaces ROIPoolForwardLaucher / ROIPoolBackwardLaucher
+ * (lib/roi_pooling_layer/roi_pooling_op_gpu.cu.cc:103-131, :232-254;
+ *  called from roi_pooling_op.cc:250-254, :358-361).
+ *  layout 0 = NHWC data (B,H,W,C), output (R,PH,PW,Cout)  [TF op]
+ *  layout 1 = NCHW data (B,C,H,W), output (R,Cout,PH,PW)  [my_tools _RoIPooling]
+ *  rois (R_cap, roi_stride) rows [b, cls, x1, y1, x2, y2, ...] (roi_stride >= 6), or
+ *       with roi_stride == 5 rows [b, x1, y1, x2, y2] (pth API, class column absent)
+ *  num_rois_dev: optional device int; when non-NULL the row count is
+ *       min(*num_rois_dev, R_cap) (rows beyond are not touched)
+ *  argmax: flat index within the image, (h*W + w)*C + c (NHWC) or (c*H + h)*W + w (NCHW)
+ * ------------------------------------------------------------------------- */
+int pcnn_roi_pool_fwd(const float* data, int B, int H, int W, int C, int layout, const float* rois, int R_cap,
+                      int roi_stride, const int32_t* num_rois_dev, float spatial_scale, int pooled_h, int pooled_w,
+                      int pool_channel, float* top, int32_t* argmax, void* stream);
+
+size_t pcnn_roi_pool_bwd_workspace_size(int B, int R_cap);
+
+int pcnn_roi_pool_bwd(const float* top_diff, const int32_t* argmax, int B, int H, int W, int C, int layout,
+                      const float* rois, int R_cap, int roi_stride, const int32_t* num_rois_dev,
+                      float spatial_scale, int pooled_h, int pooled_w, int pool_channel, float* bottom_diff,
+                      void* workspace, size_t workspace_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * ADD / ADD-S pose loss (Averagedistance / AveragedistanceGrad).
+ * Replaces AveragedistanceForwardLaucher / AveragedistanceBackwardLaucher
+ * (lib/average_distance_loss/average_distance_loss_op_gpu.cu.cc:256-343, :357-377;
+ *  called from average_distance_loss_op.cc:228-231, :362-363).
+ *  pred/target/weight (R_cap, 4C), points (C,P,3), symmetry (C)
+ *  loss (1) f32, bottom_diff (R_cap, 4C); rows counted from num_rois_dev when non-NULL.
+ *  loss_norm_rows: when > 0, the normaliser R of (d - m)/(2 R P) and of the
+ *       gradient (an image-sharded run passes the global row count so that the
+ *       per-rank losses sum to the single-device loss); <= 0 uses the local R.
+ * ------------------------------------------------------------------------- */
+size_t pcnn_add_loss_workspace_size(int R_cap, int C, int P);
+
+int pcnn_add_loss_fwd(const float* pred, const float* target, const float* weight, const float* points,
+                      const float* symmetry, int R_cap, const int32_t* num_rois_dev, int C, int P, float margin,
+                      int loss_norm_rows, const int32_t* loss_norm_rows_dev, float* loss, float* bottom_diff,
+                      void* workspace, size_t workspace_bytes, void* stream);
+
+/* out[i] = top_diff[0] * bottom_diff[i], n = rows * 4C */
+int pcnn_add_loss_bwd(const float* top_diff, const float* bottom_diff, int n, const int32_t* num_rois_dev,
+                      int row_len, float* out, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Depth backprojection (Backproject / BackprojectGrad).
+ * Replaces BackprojectForwardLaucher / BackprojectBackwardLaucher
+ * (lib/backprojecting_layer/backprojecting_op_gpu.cu.cc:129-155, :220-242;
+ *  called from backprojecting_op.cc:262-267, :388-390).
+ *  data (B,H,W,Ch) label (B,H,W,NC) depth (B,H,W) meta (B,num_meta) label_3d (B,G,G,G,NC)
+ *  -> top_data (B,G,G,G,Ch), top_label (B,G,G,G,NC), top_flag (B,G,G,G,Ch)
+ * ------------------------------------------------------------------------- */
+int pcnn_backproject_fwd(const float* data, const float* label, const float* depth, const float* meta, int num_meta,
+                         const float* label_3d, int B, int H, int W, int Ch, int NC, int grid_size,
+                         int kernel_size, float threshold, float* top_data, float* top_label, float* top_flag,
+                         void* stream);
+
+int pcnn_backproject_bwd(const float* top_diff, const float* depth, const float* meta, int num_meta, int B, int H,
+                         int W, int Ch, int grid_size, float* bottom_diff, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Pose-head FC contraction (MFMA).  Replaces the TF matmuls of
+ * Network.fc (lib/networks/network.py:393-423) as wired by vgg16_convs.py:186-197:
+ *   C[M,N] = epilogue( op(A)[M,K] (+ op(A2)) * op(B)[K,N] )
+ *  a_trans: 0 -> A stored (M,K) row-major (lda >= K); 1 -> A stored (K,M) (lda >= M)
+ *  b_trans: 0 -> B stored (K,N) (ldb >= N);           1 -> B stored (N,K) (ldb >= K)
+ *  A2 (optional): same layout as A, added elementwise (pool5 + pool4 fusion)
+ *  M_dev / K_dev (optional device ints): effective M / K = min(*dev, M / K)
+ *  epilogue: bias (N) added if non-NULL; act 0 none, 1 relu;
+ *            mask (optional, ldm) -> C *= (mask > 0)  (relu backward)
+ *  precision: 0 = exact fp32 MFMA (v_mfma_f32_32x32x2_f32),
+ *             1 = split-bf16 x3 MFMA (fp32-class accuracy, ~5x the fp32 rate)
+ *  Deterministic (split-K partials are reduced in fixed order).
+ * ------------------------------------------------------------------------- */
+size_t pcnn_gemm_workspace_size(int M, int N, int K, int precision);
+
+int pcnn_gemm(int M, int N, int K, const float* A, const float* A2, int lda, int a_trans, const float* B, int ldb,
+              int b_trans, float* Cm, int ldc, const float* bias, int act, const float* mask, int ldm,
+              const int32_t* M_dev, const int32_t* K_dev, int precision, void* workspace, size_t workspace_bytes,
+              void* stream);
+
+/* Column sums over the first min(*M_dev, M) rows: out[n] = sum_m X[m, n] (bias gradients). */
+int pcnn_colsum(const float* X, int M, int N, int ldx, const int32_t* M_dev, float* out, void* stream);
+
+/* Pose-head tail (vgg16_convs.py:193-197): T = tanh(Y8); Mw = T * poses_weight;
+ * pred = Mw / sqrt(max(sum(Mw^2), 1e-12)) (tf.nn.l2_normalize, dim 1).  Rows (R_cap, D). */
+int pcnn_pose_head_fwd(const float* y8, const float* poses_weight, int R_cap, const int32_t* num_rois_dev, int D,
+                       float* tanh_out, float* pred, void* stream);
+
+/* Backward of the tail: d_pred -> d_y8 (through l2_normalize, multiply, tanh). */
+int pcnn_pose_head_bwd(const float* d_pred, const float* tanh_out, const float* poses_weight, const float* pred,
+                       int R_cap, const int32_t* num_rois_dev, int D, float* d_y8, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* POSECNN_HIP_H */

@@ -1,0 +1,204 @@
+"""ORACLE — TEST INFRASTRUCTURE ONLY.
+
+ctypes bindings of oracle/build/liborc.so, the CPU C++ restatement of the
+reference ops (see orc_common.h for the parity status: UNPINNED — no reference
+golden vectors exist and the reference cannot be built here; pinned by the
+hand-derived KATs in tests/test_oracle_kat.py).
+
+May be imported only by tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg, and only as the checker / CPU baseline.
+"""
+import ctypes
+import os
+import subprocess
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "build", "liborc.so")
+_lib = None
+
+F32P = ctypes.POINTER(ctypes.c_float)
+I32P = ctypes.POINTER(ctypes.c_int)
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", _HERE])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        _lib = ctypes.CDLL(_LIB_PATH)
+        _lib.orc_hough_voting.restype = ctypes.c_int
+        _lib.orc_hough_class_counts.restype = ctypes.c_int
+        _lib.orc_roi_pool_fwd.restype = ctypes.c_int
+        _lib.orc_roi_pool_bwd.restype = ctypes.c_int
+        _lib.orc_ransac_hough.restype = ctypes.c_int
+    return _lib
+
+
+def _f(a):
+    a = np.ascontiguousarray(a, dtype=np.float32)
+    return a, a.ctypes.data_as(F32P)
+
+
+def _i(a):
+    a = np.ascontiguousarray(a, dtype=np.int32)
+    return a, a.ctypes.data_as(I32P)
+
+
+MAX_ROI = 128
+
+
+def hough_voting(label, vertex, extents, meta, gt, is_train, threshold_vote, threshold_percentage, skip_pixels,
+                 inlier_threshold=0.9, label_threshold=500, batch_base=0, global_batch=None, exact_rows=True):
+    """Reference semantics of hough_voting_gpu (canonical order).  Returns
+    (box, pose, target, weight, domain, num_rois) with exact-size outputs
+    (one zero dummy row when num_rois == 0) when exact_rows."""
+    label, lp = _i(label)
+    vertex, vp = _f(vertex)
+    extents, ep = _f(extents)
+    B, H, W = label.shape
+    C = vertex.shape[3] // 3
+    meta2 = np.ascontiguousarray(np.asarray(meta, np.float32).reshape(B, -1))
+    num_meta = meta2.shape[1]
+    meta2, mp = _f(meta2)
+    gt2 = np.ascontiguousarray(np.asarray(gt, np.float32).reshape(-1, 13))
+    gt2, gp = _f(gt2)
+    cap = MAX_ROI * 9
+    box = np.zeros((cap, 7), np.float32)
+    pose = np.zeros((cap, 7), np.float32)
+    target = np.zeros((cap, 4 * C), np.float32)
+    weight = np.zeros((cap, 4 * C), np.float32)
+    domain = np.zeros((cap,), np.int32)
+    n = lib().orc_hough_voting(lp, vp, ep, mp, num_meta, gp, gt2.shape[0], B, H, W, C, batch_base,
+                               global_batch or B, int(is_train), ctypes.c_float(inlier_threshold), label_threshold,
+                               ctypes.c_float(threshold_vote), ctypes.c_float(threshold_percentage), skip_pixels,
+                               box.ctypes.data_as(F32P), pose.ctypes.data_as(F32P), target.ctypes.data_as(F32P),
+                               weight.ctypes.data_as(F32P), domain.ctypes.data_as(I32P), cap)
+    if n < 0:
+        raise RuntimeError("oracle hough: capacity exceeded")
+    if exact_rows:
+        k = max(n, 1)
+        return box[:k], pose[:k], target[:k], weight[:k], domain[:k], n
+    return box, pose, target, weight, domain, n
+
+
+def hough_class_counts(label_img, vertex_img, extents, meta_row, cls, skip, inlier_threshold=0.9):
+    label_img, lp = _i(label_img)
+    vertex_img, vp = _f(vertex_img)
+    extents, ep = _f(extents)
+    meta_row, mp = _f(np.asarray(meta_row, np.float32).reshape(-1))
+    H, W = label_img.shape
+    C = vertex_img.shape[2] // 3
+    counts = np.zeros((H, W), np.float32)
+    dsum = np.zeros((H, W), np.float32)
+    nv = lib().orc_hough_class_counts(lp, vp, ep, mp, H, W, C, cls, ctypes.c_float(inlier_threshold), skip,
+                                      counts.ctypes.data_as(F32P), dsum.ctypes.data_as(F32P))
+    return counts, dsum, nv
+
+
+def hough_data_at(label_img, vertex_img, extents, meta_row, cls, skip, cx, cy, count, dsum, inlier_threshold=0.9):
+    label_img, lp = _i(label_img)
+    vertex_img, vp = _f(vertex_img)
+    extents, ep = _f(extents)
+    meta_row, mp = _f(np.asarray(meta_row, np.float32).reshape(-1))
+    H, W = label_img.shape
+    C = vertex_img.shape[2] // 3
+    out = np.zeros(3, np.float32)
+    lib().orc_hough_data_at(lp, vp, ep, mp, H, W, C, cls, ctypes.c_float(inlier_threshold), skip, cx, cy,
+                            ctypes.c_float(count), ctypes.c_float(dsum), out.ctypes.data_as(F32P))
+    return out
+
+
+def roi_pool_fwd(data, rois, pooled_h, pooled_w, spatial_scale, pool_channel=0):
+    data, dp = _f(data)
+    rois, rp = _f(np.asarray(rois, np.float32).reshape(np.asarray(rois).shape[0], -1))
+    B, H, W, C = data.shape
+    R, rs = rois.shape
+    Co = 1 if pool_channel else C
+    top = np.zeros((R, pooled_h, pooled_w, Co), np.float32)
+    arg = np.zeros((R, pooled_h, pooled_w, Co), np.int32)
+    rc = lib().orc_roi_pool_fwd(dp, B, H, W, C, rp, R, rs, ctypes.c_float(spatial_scale), pooled_h, pooled_w,
+                                int(pool_channel), top.ctypes.data_as(F32P), arg.ctypes.data_as(I32P))
+    if rc != 0:
+        raise ValueError("roi batch index out of range")
+    return top, arg
+
+
+def roi_pool_bwd(top_diff, argmax, data_shape, rois, pooled_h, pooled_w, spatial_scale, pool_channel=0):
+    top_diff, tp = _f(top_diff)
+    argmax, ap = _i(argmax)
+    rois, rp = _f(np.asarray(rois, np.float32).reshape(np.asarray(rois).shape[0], -1))
+    B, H, W, C = data_shape
+    R, rs = rois.shape
+    out = np.zeros((B, H, W, C), np.float32)
+    lib().orc_roi_pool_bwd(tp, ap, B, H, W, C, rp, R, rs, ctypes.c_float(spatial_scale), pooled_h, pooled_w,
+                           int(pool_channel), out.ctypes.data_as(F32P))
+    return out
+
+
+def average_distance_loss(pred, target, weight, points, symmetry, margin):
+    pred, pp = _f(pred)
+    target, tp = _f(target)
+    weight, wp = _f(weight)
+    points, ptp = _f(points)
+    symmetry, sp = _f(symmetry)
+    R, PC = pred.shape
+    C = PC // 4
+    P = points.shape[1]
+    loss = np.zeros(1, np.float32)
+    diff = np.zeros((R, PC), np.float32)
+    rows = np.zeros(R, np.float32)
+    lib().orc_add_loss_fwd(pp, tp, wp, ptp, sp, R, C, P, ctypes.c_float(margin), loss.ctypes.data_as(F32P),
+                           diff.ctypes.data_as(F32P), rows.ctypes.data_as(F32P))
+    return loss, diff, rows
+
+
+def backproject_fwd(data, label, depth, meta, label_3d, grid_size, kernel_size, threshold):
+    data, dp = _f(data)
+    label, lp = _f(label)
+    depth, zp = _f(depth)
+    B, H, W, Ch = data.shape
+    NC = label.shape[3]
+    meta2 = np.ascontiguousarray(np.asarray(meta, np.float32).reshape(B, -1))
+    meta2, mp = _f(meta2)
+    label_3d, l3p = _f(label_3d)
+    G = grid_size
+    td = np.zeros((B, G, G, G, Ch), np.float32)
+    tl = np.zeros((B, G, G, G, NC), np.float32)
+    tf = np.zeros((B, G, G, G, Ch), np.float32)
+    lib().orc_backproject_fwd(dp, lp, zp, mp, meta2.shape[1], l3p, B, H, W, Ch, NC, G, kernel_size,
+                              ctypes.c_float(threshold), td.ctypes.data_as(F32P), tl.ctypes.data_as(F32P),
+                              tf.ctypes.data_as(F32P))
+    return td, tl, tf
+
+
+def backproject_bwd(top_diff, depth, meta, H, W, grid_size):
+    top_diff, tp = _f(top_diff)
+    depth, zp = _f(depth)
+    B = top_diff.shape[0]
+    Ch = top_diff.shape[-1]
+    meta2 = np.ascontiguousarray(np.asarray(meta, np.float32).reshape(B, -1))
+    meta2, mp = _f(meta2)
+    out = np.zeros((B, H, W, Ch), np.float32)
+    lib().orc_backproject_bwd(tp, zp, mp, meta2.shape[1], B, H, W, Ch, grid_size, out.ctypes.data_as(F32P))
+    return out
+
+
+def ransac_hough(label, vertex, extents, meta, is_train=0, num_threads=0):
+    """CPU baseline (reference Houghvoting op restatement); rows of 13 floats."""
+    label, lp = _i(label)
+    vertex, vp = _f(vertex)
+    extents, ep = _f(extents)
+    B, H, W = label.shape
+    C = vertex.shape[3] // 3
+    meta2 = np.ascontiguousarray(np.asarray(meta, np.float32).reshape(B, -1))
+    meta2, mp = _f(meta2)
+    cap = 4096
+    rows = np.zeros((cap, 13), np.float32)
+    n = lib().orc_ransac_hough(lp, vp, ep, mp, meta2.shape[1], B, H, W, C, int(is_train), int(num_threads),
+                               rows.ctypes.data_as(F32P), cap)
+    return rows[:min(n, cap)]

@@ -1,0 +1,83 @@
+"""Pose head of vgg16_convs (lib/networks/vgg16_convs.py:186-200) on the HIP
+MFMA GEMM: pool5 + pool4 -> fc6 (relu) -> fc7 (relu) -> fc8 -> tanh ->
+* poses_weight -> l2_normalize, forward and backward, with every row count
+read on the device (capacity-sized RoI buffers, no host sync).
+
+Weights follow Network.fc (network.py:393-423): `weights` [in, out] with
+truncated-normal(0, 0.001) init (network.py:415), `biases` [out] zero; the
+reshape of the (R,7,7,512) pooled features is NHWC-flat ((h*7+w)*512+c).
+Dropout is the identity (keep_prob = 1, the test-time graph).
+"""
+import torch
+
+from . import _lib
+
+
+def gemm(A, B, C, a_trans=0, b_trans=0, A2=None, bias=None, act=0, mask=None, M_dev=None, K_dev=None, M=None,
+         N=None, K=None, precision=0, stream=None):
+    """C[M,N] = epilogue(op(A) (+ op(A2)) @ op(B)); see pcnn_gemm in include/posecnn_hip.h."""
+    _lib.require_gpu(A, B, C)
+    for t in (A, B, C, A2, bias, mask):
+        if t is not None and (t.dtype != torch.float32 or t.stride(-1) != 1):
+            raise ValueError("gemm operands must be fp32 with unit inner stride")
+    if M is None:
+        M = A.shape[1] if a_trans else A.shape[0]
+    if K is None:
+        K = A.shape[0] if a_trans else A.shape[1]
+    if N is None:
+        N = B.shape[0] if b_trans else B.shape[1]
+    lib = _lib.load()
+    ws = _lib.workspace(lib.pcnn_gemm_workspace_size(M, N, K, precision), C.device, "gemm")
+    rc = lib.pcnn_gemm(M, N, K, _lib.ptr(A), _lib.ptr(A2), A.stride(0), int(a_trans), _lib.ptr(B), B.stride(0),
+                       int(b_trans), _lib.ptr(C), C.stride(0), _lib.ptr(bias), int(act), _lib.ptr(mask),
+                       mask.stride(0) if mask is not None else 0, _lib.ptr(M_dev), _lib.ptr(K_dev), int(precision),
+                       _lib.ptr(ws), ws.numel(), _lib.stream_ptr(stream))
+    _lib.check(rc, "gemm")
+    return C
+
+
+def colsum(X, out, M_dev=None, stream=None):
+    rc = _lib.load().pcnn_colsum(_lib.ptr(X), X.shape[0], X.shape[1], X.stride(0), _lib.ptr(M_dev), _lib.ptr(out),
+                                 _lib.stream_ptr(stream))
+    _lib.check(rc, "colsum")
+    return out
+
+
+def head_fwd(y8, poses_weight, tanh_out, pred, num_rois=None, stream=None):
+    R, D = y8.shape
+    rc = _lib.load().pcnn_pose_head_fwd(_lib.ptr(y8), _lib.ptr(poses_weight), R, _lib.ptr(num_rois), D,
+                                        _lib.ptr(tanh_out), _lib.ptr(pred), _lib.stream_ptr(stream))
+    _lib.check(rc, "pose_head_fwd")
+
+
+def head_bwd(d_pred, tanh_out, poses_weight, pred, d_y8, num_rois=None, stream=None):
+    R, D = d_pred.shape
+    rc = _lib.load().pcnn_pose_head_bwd(_lib.ptr(d_pred), _lib.ptr(tanh_out), _lib.ptr(poses_weight),
+                                        _lib.ptr(pred), R, _lib.ptr(num_rois), D, _lib.ptr(d_y8),
+                                        _lib.stream_ptr(stream))
+    _lib.check(rc, "pose_head_bwd")
+
+
+def truncated_normal(shape, std, generator, device):
+    t = torch.empty(shape, dtype=torch.float32, device=device)
+    torch.nn.init.trunc_normal_(t, 0.0, std, -2 * std, 2 * std, generator=generator)
+    return t
+
+
+class PoseHeadWeights:
+    """fc6 / fc7 / fc8 variables of the pose head (vgg16_convs.py:186-192)."""
+
+    def __init__(self, num_classes, device, in_dim=7 * 7 * 512, units=4096, seed=0):
+        g = torch.Generator(device=device)
+        g.manual_seed(seed)
+        D = 4 * num_classes
+        self.w6 = truncated_normal((in_dim, units), 0.001, g, device)
+        self.b6 = torch.zeros(units, device=device)
+        self.w7 = truncated_normal((units, units), 0.001, g, device)
+        self.b7 = torch.zeros(units, device=device)
+        self.w8 = truncated_normal((units, D), 0.001, g, device)
+        self.b8 = torch.zeros(D, device=device)
+        self.in_dim, self.units, self.D = in_dim, units, D
+
+    def grads_like(self):
+        return {k: torch.empty_like(getattr(self, k)) for k in ("w6", "b6", "w7", "b7", "w8", "b8")}

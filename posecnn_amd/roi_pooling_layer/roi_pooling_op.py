@@ -1,0 +1,79 @@
+"""Drop-in for lib/roi_pooling_layer/roi_pooling_op.py (:4-7): `roi_pool` /
+`roi_pool_grad` over NHWC features (REGISTER_OP("RoiPool") / "RoiPoolGrad",
+roi_pooling_op.cc:29-50), backed by libposecnn_hip.so.
+
+roi_pool(data (B,H,W,C), rois (R, >=6), pooled_height, pooled_width,
+         spatial_scale, pool_channel) -> (top (R,PH,PW,C or 1), argmax int32)
+roi_pool_grad(data, rois, argmax, grad, ...) -> d data  (roi_pooling_op_grad.py:33-50)
+`num_rois` (optional device int32 scalar tensor) bounds the rows used, for the
+capacity-sized RoI buffers of the fused pose step.
+"""
+import torch
+
+from .. import _lib
+
+
+def roi_pool(bottom_data, bottom_rois, pooled_height, pooled_width, spatial_scale, pool_channel=0, name=None,
+             num_rois=None, layout=0, out=None):
+    _lib.require_gpu(bottom_data, bottom_rois)
+    if bottom_data.dim() != 4:
+        raise ValueError("data must be 4-dimensional")  # roi_pooling_op.cc:92-93
+    if bottom_rois.dim() != 2:
+        raise ValueError("rois must be 2-dimensional")  # :96-97
+    data = bottom_data.contiguous().float()
+    rois = bottom_rois.contiguous().float()
+    if layout == 0:
+        B, H, W, C = data.shape
+    else:
+        B, C, H, W = data.shape
+    R, stride = rois.shape
+    Co = 1 if pool_channel else C
+    shape = (R, pooled_height, pooled_width, Co) if layout == 0 else (R, Co, pooled_height, pooled_width)
+    if out is None:
+        top = torch.empty(shape, dtype=torch.float32, device=data.device)
+        arg = torch.empty(shape, dtype=torch.int32, device=data.device)
+    else:
+        top, arg = out
+    rc = _lib.load().pcnn_roi_pool_fwd(_lib.ptr(data), B, H, W, C, layout, _lib.ptr(rois), R, stride,
+                                       _lib.ptr(num_rois), float(spatial_scale), int(pooled_height),
+                                       int(pooled_width), int(pool_channel), _lib.ptr(top), _lib.ptr(arg),
+                                       _lib.stream_ptr())
+    _lib.check(rc, "roi_pool")
+    return top, arg
+
+
+def roi_pool_grad(bottom_data, bottom_rois, argmax, grad, pooled_height, pooled_width, spatial_scale,
+                  pool_channel=0, name=None, num_rois=None, layout=0, out=None):
+    _lib.require_gpu(bottom_data, bottom_rois, argmax, grad)
+    rois = bottom_rois.contiguous().float()
+    if layout == 0:
+        B, H, W, C = bottom_data.shape
+    else:
+        B, C, H, W = bottom_data.shape
+    R, stride = rois.shape
+    lib = _lib.load()
+    ws = _lib.workspace(lib.pcnn_roi_pool_bwd_workspace_size(B, R), bottom_data.device, "roi_bwd")
+    dd = out if out is not None else torch.empty(bottom_data.shape, dtype=torch.float32, device=bottom_data.device)
+    rc = lib.pcnn_roi_pool_bwd(_lib.ptr(grad.contiguous()), _lib.ptr(argmax.contiguous()), B, H, W, C, layout,
+                               _lib.ptr(rois), R, stride, _lib.ptr(num_rois), float(spatial_scale),
+                               int(pooled_height), int(pooled_width), int(pool_channel), _lib.ptr(dd),
+                               _lib.ptr(ws), ws.numel(), _lib.stream_ptr())
+    _lib.check(rc, "roi_pool_grad")
+    return dd
+
+
+class RoiPoolFunction(torch.autograd.Function):
+    """autograd binding (the TF gradient registration, roi_pooling_op_grad.py:29-50)."""
+
+    @staticmethod
+    def forward(ctx, data, rois, pooled_height, pooled_width, spatial_scale, pool_channel=0, layout=0):
+        top, arg = roi_pool(data, rois, pooled_height, pooled_width, spatial_scale, pool_channel, layout=layout)
+        ctx.save_for_backward(data, rois, arg)
+        ctx.params = (pooled_height, pooled_width, spatial_scale, pool_channel, layout)
+        return top, arg
+
+    @staticmethod
+    def backward(ctx, grad, _garg):
+        data, rois, arg = ctx.saved_tensors
+        ph, pw, sc, pc, layout = ctx.params
+        return roi_pool_grad(data, rois, arg, grad, ph, pw, sc, pc, layout=layout), None, None, None, None, None, None

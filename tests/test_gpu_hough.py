@@ -1,0 +1,93 @@
+"""GPU parity: hough_voting_gpu (HIP) vs the oracle restatement of the
+reference (oracle/orc_hough.cpp), bit-exact on every output column."""
+import numpy as np
+import pytest
+import torch
+
+from posecnn_amd import synth
+from posecnn_amd.hough_voting_gpu_layer import hough_voting_gpu_op as hv
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(fr, is_train, vote_thr=-1.0, per=0.02, skip=10, global_batch=None, batch_base=0):
+    d = torch.device("cuda")
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(d)
+    o = hv.hough_voting_gpu_capacity(t(fr["label"]), t(fr["vertex"]), t(fr["extents"]), t(fr["meta"]), t(fr["gt"]),
+                                     is_train, vote_thr, per, skip, global_batch=global_batch, batch_base=batch_base)
+    torch.cuda.synchronize()
+    n = int(o["num_rois"][1].item())
+    diag = hv.hough_voting_diag(o)
+    res = [o[k][:n].cpu().numpy() for k in ("box", "pose", "target", "weight", "domain")]
+    return res, int(o["num_rois"][0].item()), diag
+
+
+def _check(orc, fr, is_train, vote_thr=-1.0, skip=10, global_batch=None, batch_base=0):
+    (box, pose, tgt, wgt, dom), n, diag = _run(fr, is_train, vote_thr, skip=skip, global_batch=global_batch,
+                                               batch_base=batch_base)
+    ob, op, ot, ow, od, on = orc.hough_voting(fr["label"], fr["vertex"], fr["extents"], fr["meta"], fr["gt"],
+                                              is_train, vote_thr, 0.02, skip, global_batch=global_batch,
+                                              batch_base=batch_base)
+    assert diag[0] == 0, "interval vote count != exact re-count"
+    assert n == on
+    np.testing.assert_array_equal(box, ob)
+    np.testing.assert_array_equal(pose, op)
+    np.testing.assert_array_equal(tgt, ot)
+    np.testing.assert_array_equal(wgt, ow)
+    np.testing.assert_array_equal(dom, od)
+    return n
+
+
+@pytest.mark.parametrize("is_train", [0, 1])
+def test_hough_small_frames(hip, orc, is_train):
+    fr = synth.make_frames(3, H=120, W=160, num_classes=22, objects_per_image=4, seed=11)
+    n = _check(orc, fr, is_train, skip=3)
+    assert n > 0
+
+
+def test_hough_full_frame_train(hip, orc):
+    fr = synth.make_frames(1, seed=2)
+    assert _check(orc, fr, 1, skip=10) > 0
+
+
+def test_hough_full_frame_skip1(hip, orc):
+    fr = synth.make_frames(1, H=240, W=320, seed=5)
+    assert _check(orc, fr, 0, skip=1) > 0
+
+
+def test_hough_counts_map_exact(hip, orc):
+    """The whole per-class Hough space (reference hough_space) matches exactly."""
+    fr = synth.make_frames(1, H=120, W=160, seed=7, objects_per_image=3)
+    d = torch.device("cuda")
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(d)
+    B, H, W = fr["label"].shape
+    C = 22
+    dbg = torch.zeros((B, C - 1, H, W), dtype=torch.int32, device=d)
+    o = hv.hough_voting_gpu_capacity(t(fr["label"]), t(fr["vertex"]), t(fr["extents"]), t(fr["meta"]),
+                                     t(fr["gt"]), 0, -1.0, 0.02, 2, debug_counts=dbg)
+    torch.cuda.synchronize()
+    dbg = dbg.cpu().numpy()
+    counts = np.bincount(fr["label"][0].ravel(), minlength=C)
+    present = [c for c in range(1, C) if counts[c] > 500]
+    assert present
+    for s, c in enumerate(present):
+        oc, _, _ = orc.hough_class_counts(fr["label"][0], fr["vertex"][0], fr["extents"], fr["meta"][0], c, 2)
+        np.testing.assert_array_equal(dbg[0, s], oc.astype(np.int32))
+
+
+def test_hough_multi_instance_nms(hip, orc):
+    fr = synth.make_frames(2, H=120, W=160, seed=3, objects_per_image=4)
+    _check(orc, fr, 1, vote_thr=20.0, skip=2)
+
+
+def test_hough_sharded_rebase(hip, orc):
+    """index_size from the global batch, batch column rebased (sharded runs)."""
+    fr = synth.make_frames(2, H=120, W=160, seed=4, image_offset=6)
+    _check(orc, fr, 1, skip=3, global_batch=64, batch_base=6)
+
+
+def test_hough_no_detection_dummy_row(hip, orc):
+    fr = synth.make_frames(2, H=60, W=80, seed=1, objects_per_image=2)
+    fr["label"][:] = 0
+    (box, pose, tgt, wgt, dom), n, _ = _run(fr, 1)
+    assert n == 0 and box.shape == (1, 7) and not box.any() and not pose.any()
