@@ -150,7 +150,7 @@ int pcnn_backproject_bwd(const float* top_diff, const float* depth, const float*
  *             1 = split-bf16 x3 MFMA (fp32-class accuracy, ~5x the fp32 rate)
  *  Deterministic (split-K partials are reduced in fixed order).
  * ------------------------------------------------------------------------- */
-size_t pcnn_gemm_workspace_size(int M, int N, int K, int precision);
+size_t pcnn_gemm_workspace_size(int M, int N, int K, int m_dynamic, int precision);
 
 int pcnn_gemm(int M, int N, int K, const float* A, const float* A2, int lda, int a_trans, const float* B, int ldb,
               int b_trans, float* Cm, int ldc, const float* bias, int act, const float* mask, int ldm,

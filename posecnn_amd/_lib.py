@@ -46,7 +46,7 @@ _SIGS = {
                                      c_int, c_int, c_int, c_int, c_float, c_void_p, c_void_p, c_void_p, c_void_p]),
     "pcnn_backproject_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int,
                                      c_void_p, c_void_p]),
-    "pcnn_gemm_workspace_size": (c_size_t, [c_int, c_int, c_int, c_int]),
+    "pcnn_gemm_workspace_size": (c_size_t, [c_int, c_int, c_int, c_int, c_int]),
     "pcnn_gemm": (c_int, [c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p,
                           c_int, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_size_t,
                           c_void_p]),

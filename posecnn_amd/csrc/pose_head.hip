@@ -336,10 +336,12 @@ __global__ void __launch_bounds__(256) k_head_bwd(const float* __restrict__ dpre
 
 }  // namespace
 
-extern "C" size_t pcnn_gemm_workspace_size(int M, int N, int K, int precision) {
-  (void)K;
+extern "C" size_t pcnn_gemm_workspace_size(int M, int N, int K, int m_dynamic, int precision) {
   (void)precision;
-  return pcnn::align_up((size_t)kMaxSplit * (M > 0 ? M : 1) * (N > 0 ? N : 1) * sizeof(float), 256) + 256;
+  if (M <= 0 || N <= 0) return 256;
+  // split-K partial slabs; the split only grows when the device-side M shrinks
+  const int s = split_for(m_dynamic ? 1 : M, N, K);
+  return s > 1 ? pcnn::align_up((size_t)s * M * N * sizeof(float), 256) + 256 : 256;
 }
 
 extern "C" int pcnn_gemm(int M, int N, int K, const float* A, const float* A2, int lda, int a_trans, const float* B,
@@ -352,7 +354,8 @@ extern "C" int pcnn_gemm(int M, int N, int K, const float* A, const float* A2, i
   PCNN_REQUIRE(!mask || ldm >= N);
   PCNN_REQUIRE(act == 0 || act == 1);
   if (M == 0) return PCNN_OK;
-  if (workspace_bytes < pcnn_gemm_workspace_size(M, N, K, precision) || !workspace) return PCNN_ECAPACITY;
+  if (workspace_bytes < pcnn_gemm_workspace_size(M, N, K, M_dev != nullptr, precision) || !workspace)
+    return PCNN_ECAPACITY;
   GemmArgs g{M, N, K, A, A2, lda, B, ldb, Cm, ldc, bias, act, mask, ldm, M_dev, K_dev, (float*)workspace};
   hipStream_t st = (hipStream_t)stream;
   const int mt = (M + BM - 1) / BM, nt = (N + BN - 1) / BN;

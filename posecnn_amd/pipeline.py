@@ -1,0 +1,179 @@
+"""The hot path as one sync-free step (vgg16_convs.py:167-200 + the backward
+TF derives for it): hough_voting_gpu -> roi_pool(conv5_3, 1/16) +
+roi_pool(conv4_3, 1/8) -> fc6/fc7/fc8 -> tanh * poses_weight -> l2_normalize
+-> average_distance_loss(margin 0.01), then backward through the loss, the
+pose head and both RoI pools (the Hough op's gradient is identically zero,
+hough_voting_gpu_op.cc:440-484, and is not materialised).
+
+Every buffer is capacity-sized (MAX_ROI * 9 = 1152 RoI rows) and every kernel
+reads the RoI row count from the device, so a step issues no host sync and can
+be captured in a HIP graph.
+
+Image sharding (one process per GPU): rank r votes on images
+[r*B, (r+1)*B) with index_size = MAX_ROI / global_batch and the batch column
+rebased to the global image index; the detected RoI boxes + initial poses
+and the row counts are all-gathered over RCCL (torch.distributed "nccl"),
+the ADD-loss normaliser is the global row count (so per-rank losses sum to
+the single-device loss) and the loss scalar is all-reduced.
+"""
+import torch
+
+from . import _lib
+from . import pose_head as ph
+from .hough_voting_gpu_layer import hough_voting_gpu_op as hv
+from .roi_pooling_layer import roi_pooling_op as rp
+from .average_distance_loss import average_distance_loss_op as adl
+
+CAP = hv.CAPACITY
+
+
+class PoseStep:
+    def __init__(self, B, H, W, num_classes, device, conv4_hw=None, conv5_hw=None, channels=512, units=4096,
+                 is_train=1, skip_pixels=10, vote_threshold=-1.0, vote_percentage=0.02, margin=0.01,
+                 global_batch=None, batch_base=0, weights=None, dist=None, backward=True):
+        self.B, self.H, self.W, self.C = B, H, W, num_classes
+        self.dev = device
+        self.is_train, self.skip, self.vthr, self.vper, self.margin = is_train, skip_pixels, vote_threshold, \
+            vote_percentage, margin
+        self.global_batch = global_batch or B
+        self.batch_base = batch_base
+        self.dist = dist  # torch.distributed module (initialised) or None
+        self.backward = backward
+        self.h4, self.w4 = conv4_hw or (H // 8, W // 8)
+        self.h5, self.w5 = conv5_hw or (H // 16, W // 16)
+        self.Ch = channels
+        D = 4 * num_classes
+        self.D = D
+        self.weights = weights or ph.PoseHeadWeights(num_classes, device, in_dim=49 * channels, units=units)
+        f32 = dict(dtype=torch.float32, device=device)
+        i32 = dict(dtype=torch.int32, device=device)
+        K6 = 49 * channels
+        self.hough = dict(box=torch.zeros((CAP, 7), **f32), pose=torch.zeros((CAP, 7), **f32),
+                          target=torch.zeros((CAP, D), **f32), weight=torch.zeros((CAP, D), **f32),
+                          domain=torch.zeros((CAP,), **i32), num_rois=torch.zeros((2,), **i32))
+        self.pool5 = torch.zeros((CAP, 7, 7, channels), **f32)
+        self.arg5 = torch.zeros((CAP, 7, 7, channels), **i32)
+        self.pool4 = torch.zeros((CAP, 7, 7, channels), **f32)
+        self.arg4 = torch.zeros((CAP, 7, 7, channels), **i32)
+        self.y6 = torch.zeros((CAP, units), **f32)
+        self.y7 = torch.zeros((CAP, units), **f32)
+        self.y8 = torch.zeros((CAP, D), **f32)
+        self.t8 = torch.zeros((CAP, D), **f32)
+        self.pred = torch.zeros((CAP, D), **f32)
+        self.loss = torch.zeros((1,), **f32)
+        self.diff = torch.zeros((CAP, D), **f32)
+        self.one = torch.ones((1,), **f32)
+        self.dpred = torch.zeros((CAP, D), **f32)
+        self.dy8 = torch.zeros((CAP, D), **f32)
+        self.dy7 = torch.zeros((CAP, units), **f32)
+        self.dy6 = torch.zeros((CAP, units), **f32)
+        self.dx = torch.zeros((CAP, K6), **f32)
+        self.grads = self.weights.grads_like()
+        self.dconv4 = torch.zeros((B, self.h4, self.w4, channels), **f32)
+        self.dconv5 = torch.zeros((B, self.h5, self.w5, channels), **f32)
+        self.norm_rows = torch.zeros((1,), **i32)
+        self.timer = None  # optional {name: [(start_event, end_event), ...]} (bench.py)
+        if dist is not None:
+            ws = dist.get_world_size()
+            self.g_counts = torch.zeros((ws * 2,), **i32)
+            self.g_rows = torch.zeros((ws * CAP, 14), **f32)
+            self.l_rows = torch.zeros((CAP, 14), **f32)
+
+    # ------------------------------------------------------------------
+    def _t(self, name):
+        """HIP-event bracket on the current stream (no-op unless self.timer is set)."""
+        step = self
+
+        class _Ctx:
+            def __enter__(self_):
+                if step.timer is not None:
+                    self_.e0 = torch.cuda.Event(enable_timing=True)
+                    self_.e0.record()
+
+            def __exit__(self_, *a):
+                if step.timer is not None:
+                    e1 = torch.cuda.Event(enable_timing=True)
+                    e1.record()
+                    step.timer.setdefault(name, []).append((self_.e0, e1))
+        return _Ctx()
+
+    def vote(self, label, vertex, extents, meta, gt):
+        with self._t("hough_voting_gpu"):
+            return hv.hough_voting_gpu_capacity(label, vertex, extents, meta, gt, self.is_train, self.vthr,
+                                                self.vper, self.skip, global_batch=self.global_batch,
+                                                batch_base=self.batch_base, out=self.hough)
+
+    def exchange(self):
+        """RCCL all-gather of the detected RoIs + initial poses and row counts;
+        global loss normaliser = max(sum of per-rank rows, 1)."""
+        h = self.hough
+        if self.dist is None:
+            self.norm_rows.copy_(h["num_rois"][1:2])
+            return
+        d = self.dist
+        with self._t("allgather_rois"):
+            self.l_rows[:, :7].copy_(h["box"])
+            self.l_rows[:, 7:].copy_(h["pose"])
+            d.all_gather_into_tensor(self.g_counts, h["num_rois"])
+            d.all_gather_into_tensor(self.g_rows, self.l_rows)
+            tot = self.g_counts.view(-1, 2)[:, 0].sum(dtype=torch.int32).clamp_(min=1)
+            self.norm_rows.copy_(tot.view(1))
+
+    def forward(self, conv4, conv5, points, symmetry):
+        h = self.hough
+        nr = h["num_rois"][1:2]  # output row count (incl. dummy row)
+        w = self.weights
+        K6 = 49 * self.Ch
+        with self._t("roi_pool_fwd"):
+            rp.roi_pool(conv5, h["box"], 7, 7, 1.0 / 16.0, 0, num_rois=nr, out=(self.pool5, self.arg5))
+            rp.roi_pool(conv4, h["box"], 7, 7, 1.0 / 8.0, 0, num_rois=nr, out=(self.pool4, self.arg4))
+        x5 = self.pool5.view(CAP, K6)
+        x4 = self.pool4.view(CAP, K6)
+        with self._t("gemm_fc6_fwd"):
+            ph.gemm(x5, w.w6, self.y6, A2=x4, bias=w.b6, act=1, M_dev=nr)
+        with self._t("gemm_fc7_fc8_fwd"):
+            ph.gemm(self.y6, w.w7, self.y7, bias=w.b7, act=1, M_dev=nr)
+            ph.gemm(self.y7, w.w8, self.y8, bias=w.b8, act=0, M_dev=nr)
+        with self._t("head_add_loss_fwd"):
+            ph.head_fwd(self.y8, h["weight"], self.t8, self.pred, num_rois=nr)
+            adl.average_distance_loss(self.pred, h["target"], h["weight"], points, symmetry, self.margin,
+                                      num_rois=nr, loss_norm_rows_dev=self.norm_rows, out=(self.loss, self.diff))
+        if self.dist is not None:
+            with self._t("allreduce_loss"):
+                self.dist.all_reduce(self.loss)
+        return self.loss
+
+    def backward_pass(self, conv4, conv5):
+        h = self.hough
+        nr = h["num_rois"][1:2]
+        w, g = self.weights, self.grads
+        K6 = 49 * self.Ch
+        with self._t("add_loss_head_bwd"):
+            adl.average_distance_loss_grad(self.diff, self.one, num_rois=nr, out=self.dpred)
+            ph.head_bwd(self.dpred, self.t8, h["weight"], self.pred, self.dy8, num_rois=nr)
+        with self._t("gemm_fc8_fc7_bwd"):
+            ph.gemm(self.y7, self.dy8, g["w8"], a_trans=1, K_dev=nr, M=w.units, N=self.D, K=CAP)
+            ph.colsum(self.dy8, g["b8"], M_dev=nr)
+            ph.gemm(self.dy8, w.w8, self.dy7, b_trans=1, mask=self.y7, M_dev=nr)
+            ph.gemm(self.y6, self.dy7, g["w7"], a_trans=1, K_dev=nr, M=w.units, N=w.units, K=CAP)
+            ph.colsum(self.dy7, g["b7"], M_dev=nr)
+            ph.gemm(self.dy7, w.w7, self.dy6, b_trans=1, mask=self.y6, M_dev=nr)
+        x5 = self.pool5.view(CAP, K6)
+        x4 = self.pool4.view(CAP, K6)
+        with self._t("gemm_fc6_dw"):  # A = pool5 + pool4, fused
+            ph.gemm(x5, self.dy6, g["w6"], a_trans=1, A2=x4, K_dev=nr, M=K6, N=w.units, K=CAP)
+            ph.colsum(self.dy6, g["b6"], M_dev=nr)
+        with self._t("gemm_fc6_dx"):
+            ph.gemm(self.dy6, w.w6, self.dx, b_trans=1, M_dev=nr)
+        dxp = self.dx.view(CAP, 7, 7, self.Ch)
+        with self._t("roi_pool_bwd"):  # both pools receive d(pool5 + pool4) = dx
+            rp.roi_pool_grad(conv5, h["box"], self.arg5, dxp, 7, 7, 1.0 / 16.0, 0, num_rois=nr, out=self.dconv5)
+            rp.roi_pool_grad(conv4, h["box"], self.arg4, dxp, 7, 7, 1.0 / 8.0, 0, num_rois=nr, out=self.dconv4)
+
+    def step(self, inputs):
+        self.vote(inputs["label"], inputs["vertex"], inputs["extents"], inputs["meta"], inputs["gt"])
+        self.exchange()
+        loss = self.forward(inputs["conv4"], inputs["conv5"], inputs["points"], inputs["symmetry"])
+        if self.backward:
+            self.backward_pass(inputs["conv4"], inputs["conv5"])
+        return loss
