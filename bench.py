@@ -25,6 +25,7 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md, chip parameters)
 FP32_MFMA_PEAK_TFS = 157.3   # MI355X f32-input MFMA dense peak (same guide)
+BF16_MFMA_PEAK_TFS = 2500.0  # MI355X bf16 MFMA dense peak (same guide; no sparsity)
 
 
 def parse():
@@ -37,7 +38,9 @@ def parse():
     p.add_argument("--classes", type=int, default=22)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (bounded sample)")
-    p.add_argument("--breakdown", action="store_true", help="per-op event breakdown to stderr")
+    p.add_argument("--no-graph", action="store_true", help="time eager launches instead of a HIP graph")
+    p.add_argument("--precision", type=int, choices=[0, 1], default=1,
+                   help="FC GEMMs: 1 = split-bf16 x3 MFMA (fp32-class), 0 = fp32 MFMA")
     return p.parse_args()
 
 
@@ -85,7 +88,7 @@ def main():
 
     if full:
         step = PoseStep(B, H, W, C, dev, is_train=1, skip_pixels=10, global_batch=gB, batch_base=rank * B,
-                        dist=dist)
+                        dist=dist, precision=args.precision)
         run = lambda: step.step(inputs)
     else:
         hout = {}
@@ -111,15 +114,50 @@ def main():
     for _ in range(args.warmup):
         run()
     barrier()
-    if step is not None and (args.breakdown or True):
+
+    # (1) per-op breakdown: eager steps with HIP events around every op on the
+    # stream the kernels run on (feeds the roofline objects)
+    ops = {}
+    if step is not None:
         step.timer = {}
+        nb = max(3, min(args.steps, 10))
+        for _ in range(nb):
+            run()
+        barrier()
+        for k, evs in step.timer.items():
+            ops[k] = sum(a.elapsed_time(b) for a, b in evs) / nb
+        step.timer = None
+
+    # (2) timed region: K steps, HIP-graph replay on one GPU (no host launch
+    # cost), eager with RCCL collectives on N > 1
+    mode = "eager"
+    timed = run
+    if world == 1 and not args.no_graph:
+        try:
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                run()
+            torch.cuda.current_stream().wait_stream(s)
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                run()
+            graph.replay()
+            torch.cuda.synchronize()
+            timed = graph.replay
+            mode = "hipgraph"
+        except Exception as e:  # pragma: no cover - report and time eagerly
+            log(f"graph capture failed ({e}); timing eager launches")
+            torch.cuda.synchronize()
+    for _ in range(2):
+        timed()
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
     barrier()
     w0 = time.perf_counter()
     ev0.record()
     for _ in range(args.steps):
-        run()
+        timed()
     ev1.record()
     barrier()
     wall = time.perf_counter() - w0
@@ -130,13 +168,6 @@ def main():
         elapsed = float(t.item())
     frames = gB * args.steps
     value = frames / elapsed
-
-    # per-op event times (ms per step)
-    ops = {}
-    if step is not None and step.timer:
-        for k, evs in step.timer.items():
-            ops[k] = sum(a.elapsed_time(b) for a, b in evs) / args.steps
-        step.timer = None
     nrows = int((step.hough if step else hout["o"])["num_rois"][0].item())
 
     # roofline objects
@@ -157,9 +188,13 @@ def main():
         gem = {"gemm_fc6_fwd": 2.0 * R * K6 * U, "gemm_fc6_dx": 2.0 * R * K6 * U, "gemm_fc6_dw": 2.0 * R * K6 * U}
         dom = max(gem, key=lambda k: ops.get(k, 0.0))
         tf = gem[dom] / (ops[dom] / 1e3) / 1e12
-        roof = {"bound": "mfma", "achieved": round(tf, 2), "peak": FP32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
-                "frac": round(tf / FP32_MFMA_PEAK_TFS, 4), "traffic": None,
-                "kernel": f"k_gemm_f32 ({dom}, fp32 MFMA 32x32x2, R={R})", "flops_per_launch": gem[dom]}
+        if args.precision == 1:
+            # algorithmic fp32 flops against the rate of the 3 bf16 MFMA passes that produce them
+            peak, kname = BF16_MFMA_PEAK_TFS / 3, f"k_gemm_b3 ({dom}, split-bf16 x3 MFMA 32x32x16, R={R})"
+        else:
+            peak, kname = FP32_MFMA_PEAK_TFS, f"k_gemm_f32 ({dom}, fp32 MFMA 32x32x2, R={R})"
+        roof = {"bound": "mfma", "achieved": round(tf, 2), "peak": round(peak, 1), "unit": "TFLOP/s",
+                "frac": round(tf / peak, 4), "traffic": None, "kernel": kname, "flops_per_launch": gem[dom]}
     else:
         roof = roof_vote
     pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -177,8 +212,8 @@ def main():
         cpu = cpu_baseline(fr, full, args.cpu_seconds)
 
     if rank == 0:
-        if args.breakdown or True:
-            log("per-op ms/step: " + json.dumps({k: round(v, 4) for k, v in sorted(ops.items(), key=lambda x: -x[1])}))
+        if True:
+            log(f"timed mode: {mode}; per-op ms/step (eager breakdown pass): " + json.dumps({k: round(v, 4) for k, v in sorted(ops.items(), key=lambda x: -x[1])}))
             log(f"RoI rows per step (rank 0): {nrows}")
         out = {
             "metric": "frames/sec 640x480x21-class Hough-vote+RoI+ADD-loss, 1/2/4/8 MI355X",
@@ -200,11 +235,13 @@ def main():
                              "configs[1]: hough_voting_gpu(test) + roi_pool x2 forward"),
                 "global_batch": gB, "per_rank_batch": B, "height": H, "width": W, "num_classes": C,
                 "skip_pixels": 10, "index_size": 128 // gB, "roi_rows_rank0": nrows,
+                "fc_gemm": "split-bf16x3 MFMA, fp32 accumulate" if args.precision == 1 else "fp32 MFMA",
                 "parallelism": f"image-shard x{world} (RCCL all-gather of RoIs/poses)" if world > 1 else "single",
             },
             "roofline": roof,
             "roofline_vote": roof_vote,
             "ops_ms_per_step": {k: round(v, 4) for k, v in ops.items()},
+            "timing": mode,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

@@ -6,7 +6,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libposecnn_hip.so")
-SOURCES = ["capi.hip", "hough_voting.hip", "roi_pooling.hip", "average_distance.hip", "backprojecting.hip",
+SOURCES = ["capi.hip", "hough_compact.hip", "hough_vote.hip", "hough_peak.hip", "hough_emit.hip", "roi_pooling.hip", "average_distance.hip", "backprojecting.hip",
            "pose_head.hip"]
 # -ffp-contract=off: the parity arithmetic rounds every float op separately
 # (reference semantics restated by oracle/); MFMA kernels are unaffected.
@@ -18,7 +18,7 @@ def needs_build():
     if not os.path.exists(OUT):
         return True
     t = os.path.getmtime(OUT)
-    deps = [os.path.join(CSRC, s) for s in SOURCES] + [os.path.join(CSRC, "pcnn_common.h"),
+    deps = [os.path.join(CSRC, s) for s in SOURCES] + [os.path.join(CSRC, "pcnn_common.h"), os.path.join(CSRC, "hough_common.h"),
                                                       os.path.join(HERE, "..", "include", "posecnn_hip.h")]
     return any(os.path.getmtime(d) > t for d in deps)
 

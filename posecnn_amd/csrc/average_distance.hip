@@ -5,22 +5,29 @@
 //
 // The reference runs one thread per (row, point), re-deriving the row's six
 // 3x3 matrices per point into a (R, P, 54) global scratch and the per-point
-// gradient into a (R, P, 4C) scratch (~0.64 GB at R = 432), then sums both
-// sequentially per row and reduces the row losses with thrust + a host copy.
-// Here a workgroup owns (row, chunk of 256 points): the matrices are computed
-// once in registers, symmetric classes stage the GT-rotated model points in
-// LDS for the O(P) nearest-point search, and the per-point loss and the four
-// gradient terms are reduced in a fixed tree -> (R, chunks, 5) partials.
-// A single workgroup then folds the partials per row and the rows into the
-// scalar loss, both in fixed order (deterministic; the reference's sequential
-// sums are reproduced to fp32 rounding, tolerance 1e-4 relative).
+// gradient into a (R, P, 4C) scratch (~0.64 GB at R = 432), sums both
+// sequentially per row, and reduces the row losses with thrust + a host copy.
+//
+// Here a workgroup owns (row, chunk of kPts points) with kSplit lanes per
+// point: the matrices live in registers; for symmetric classes the
+// GT-rotated model points are staged once per workgroup in LDS (float4) and
+// each point's nearest-point scan (cu.cc:150-172) is split over kSplit lanes
+// and merged as a lexicographic (distance, index) minimum — exactly the
+// reference's first minimum.  Per-point loss and the four gradient terms use
+// the reference's expressions and operation order (cu.cc:174-203) and are
+// reduced in a fixed tree -> (R, chunks, 5) partials; one workgroup folds the
+// partials per row and the rows into the scalar loss, in fixed order
+// (deterministic; fp32 sums agree with the reference's sequential sums to
+// ~1e-6 relative).
 #include "pcnn_common.h"
 #include <cfloat>
 
 namespace {
 
 constexpr int kAddThreads = 256;
-constexpr int kMaxPointsLds = 4096;
+constexpr int kSplit = 4;                      // lanes per point (symmetric search split)
+constexpr int kPts = kAddThreads / kSplit;     // points per workgroup
+constexpr int kMaxPointsLds = 8192;            // float4 candidates in LDS (128 KB)
 
 __device__ __forceinline__ int rows_of(const int32_t* dev, int cap) {
   if (!dev) return cap;
@@ -41,6 +48,13 @@ __device__ __forceinline__ void quat2rot(float s, float u, float v, float w, flo
   r[8] = s * s - u * u - v * v + w * w;
 }
 
+__device__ __forceinline__ int row_class(const float* __restrict__ weight, int n, int C) {
+  const int PC = 4 * C;
+  for (int i = 0; i < C; i++)  // first class with weight > 0 (cu.cc:47-52)
+    if (weight[(size_t)n * PC + 4 * i] > 0) return i;
+  return -1;
+}
+
 __global__ void __launch_bounds__(kAddThreads) k_add_rows(const float* __restrict__ pred,
                                                            const float* __restrict__ target,
                                                            const float* __restrict__ weight,
@@ -49,73 +63,77 @@ __global__ void __launch_bounds__(kAddThreads) k_add_rows(const float* __restric
                                                            const int32_t* __restrict__ num_rois_dev, int C, int P,
                                                            float margin, int norm_rows,
                                                            const int32_t* __restrict__ norm_rows_dev, int nchunk,
+                                                           const int32_t* __restrict__ rcls,
                                                            float* __restrict__ partial) {
-  __shared__ float gpts[kMaxPointsLds * 3];
+  extern __shared__ __attribute__((aligned(16))) float4 gpts[];  // [P] GT-rotated points (symmetric rows)
   __shared__ float red[kAddThreads / 64][5];
   const int n = blockIdx.y, chunk = blockIdx.x;
   const int R = rows_of(num_rois_dev, R_cap);
   if (n >= R) return;
   const int PC = 4 * C;
-  int cls = -1;
-  for (int i = 0; i < C; i++)  // first class with weight > 0 (cu.cc:47-52)
-    if (weight[(size_t)n * PC + 4 * i] > 0) { cls = i; break; }
+  const int cls = rcls[n];
+  if (cls < 0 || !(symmetry[cls] > 0)) return;  // k_add_rows_plain handles these rows
   float* out = partial + ((size_t)n * nchunk + chunk) * 5;
-  if (cls < 0) {
-    if (threadIdx.x < 5) out[threadIdx.x] = 0.f;
-    return;
-  }
   const float* tq = target + (size_t)n * PC + 4 * cls;
   const float* pq = pred + (size_t)n * PC + 4 * cls;
   float Rg[9], Rp[9];
   quat2rot(tq[0], tq[1], tq[2], tq[3], Rg);
   const float s = pq[0], u = pq[1], v = pq[2], w = pq[3];
   quat2rot(s, u, v, w, Rp);
-  // derivative matrices of Rp w.r.t. (s, u, v, w) (cu.cc:97-139)
-  const float d0[9] = {2 * s, -2 * w, 2 * v, 2 * w, 2 * s, -2 * u, -2 * v, 2 * u, 2 * s};
-  const float d1[9] = {2 * u, 2 * v, 2 * w, 2 * v, -2 * u, -2 * s, 2 * w, 2 * s, -2 * u};
-  const float d2[9] = {-2 * v, 2 * u, 2 * s, 2 * u, 2 * v, 2 * w, -2 * s, 2 * w, -2 * v};
-  const float d3[9] = {-2 * w, -2 * s, 2 * u, 2 * s, -2 * w, 2 * v, 2 * u, 2 * v, 2 * w};
   const float* pts = points + (size_t)cls * P * 3;
   const bool sym = symmetry[cls] > 0;
   if (sym) {
     for (int i = threadIdx.x; i < P; i += blockDim.x) {
       const float X0 = pts[i * 3 + 0], X1 = pts[i * 3 + 1], X2 = pts[i * 3 + 2];
-      gpts[i * 3 + 0] = Rg[0] * X0 + Rg[1] * X1 + Rg[2] * X2;
-      gpts[i * 3 + 1] = Rg[3] * X0 + Rg[4] * X1 + Rg[5] * X2;
-      gpts[i * 3 + 2] = Rg[6] * X0 + Rg[7] * X1 + Rg[8] * X2;
+      gpts[i] = make_float4(Rg[0] * X0 + Rg[1] * X1 + Rg[2] * X2, Rg[3] * X0 + Rg[4] * X1 + Rg[5] * X2,
+                            Rg[6] * X0 + Rg[7] * X1 + Rg[8] * X2, 0.f);
     }
     __syncthreads();
   }
-  const int Rn = norm_rows_dev ? *norm_rows_dev : (norm_rows > 0 ? norm_rows : R);
-  const float bn = (float)(Rn * P);
-  const double ln = 2.0 * (double)Rn * (double)P;
-  float acc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
-  const int p = chunk * blockDim.x + threadIdx.x;
-  if (p < P) {
-    const float X0 = pts[p * 3 + 0], X1 = pts[p * 3 + 1], X2 = pts[p * 3 + 2];
-    const float x1 = Rp[0] * X0 + Rp[1] * X1 + Rp[2] * X2;
-    const float y1 = Rp[3] * X0 + Rp[4] * X1 + Rp[5] * X2;
-    const float z1 = Rp[6] * X0 + Rp[7] * X1 + Rp[8] * X2;
-    float x2, y2, z2;
-    if (sym) {  // closest GT-rotated point, first minimum (cu.cc:150-168)
-      float dmin = FLT_MAX;
-      int imin = p;
-      for (int i = 0; i < P; i++) {
-        const float ax = gpts[i * 3 + 0], ay = gpts[i * 3 + 1], az = gpts[i * 3 + 2];
-        const float dist = (x1 - ax) * (x1 - ax) + (y1 - ay) * (y1 - ay) + (z1 - az) * (z1 - az);
-        if (dist < dmin) { dmin = dist; imin = i; }
-      }
-      x2 = gpts[imin * 3 + 0];
-      y2 = gpts[imin * 3 + 1];
-      z2 = gpts[imin * 3 + 2];
-    } else {
-      x2 = Rg[0] * X0 + Rg[1] * X1 + Rg[2] * X2;
-      y2 = Rg[3] * X0 + Rg[4] * X1 + Rg[5] * X2;
-      z2 = Rg[6] * X0 + Rg[7] * X1 + Rg[8] * X2;
+  const int sub = threadIdx.x & (kSplit - 1);
+  const int p = chunk * kPts + (threadIdx.x / kSplit);
+  const bool live = p < P;
+  const int pp = live ? p : 0;
+  const float X0 = pts[pp * 3 + 0], X1 = pts[pp * 3 + 1], X2 = pts[pp * 3 + 2];
+  const float x1 = Rp[0] * X0 + Rp[1] * X1 + Rp[2] * X2;
+  const float y1 = Rp[3] * X0 + Rp[4] * X1 + Rp[5] * X2;
+  const float z1 = Rp[6] * X0 + Rp[7] * X1 + Rp[8] * X2;
+  float x2, y2, z2;
+  if (sym) {
+    float dmin = FLT_MAX;
+    int imin = 0x7fffffff;
+    for (int i = sub; i < P; i += kSplit) {
+      const float4 a = gpts[i];
+      const float dist = (x1 - a.x) * (x1 - a.x) + (y1 - a.y) * (y1 - a.y) + (z1 - a.z) * (z1 - a.z);
+      if (dist < dmin) { dmin = dist; imin = i; }  // first minimum within this lane's stride
     }
+#pragma unroll
+    for (int o = 1; o < kSplit; o <<= 1) {  // lexicographic (dist, index) min over the point's lanes
+      const float od = __shfl_xor(dmin, o, 64);
+      const int oi = __shfl_xor(imin, o, 64);
+      if (od < dmin || (od == dmin && oi < imin)) { dmin = od; imin = oi; }
+    }
+    if (imin == 0x7fffffff) imin = pp;  // no finite distance (reference leaves index_min unset)
+    const float4 a = gpts[imin];
+    x2 = a.x; y2 = a.y; z2 = a.z;
+  } else {
+    x2 = Rg[0] * X0 + Rg[1] * X1 + Rg[2] * X2;
+    y2 = Rg[3] * X0 + Rg[4] * X1 + Rg[5] * X2;
+    z2 = Rg[6] * X0 + Rg[7] * X1 + Rg[8] * X2;
+  }
+  float acc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+  if (live && sub == 0) {
+    const int Rn = norm_rows_dev ? *norm_rows_dev : (norm_rows > 0 ? norm_rows : R);
+    const float bn = (float)(Rn * P);
+    const double ln = 2.0 * (double)Rn * (double)P;
     const float dist = (x1 - x2) * (x1 - x2) + (y1 - y2) * (y1 - y2) + (z1 - z2) * (z1 - z2);
     if (!(dist < margin)) {  // cu.cc:178-179
-      acc[0] = (float)((double)(dist - margin) / ln);
+      acc[0] = (float)((double)(dist - margin) / ln);  // cu.cc:181
+      // derivative matrices of Rp w.r.t. (s, u, v, w) (cu.cc:97-139)
+      const float d0[9] = {2 * s, -2 * w, 2 * v, 2 * w, 2 * s, -2 * u, -2 * v, 2 * u, 2 * s};
+      const float d1[9] = {2 * u, 2 * v, 2 * w, 2 * v, -2 * u, -2 * s, 2 * w, 2 * s, -2 * u};
+      const float d2[9] = {-2 * v, 2 * u, 2 * s, 2 * u, 2 * v, 2 * w, -2 * s, 2 * w, -2 * v};
+      const float d3[9] = {-2 * w, -2 * s, 2 * u, 2 * s, -2 * w, 2 * v, 2 * u, 2 * v, 2 * w};
       const float X[3] = {X0, X1, X2};
       const float df[3] = {x1 - x2, y1 - y2, z1 - z2};
 #pragma unroll
@@ -142,28 +160,119 @@ __global__ void __launch_bounds__(kAddThreads) k_add_rows(const float* __restric
   }
 }
 
-// One workgroup: per-row fold of the chunk partials, bottom_diff rows, loss.
-__global__ void __launch_bounds__(1024) k_add_finish(const float* __restrict__ weight, int R_cap,
-                                                      const int32_t* __restrict__ num_rois_dev, int C, int nchunk,
-                                                      const float* __restrict__ partial, float* __restrict__ loss,
-                                                      float* __restrict__ bottom_diff) {
+// Row classes once (first class with weight > 0, cu.cc:47-52).
+__global__ void k_add_prep(const float* __restrict__ weight, int R_cap, const int32_t* __restrict__ num_rois_dev,
+                           int C, int32_t* __restrict__ rcls) {
+  const int R = rows_of(num_rois_dev, R_cap);
+  for (int n = blockIdx.x * blockDim.x + threadIdx.x; n < R; n += gridDim.x * blockDim.x) rcls[n] = row_class(weight, n, C);
+}
+
+// Non-symmetric rows (and rows without weight): one workgroup per row, points
+// strided over the threads; the per-point arithmetic is k_add_rows' (cu.cc:140-203).
+__global__ void __launch_bounds__(kAddThreads) k_add_rows_plain(const float* __restrict__ pred,
+                                                                 const float* __restrict__ target,
+                                                                 const float* __restrict__ points,
+                                                                 const float* __restrict__ symmetry, int R_cap,
+                                                                 const int32_t* __restrict__ num_rois_dev, int C,
+                                                                 int P, float margin, int norm_rows,
+                                                                 const int32_t* __restrict__ norm_rows_dev,
+                                                                 int nchunk, const int32_t* __restrict__ rcls,
+                                                                 float* __restrict__ partial) {
+  __shared__ float red[kAddThreads / 64][5];
+  const int n = blockIdx.x;
+  const int R = rows_of(num_rois_dev, R_cap);
+  if (n >= R) return;
+  const int cls = rcls[n];
+  if (cls >= 0 && symmetry[cls] > 0) return;  // k_add_rows handles symmetric rows
+  float* out = partial + (size_t)n * nchunk * 5;
+  for (int i = threadIdx.x; i < nchunk * 5; i += blockDim.x) out[i] = 0.f;
+  if (cls < 0) return;
+  const int PC = 4 * C;
+  const float* tq = target + (size_t)n * PC + 4 * cls;
+  const float* pq = pred + (size_t)n * PC + 4 * cls;
+  float Rg[9], Rp[9];
+  quat2rot(tq[0], tq[1], tq[2], tq[3], Rg);
+  const float s = pq[0], u = pq[1], v = pq[2], w = pq[3];
+  quat2rot(s, u, v, w, Rp);
+  const float d0[9] = {2 * s, -2 * w, 2 * v, 2 * w, 2 * s, -2 * u, -2 * v, 2 * u, 2 * s};
+  const float d1[9] = {2 * u, 2 * v, 2 * w, 2 * v, -2 * u, -2 * s, 2 * w, 2 * s, -2 * u};
+  const float d2[9] = {-2 * v, 2 * u, 2 * s, 2 * u, 2 * v, 2 * w, -2 * s, 2 * w, -2 * v};
+  const float d3[9] = {-2 * w, -2 * s, 2 * u, 2 * s, -2 * w, 2 * v, 2 * u, 2 * v, 2 * w};
+  const int Rn = norm_rows_dev ? *norm_rows_dev : (norm_rows > 0 ? norm_rows : R);
+  const float bn = (float)(Rn * P);
+  const double ln = 2.0 * (double)Rn * (double)P;
+  const float* pts = points + (size_t)cls * P * 3;
+  float acc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int p = threadIdx.x; p < P; p += blockDim.x) {
+    const float X0 = pts[p * 3 + 0], X1 = pts[p * 3 + 1], X2 = pts[p * 3 + 2];
+    const float x1 = Rp[0] * X0 + Rp[1] * X1 + Rp[2] * X2;
+    const float y1 = Rp[3] * X0 + Rp[4] * X1 + Rp[5] * X2;
+    const float z1 = Rp[6] * X0 + Rp[7] * X1 + Rp[8] * X2;
+    const float x2 = Rg[0] * X0 + Rg[1] * X1 + Rg[2] * X2;
+    const float y2 = Rg[3] * X0 + Rg[4] * X1 + Rg[5] * X2;
+    const float z2 = Rg[6] * X0 + Rg[7] * X1 + Rg[8] * X2;
+    const float dist = (x1 - x2) * (x1 - x2) + (y1 - y2) * (y1 - y2) + (z1 - z2) * (z1 - z2);
+    if (dist < margin) continue;
+    acc[0] += (float)((double)(dist - margin) / ln);
+    const float X[3] = {X0, X1, X2};
+    const float df[3] = {x1 - x2, y1 - y2, z1 - z2};
+    float e0 = 0.f, e1 = 0.f, e2 = 0.f, e3 = 0.f;  // this point's terms, reference order
+#pragma unroll
+    for (int j = 0; j < 3; j++)
+#pragma unroll
+      for (int k = 0; k < 3; k++) {
+        e0 += df[j] * X[k] * d0[j * 3 + k] / bn;
+        e1 += df[j] * X[k] * d1[j * 3 + k] / bn;
+        e2 += df[j] * X[k] * d2[j * 3 + k] / bn;
+        e3 += df[j] * X[k] * d3[j * 3 + k] / bn;
+      }
+    acc[1] += e0; acc[2] += e1; acc[3] += e2; acc[4] += e3;
+  }
+#pragma unroll
+  for (int q = 0; q < 5; q++) acc[q] = pcnn::wave_sum(acc[q]);
+  if (pcnn::lane_id() == 0)
+    for (int q = 0; q < 5; q++) red[threadIdx.x >> 6][q] = acc[q];
+  __syncthreads();
+  if (threadIdx.x < 5) {
+    float t = 0.f;
+    for (int i = 0; i < (int)(blockDim.x >> 6); i++) t += red[i][threadIdx.x];
+    out[threadIdx.x] = t;
+  }
+}
+
+// One wave per row: fold the chunk partials (fixed tree), write the row of
+// bottom_diff (zeros except the class's 4 channels) and the row loss.
+__global__ void __launch_bounds__(256) k_add_finish_rows(int R_cap, const int32_t* __restrict__ num_rois_dev, int C,
+                                                          int nchunk, const int32_t* __restrict__ rcls,
+                                                          const float* __restrict__ partial,
+                                                          float* __restrict__ row_loss,
+                                                          float* __restrict__ bottom_diff) {
+  const int R = rows_of(num_rois_dev, R_cap);
+  const int n = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = pcnn::lane_id();
+  if (n >= R) return;
+  const int cls = rcls[n];
+  float s[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int k = lane; k < nchunk; k += 64)
+    for (int q = 0; q < 5; q++) s[q] += partial[((size_t)n * nchunk + k) * 5 + q];
+#pragma unroll
+  for (int q = 0; q < 5; q++) s[q] = pcnn::wave_sum(s[q]);
+  const int PC = 4 * C;
+  for (int col = lane; col < PC; col += 64) {
+    float vv = 0.f;
+    if (cls >= 0 && col >= 4 * cls && col < 4 * cls + 4) vv = s[1 + col - 4 * cls];
+    bottom_diff[(size_t)n * PC + col] = vv;
+  }
+  if (lane == 0) row_loss[n] = cls >= 0 ? s[0] : 0.f;
+}
+
+// Scalar loss: fixed-order sum of the row losses (thrust::reduce, cu.cc:333-334).
+__global__ void __launch_bounds__(1024) k_add_total(int R_cap, const int32_t* __restrict__ num_rois_dev,
+                                                     const float* __restrict__ row_loss, float* __restrict__ loss) {
   __shared__ float red[16];
   const int R = rows_of(num_rois_dev, R_cap);
-  const int PC = 4 * C;
   float my = 0.f;
-  for (int n = threadIdx.x; n < R; n += blockDim.x) {
-    int cls = -1;
-    for (int i = 0; i < C; i++)
-      if (weight[(size_t)n * PC + 4 * i] > 0) { cls = i; break; }
-    float s[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
-    for (int k = 0; k < nchunk; k++)
-      for (int q = 0; q < 5; q++) s[q] += partial[((size_t)n * nchunk + k) * 5 + q];
-    float* bd = bottom_diff + (size_t)n * PC;
-    for (int t = 0; t < PC; t++) bd[t] = 0.f;
-    if (cls >= 0)
-      for (int q = 0; q < 4; q++) bd[4 * cls + q] = s[q + 1];
-    my += cls >= 0 ? s[0] : 0.f;
-  }
+  for (int n = threadIdx.x; n < R; n += blockDim.x) my += row_loss[n];
   my = pcnn::wave_sum(my);
   if (pcnn::lane_id() == 0) red[threadIdx.x >> 6] = my;
   __syncthreads();
@@ -192,8 +301,10 @@ __global__ void k_add_bwd_rows(const float* __restrict__ top_diff, const float* 
 
 extern "C" size_t pcnn_add_loss_workspace_size(int R_cap, int C, int P) {
   (void)C;
-  const int nchunk = (P + kAddThreads - 1) / kAddThreads;
-  return pcnn::align_up((size_t)(R_cap > 0 ? R_cap : 1) * nchunk * 5 * sizeof(float), 256) + 256;
+  const int nchunk = (P + kPts - 1) / kPts;
+  const size_t R = (size_t)(R_cap > 0 ? R_cap : 1);
+  return pcnn::align_up(R * nchunk * 5 * sizeof(float), 256) + pcnn::align_up(R * sizeof(int32_t), 256) +
+         pcnn::align_up(R * sizeof(float), 256) + 256;
 }
 
 extern "C" int pcnn_add_loss_fwd(const float* pred, const float* target, const float* weight, const float* points,
@@ -204,13 +315,20 @@ extern "C" int pcnn_add_loss_fwd(const float* pred, const float* target, const f
   PCNN_REQUIRE(R_cap > 0 && C > 0 && P > 0 && P <= kMaxPointsLds);
   if (workspace_bytes < pcnn_add_loss_workspace_size(R_cap, C, P)) return PCNN_ECAPACITY;
   hipStream_t st = (hipStream_t)stream;
-  const int nchunk = (P + kAddThreads - 1) / kAddThreads;
-  float* partial = (float*)workspace;
-  hipLaunchKernelGGL(k_add_rows, dim3(nchunk, R_cap), dim3(kAddThreads), 0, st, pred, target, weight, points,
-                     symmetry, R_cap, num_rois_dev, C, P, margin, loss_norm_rows, loss_norm_rows_dev, nchunk,
-                     partial);
-  hipLaunchKernelGGL(k_add_finish, dim3(1), dim3(1024), 0, st, weight, R_cap, num_rois_dev, C, nchunk, partial, loss,
-                     bottom_diff);
+  const int nchunk = (P + kPts - 1) / kPts;
+  pcnn::Carve cv(workspace);
+  float* partial = cv.take<float>((size_t)R_cap * nchunk * 5);
+  int32_t* rcls = cv.take<int32_t>(R_cap);
+  float* row_loss = cv.take<float>(R_cap);
+  hipLaunchKernelGGL(k_add_prep, dim3((R_cap + 255) / 256), dim3(256), 0, st, weight, R_cap, num_rois_dev, C, rcls);
+  hipLaunchKernelGGL(k_add_rows_plain, dim3(R_cap), dim3(kAddThreads), 0, st, pred, target, points, symmetry, R_cap,
+                     num_rois_dev, C, P, margin, loss_norm_rows, loss_norm_rows_dev, nchunk, rcls, partial);
+  hipLaunchKernelGGL(k_add_rows, dim3(nchunk, R_cap), dim3(kAddThreads), (size_t)P * sizeof(float4), st, pred,
+                     target, weight, points, symmetry, R_cap, num_rois_dev, C, P, margin, loss_norm_rows,
+                     loss_norm_rows_dev, nchunk, rcls, partial);
+  hipLaunchKernelGGL(k_add_finish_rows, dim3((R_cap + 3) / 4), dim3(256), 0, st, R_cap, num_rois_dev, C, nchunk,
+                     rcls, partial, row_loss, bottom_diff);
+  hipLaunchKernelGGL(k_add_total, dim3(1), dim3(1024), 0, st, R_cap, num_rois_dev, row_loss, loss);
   PCNN_CHECK_LAUNCH();
   return PCNN_OK;
 }

@@ -1,0 +1,214 @@
+// Shared state and reference arithmetic of the Hough-voting op (see
+// hough_emit.hip for the op overview).  Split across translation units:
+//   hough_compact.hip  label histogram / scan / voter compaction
+//   hough_vote.hip     interval vote into LDS difference arrays + argmax key
+//   hough_peak.hip     exact hough_data at maxima, multi-instance NMS
+//   hough_emit.hip     RoI emission + the C-ABI entry points
+#pragma once
+#include "pcnn_common.h"
+#include <math.h>
+
+namespace pcnn_hough {
+
+constexpr int kMaxClasses = 256;
+constexpr int kPixPerBlk = 4096;   // label pixels per compaction block
+constexpr int kCompactThreads = 256;
+constexpr int kBand = 8;           // Hough rows per vote workgroup
+constexpr int kVoteThreads = 256;
+constexpr int kPeakThreads = 256;
+constexpr int kPeakChunk = 4096;   // voters per ordered-sum chunk (LDS floats)
+constexpr int kCandCap = 4096;     // NMS candidates per image
+constexpr int kEmitThreads = 256;
+constexpr double kConeEps = 2e-6;  // margin of the exact-predicate band (in cos)
+
+// per-voter row-bound codes (2 bits per bound, 4 bounds: outer s1, s2, inner s1, s2)
+constexpr int kBoundLower = 0, kBoundUpper = 1, kNeedPosDy = 2, kNeedNegDy = 3;
+constexpr int kSlowVoter = 1 << 16;   // evaluate the exact predicate on every box cell
+constexpr int kDeadVoter = 1 << 17;   // votes for no cell (T <= 0 or NaN)
+
+struct HoughWs {
+  int32_t* blk;       // [B][NBLK][C] per-block class histogram -> exclusive offsets
+  int32_t* total;     // [B][C]
+  int32_t* nslots;    // [B] present classes
+  int32_t* nvote;     // [B] slots voted (default: min(count, index_size)); after NMS: kept maxima
+  int32_t* nvtot;     // [B] voters of the voted slots
+  int32_t* slot_cls;  // [B][C]
+  int32_t* vbase;     // [B][C] voter list offset of class c (image-relative)
+  int32_t* vcount;    // [B][C] voters of class c (0 when not voted)
+  float4* vdat;       // [B][VCAP] (u, v, d, T)
+  int32_t* vpos;      // [B][VCAP] y*W + x
+  double4* vcone;     // [B][VCAP] row-bound slopes (outer s1, s2, inner s1, s2)
+  int32_t* vcode;     // [B][VCAP] bound codes | kSlowVoter | kDeadVoter
+  unsigned long long* key;  // [B][C] argmax key per slot
+  float* peak;        // [B][PKS][8] count, distance, 2bb_h, 2bb_w, cx, cy, slot
+  int32_t* counts;    // [B][C-1][H*W] (NMS path)
+  int32_t* ncand;     // [B]
+  int32_t* cand;      // [B][kCandCap] slot*HW + cell
+  float* cand_data;   // [B][kCandCap][4] count, distance, 2bb_h, 2bb_w
+  int32_t* diag;      // [4]
+  int nblk, vcap, pks;  // pks = peak slots per image = max(C, PCNN_MAX_ROI)
+};
+
+inline HoughWs carve_ws(void* base, int B, int H, int W, int C, int skip, bool nms, size_t* total_bytes) {
+  pcnn::Carve cv(base);
+  HoughWs ws;
+  const long HW = (long)H * W;
+  ws.nblk = (int)((HW + kPixPerBlk - 1) / kPixPerBlk);
+  ws.vcap = (int)((HW + skip - 1) / skip) + C;
+  ws.pks = C > PCNN_MAX_ROI ? C : PCNN_MAX_ROI;
+  ws.diag = cv.take<int32_t>(4);
+  ws.blk = cv.take<int32_t>((size_t)B * ws.nblk * C);
+  ws.total = cv.take<int32_t>((size_t)B * C);
+  ws.nslots = cv.take<int32_t>(B);
+  ws.nvote = cv.take<int32_t>(B);
+  ws.nvtot = cv.take<int32_t>(B);
+  ws.slot_cls = cv.take<int32_t>((size_t)B * C);
+  ws.vbase = cv.take<int32_t>((size_t)B * C);
+  ws.vcount = cv.take<int32_t>((size_t)B * C);
+  ws.vdat = cv.take<float4>((size_t)B * ws.vcap);
+  ws.vpos = cv.take<int32_t>((size_t)B * ws.vcap);
+  ws.vcone = cv.take<double4>((size_t)B * ws.vcap);
+  ws.vcode = cv.take<int32_t>((size_t)B * ws.vcap);
+  ws.key = cv.take<unsigned long long>((size_t)B * C);
+  ws.peak = cv.take<float>((size_t)B * ws.pks * 8);
+  ws.ncand = cv.take<int32_t>(B);
+  if (nms) {
+    ws.counts = cv.take<int32_t>((size_t)B * (C - 1) * HW);
+    ws.cand = cv.take<int32_t>((size_t)B * kCandCap);
+    ws.cand_data = cv.take<float>((size_t)B * kCandCap * 4);
+  } else {
+    ws.counts = nullptr;
+    ws.cand = nullptr;
+    ws.cand_data = nullptr;
+  }
+  if (total_bytes) *total_bytes = cv.off;
+  return ws;
+}
+
+// ---------------------------------------------------------------------------
+// Reference arithmetic (every float op rounded separately, -ffp-contract=off).
+
+// angle_distance(...) > inlierThreshold (cu.cc:32-42, :283)
+__device__ __forceinline__ bool cone_pred(int cx, int cy, int x, int y, float u, float v, float thr) {
+  float dx = (float)(cx - x);
+  float dy = (float)(cy - y);
+  float n1 = sqrtf(u * u + v * v);
+  float n2 = sqrtf(dx * dx + dy * dy);
+  float dot = u * dx + v * dy;
+  return dot / (n1 * n2) > thr;
+}
+
+// project_box (cu.cc:84-120)
+__device__ __forceinline__ float project_box(int cls, const float* __restrict__ extents,
+                                             const float* __restrict__ meta, float distance, float factor) {
+  float xHalf = (float)((double)extents[cls * 3 + 0] * 0.5);
+  float yHalf = (float)((double)extents[cls * 3 + 1] * 0.5);
+  float zHalf = (float)((double)extents[cls * 3 + 2] * 0.5);
+  const float fx = meta[0], fy = meta[4], px = meta[2], py = meta[5];
+  const float zf = zHalf + distance, zb = -zHalf + distance;
+  float minX = 1e8f, maxX = -1e8f, minY = 1e8f, maxY = -1e8f;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const float X = (i & 1) ? -xHalf : xHalf;
+    const float Y = (i & 2) ? -yHalf : yHalf;
+    const float Z = (i & 4) ? zb : zf;
+    float x = fx * (X / Z) + px;
+    float y = fy * (Y / Z) + py;
+    minX = fminf(minX, x);
+    minY = fminf(minY, y);
+    maxX = fmaxf(maxX, x);
+    maxY = fmaxf(maxY, y);
+  }
+  float width = maxX - minX + 1;
+  float height = maxY - minY + 1;
+  return fmaxf(width, height) * factor;
+}
+
+// IoU (cu.cc:73-82)
+__device__ __forceinline__ float iou4(const float* a, const float* b) {
+  float left = fmaxf(a[0], b[0]), right = fminf(a[2], b[2]);
+  float top = fmaxf(a[1], b[1]), bottom = fminf(a[3], b[3]);
+  float width = fmaxf(right - left + 1, 0.f), height = fmaxf(bottom - top + 1, 0.f);
+  float interS = width * height;
+  float Sa = (a[2] - a[0] + 1) * (a[3] - a[1] + 1);
+  float Sb = (b[2] - b[0] + 1) * (b[3] - b[1] + 1);
+  return interS / (Sa + Sb - interS);
+}
+
+// compute_box_overlap (cu.cc:123-172); Eigen Quaternionf::toRotationMatrix,
+// lazy 3x3*3x8 product summed a0 + (a1 + a2).
+__device__ __forceinline__ float box_overlap(int cls, const float* __restrict__ extents,
+                                             const float* __restrict__ meta, const float* __restrict__ pose,
+                                             const float* box) {
+  float xHalf = (float)((double)extents[cls * 3 + 0] * 0.5);
+  float yHalf = (float)((double)extents[cls * 3 + 1] * 0.5);
+  float zHalf = (float)((double)extents[cls * 3 + 2] * 0.5);
+  float qw = pose[6], qx = pose[7], qy = pose[8], qz = pose[9];
+  float tx = 2.f * qx, ty = 2.f * qy, tz = 2.f * qz;
+  float twx = tx * qw, twy = ty * qw, twz = tz * qw;
+  float txx = tx * qx, txy = ty * qx, txz = tz * qx;
+  float tyy = ty * qy, tyz = tz * qy, tzz = tz * qz;
+  float R[9] = {1.f - (tyy + tzz), txy - twz, txz + twy, txy + twz, 1.f - (txx + tzz), tyz - twx,
+                txz - twy, tyz + twx, 1.f - (txx + tyy)};
+  const float fx = meta[0], fy = meta[4], px = meta[2], py = meta[5];
+  float x1 = 1e8f, x2 = -1e8f, y1 = 1e8f, y2 = -1e8f;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const float bx = (i & 1) ? -xHalf : xHalf;
+    const float by = (i & 2) ? -yHalf : yHalf;
+    const float bz = (i & 4) ? -zHalf : zHalf;
+    float X = R[0] * bx + (R[1] * by + R[2] * bz);
+    float Y = R[3] * bx + (R[4] * by + R[5] * bz);
+    float Z = R[6] * bx + (R[7] * by + R[8] * bz);
+    X = X + pose[10];
+    Y = Y + pose[11];
+    Z = Z + pose[12];
+    float x = fx * (X / Z) + px;
+    float y = fy * (Y / Z) + py;
+    x1 = fminf(x1, x);
+    y1 = fminf(y1, y);
+    x2 = fmaxf(x2, x);
+    y2 = fmaxf(y2, y);
+  }
+  float gtb[4] = {x1, y1, x2, y2};
+  return iou4(box, gtb);
+}
+
+// largest integer k with k < T (the box test |dx| < T on integer dx), or -1.
+__device__ __forceinline__ int box_radius(float T) {
+  if (!(T > 0.f)) return -1;
+  if (T > 1.0e7f) return 10000000;
+  return (int)ceilf(T) - 1;
+}
+
+// Wave-aggregated grouping of lanes by label: calls fn(label, mask) once per
+// distinct valid label of the wave (same label in every lane of `mask`).
+template <typename F>
+__device__ __forceinline__ void for_each_label_group(int lab, bool valid, F fn) {
+  uint64_t active = __ballot(valid);
+  while (active) {
+    int leader = __ffsll((long long)active) - 1;
+    int l0 = __shfl(lab, leader, 64);
+    uint64_t m = __ballot(valid && lab == l0);
+    fn(l0, m);
+    active &= ~m;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// kernels (defined in the TUs listed above)
+__global__ void k_label_hist(const int32_t* __restrict__ label, int HW, int C, HoughWs ws);
+__global__ void k_label_scan(int C, int label_thr, int index_size, int nms, int skip, HoughWs ws);
+__global__ void k_label_scatter(const int32_t* __restrict__ label, const float* __restrict__ vertex,
+                                const float* __restrict__ extents, const float* __restrict__ meta, int num_meta,
+                                int H, int W, int C, int skip, HoughWs ws);
+__global__ void k_voter_setup(float inlier, double so, double si, HoughWs ws);
+__global__ void k_hough_vote(int H, int W, int C, float inlier, HoughWs ws, int32_t* __restrict__ counts_out);
+__global__ void k_hough_peak(int H, int W, int C, float inlier, const float* __restrict__ extents,
+                             const float* __restrict__ meta, int num_meta, HoughWs ws);
+__global__ void k_hough_nms_cand(int H, int W, int C, float vote_thr, HoughWs ws);
+__global__ void k_hough_cand_data(int H, int W, int C, float inlier, const float* __restrict__ extents,
+                                  const float* __restrict__ meta, int num_meta, HoughWs ws);
+__global__ void k_hough_nms_select(int H, int W, int C, float per_thr, int index_size, HoughWs ws);
+
+}  // namespace pcnn_hough

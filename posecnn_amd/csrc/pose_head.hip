@@ -42,6 +42,7 @@ struct GemmArgs {
   const int32_t* M_dev;
   const int32_t* K_dev;
   float* slab;  // split-K partials [kMaxSplit][M][N]
+  int prec;     // 0 fp32 MFMA, 1 split-bf16 x3 (selects the split rule)
 };
 
 __device__ __forceinline__ int eff_dim(int full, const int32_t* dev) {
@@ -244,10 +245,275 @@ __global__ void __launch_bounds__(kGemmThreads) k_gemm_f32(GemmArgs g) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// Split-bf16 ("bf16x3") GEMM: x = x_hi + x_lo with x_hi = bf16(x),
+// x_lo = bf16(x - x_hi) (16 significant bits), a*b ~ a_hi b_hi + a_hi b_lo +
+// a_lo b_hi accumulated in fp32 by v_mfma_f32_32x32x16_bf16 — relative error
+// ~1e-5 per product (fp32-class for the 1e-4 quaternion tolerance) at 3/16 of
+// the fp32-MFMA cost.  fp32 operands are split while staging into LDS, so the
+// weights stay fp32 in HBM (no conversion pass).
+//
+// Tile 256 x 256 x 32, 512 threads (8 waves as 2 (M) x 4 (N), 128 x 64 per
+// wave = 4 x 2 accumulators of 32 x 32), one workgroup per CU with two 64 KiB
+// LDS stages: the global loads of step s+2 are in flight (registers) while
+// step s computes and step s+1 sits in LDS.  At 512 flop per staged fp32 byte
+// pair the tile needs ~21 B/clk/CU at the MFMA rate, inside the L2 share.
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+constexpr int XBM = 256, XBN = 256, XBK = 32, kXThreads = 512;
+constexpr int kXPart = 256 * 64;        // one operand half (hi or lo): 256 rows x 32 bf16
+constexpr int kXStage = 4 * kXPart;     // a_hi, a_lo, b_hi, b_lo
+constexpr int kXLds = 2 * kXStage;      // 128 KiB
+constexpr int kXMaxGrid = 256;          // one workgroup per CU
+
+// LDS image of an operand half: rows of 64 B = 4 chunks of 8 bf16 (k), chunk
+// XOR-swizzled by g(row) = r2 | (r1 ^ r3) << 1 — conflict-free for the
+// ds_read_b128 fragment reads (4 x 16-lane groups), the KC-staging
+// ds_write_b64 and the NC-staging ds_write_b128 (searched exhaustively over
+// linear GF(2) swizzles against the gfx950 lane-group table).
+__device__ __forceinline__ int x_off(int row, int c) {
+  const int g = ((row >> 2) & 1) | ((((row >> 1) ^ (row >> 3)) & 1) << 1);
+  return row * 64 + 16 * (c ^ g);
+}
+
+// split-K factor of the x3 kernel for the effective shape
+__host__ __device__ __forceinline__ int split_x3(int M, int N, int K) {
+  const int tiles = ((M + XBM - 1) / XBM) * ((N + XBN - 1) / XBN);
+  if (tiles >= 128 || M == 0) return 1;
+  int s = kXMaxGrid / tiles;
+  const int smax = K / 128;
+  if (s > smax) s = smax;
+  if (s > kMaxSplit) s = kMaxSplit;
+  return s < 1 ? 1 : s;
+}
+
+// Operand view for buffer loads: SGPR descriptor + the extent in bytes.  All
+// per-lane address math is one 32-bit voffset; uniform parts go to soffset.
+// Masked lanes use voffset kXOob (>= every extent, < 2^31): the hardware
+// range check returns 0 whether or not soffset takes part in it.
+constexpr unsigned kXOob = 0x80000000u;
+struct XOp {
+  __amdgpu_buffer_rsrc_t rs;
+  int ld;
+  bool valid;
+};
+__device__ __forceinline__ XOp x_op(const float* P, int ld, long elems) {
+  XOp o;
+  o.valid = P != nullptr;
+  o.rs = __builtin_amdgcn_make_buffer_rsrc((void*)P, (short)0, (int)(elems * 4), 0x00020000);
+  o.ld = ld;
+  return o;
+}
+__device__ __forceinline__ float x_ld1(const XOp& o, unsigned voff, int soff) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(o.rs, voff, soff, 0));
+}
+typedef float xf4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ xf4 x_ld4(const XOp& o, unsigned voff, int soff) {
+  return __builtin_bit_cast(xf4, __builtin_amdgcn_raw_buffer_load_b128(o.rs, voff, soff, 0));
+}
+
+// Staging of one 256-row x 32-k operand tile into 16 fp32 registers.
+// KC (operand stored k-contiguous): lane -> k quad t & 7 of rows (t >> 3) + 64 i
+// (8 full 128-B lines per load instruction).  NC (stored row-contiguous, k
+// rows of ld): lane -> 4 consecutive rows 4 (t & 63), 4 k rows 4 (t >> 6) + j
+// (1 KiB per load instruction).  Rows past rlim and k past ke load as 0.
+template <bool KC>
+__device__ __forceinline__ void x_load(const XOp& P, const XOp& P2, int r0, int rlim, int k0, int ke,
+                                       float (&v)[16]) {
+  const int t = threadIdx.x;
+  if (KC) {
+    const int kq = t & 7;
+    const int row0 = r0 + (t >> 3);
+    const int kl = k0 + 4 * kq;
+    const bool kfull = kl + 4 <= ke;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const int row = row0 + 64 * i;
+      const bool ok = row < rlim && kl < ke;
+      const unsigned vo = ok ? (unsigned)(row * P.ld + kl) * 4u : kXOob;
+      xf4 x;
+      if (kfull || !ok) {
+        x = x_ld4(P, vo, 0);
+        if (P2.valid) x += x_ld4(P2, vo, 0);
+      } else {  // ragged K tail (K % 4 != 0): element-wise
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+          const unsigned ve = kl + e < ke ? vo + 4u * e : kXOob;
+          x[e] = x_ld1(P, ve, 0);
+          if (P2.valid) x[e] += x_ld1(P2, ve, 0);
+        }
+      }
+      v[4 * i + 0] = x[0]; v[4 * i + 1] = x[1]; v[4 * i + 2] = x[2]; v[4 * i + 3] = x[3];
+    }
+  } else {
+    // lane -> rows 4 (t & 63) .. +3 (float4 along the row direction), k = 4 (t >> 6) + j
+    const int rq = r0 + 4 * (t & 63), kg = k0 + 4 * (t >> 6);  // kg: wave-uniform
+    const bool rfull = rq + 4 <= rlim;
+    const unsigned vo = rq < rlim ? (unsigned)rq * 4u : kXOob;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const int k = kg + j;
+      const int kc = k < ke ? k : ke - 1;  // keep soffset inside the extent
+      xf4 x;
+      if (rfull || rq >= rlim) {
+        x = x_ld4(P, vo, kc * P.ld * 4);
+        if (P2.valid) x += x_ld4(P2, vo, kc * P2.ld * 4);
+      } else {  // ragged row tail
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+          const unsigned ve = rq + e < rlim ? vo + 4u * e : kXOob;
+          x[e] = x_ld1(P, ve, kc * P.ld * 4);
+          if (P2.valid) x[e] += x_ld1(P2, ve, kc * P2.ld * 4);
+        }
+      }
+      if (k >= ke) x = (xf4){0.f, 0.f, 0.f, 0.f};
+      v[4 * j + 0] = x[0]; v[4 * j + 1] = x[1]; v[4 * j + 2] = x[2]; v[4 * j + 3] = x[3];
+    }
+  }
+}
+
+template <bool KC>
+__device__ __forceinline__ void x_store(const float (&v)[16], char* hi, char* lo) {
+  const int t = threadIdx.x;
+  if (KC) {
+    const int kq = t & 7;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const int row = (t >> 3) + 64 * i;
+      bf16x4 h, l;
+#pragma unroll
+      for (int e = 0; e < 4; e++) {
+        const __bf16 b = (__bf16)v[4 * i + e];
+        h[e] = b;
+        l[e] = (__bf16)(v[4 * i + e] - (float)b);
+      }
+      const int o = x_off(row, kq >> 1) + (kq & 1) * 8;
+      *(bf16x4*)(hi + o) = h;
+      *(bf16x4*)(lo + o) = l;
+    }
+  } else {  // v[4 j + e] = (k = 4 kgrp + j, row = 4 q + e): transpose into k-contiguous rows
+    const int q = t & 63, kgrp = t >> 6;
+#pragma unroll
+    for (int e = 0; e < 4; e++) {
+      const int row = 4 * q + e;
+      bf16x4 h, l;
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const __bf16 b = (__bf16)v[4 * j + e];
+        h[j] = b;
+        l[j] = (__bf16)(v[4 * j + e] - (float)b);
+      }
+      const int o = x_off(row, kgrp >> 1) + (kgrp & 1) * 8;
+      *(bf16x4*)(hi + o) = h;
+      *(bf16x4*)(lo + o) = l;
+    }
+  }
+}
+
+template <bool A_T, bool B_T>
+__global__ void __launch_bounds__(kXThreads, 1) k_gemm_x3(GemmArgs g) {
+  extern __shared__ __attribute__((aligned(16))) char xl[];
+  constexpr bool A_KC = !A_T, B_KC = B_T;
+  const int Meff = eff_dim(g.M, g.M_dev);
+  const int Keff = eff_dim(g.K, g.K_dev);
+  const int mt = (Meff + XBM - 1) / XBM, nt = (g.N + XBN - 1) / XBN;
+  const int S = split_x3(Meff, g.N, Keff);
+  const int kchunk = ((Keff + S - 1) / S + XBK - 1) / XBK * XBK;
+  const int items = mt * nt * S;
+  const int lane = pcnn::lane_id(), wave = threadIdx.x >> 6;
+  const int wm = wave >> 2, wn = wave & 3;
+  const int r = lane & 31, hsel = lane >> 5;
+  // operand extents (elements): A (M,K) or (K,M); B (K,N) or (N,K)
+  const long a_el = A_T ? (long)(g.K - 1) * g.lda + g.M : (long)(g.M - 1) * g.lda + g.K;
+  const long b_el = B_T ? (long)(g.N - 1) * g.ldb + g.K : (long)(g.K - 1) * g.ldb + g.N;
+  const XOp oa = x_op(g.A, g.lda, a_el), oa2 = x_op(g.A2, g.lda, a_el), ob = x_op(g.B, g.ldb, b_el), onull = x_op(nullptr, 0, 0);
+  // XCD-aware order: the G/8 workgroups of one XCD take consecutive items —
+  // the m/n tiles of one K slice — so shared operand rows meet in one L2.
+  const int G = gridDim.x;
+  const int wg = (G % 8 == 0) ? (int)(blockIdx.x % 8) * (G / 8) + (int)(blockIdx.x / 8) : (int)blockIdx.x;
+  const bool m_fast = mt <= nt;  // the dimension with fewer tiles runs fastest: its
+                                 // neighbours share the other operand's tile in L2
+  for (int item = wg; item < items; item += G) {
+    const int tile = item % (mt * nt), z = item / (mt * nt);
+    const int mi = m_fast ? tile % mt : tile / nt;
+    const int ni = m_fast ? tile / mt : tile % nt;
+    const int m0 = mi * XBM, n0 = ni * XBN;
+    const int kb = z * kchunk, ke = min(Keff, kb + kchunk);
+    const int nsteps = kb < ke ? (ke - kb + XBK - 1) / XBK : 0;
+    f32x16 acc[4][2];
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+#pragma unroll
+      for (int j = 0; j < 2; j++) acc[i][j] = (f32x16){};
+    float va[16], vb[16];
+    if (nsteps > 0) {
+      x_load<A_KC>(oa, oa2, m0, Meff, kb, ke, va);
+      x_load<B_KC>(ob, onull, n0, g.N, kb, ke, vb);
+    }
+    for (int s = 0; s < nsteps; s++) {
+      char* cur = xl + (s & 1) * kXStage;
+      if (s == 0) {
+        x_store<A_KC>(va, cur, cur + kXPart);
+        x_store<B_KC>(vb, cur + 2 * kXPart, cur + 3 * kXPart);
+        if (nsteps > 1) {
+          x_load<A_KC>(oa, oa2, m0, Meff, kb + XBK, ke, va);
+          x_load<B_KC>(ob, onull, n0, g.N, kb + XBK, ke, vb);
+        }
+        __syncthreads();
+      }
+#pragma unroll
+      for (int ks = 0; ks < 2; ks++) {
+        bf16x8 bh[2], bl[2];
+#pragma unroll
+        for (int j = 0; j < 2; j++) {
+          const int o = x_off(wn * 64 + j * 32 + r, 2 * ks + hsel);
+          bh[j] = *(const bf16x8*)(cur + 2 * kXPart + o);
+          bl[j] = *(const bf16x8*)(cur + 3 * kXPart + o);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; i++) {  // A fragments streamed per sub-tile (register budget)
+          const int o = x_off(wm * 128 + i * 32 + r, 2 * ks + hsel);
+          const bf16x8 ah = *(const bf16x8*)(cur + o);
+          const bf16x8 al = *(const bf16x8*)(cur + kXPart + o);
+#pragma unroll
+          for (int j = 0; j < 2; j++) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh[j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl[j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh[j], acc[i][j], 0, 0, 0);
+          }
+        }
+      }
+      if (s + 1 < nsteps) {  // stage s+1 into the other buffer (read at step s-1, released by its barrier)
+        char* nxt = xl + ((s + 1) & 1) * kXStage;
+        x_store<A_KC>(va, nxt, nxt + kXPart);
+        x_store<B_KC>(vb, nxt + 2 * kXPart, nxt + 3 * kXPart);
+        if (s + 2 < nsteps) {
+          x_load<A_KC>(oa, oa2, m0, Meff, kb + (s + 2) * XBK, ke, va);
+          x_load<B_KC>(ob, onull, n0, g.N, kb + (s + 2) * XBK, ke, vb);
+        }
+      }
+      __syncthreads();
+    }
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+#pragma unroll
+      for (int j = 0; j < 2; j++)
+#pragma unroll
+        for (int q = 0; q < 16; q++) {
+          const int m = m0 + wm * 128 + i * 32 + (q & 3) + 8 * (q >> 2) + 4 * hsel;
+          const int n = n0 + wn * 64 + j * 32 + r;
+          if (m < Meff && n < g.N) {
+            if (S == 1) g.C[(size_t)m * g.ldc + n] = epilogue(acc[i][j][q], g, m, n);
+            else g.slab[((size_t)z * g.M + m) * g.N + n] = acc[i][j][q];
+          }
+        }
+  }
+}
+
 __global__ void __launch_bounds__(256) k_gemm_reduce(GemmArgs g) {
   const int Meff = eff_dim(g.M, g.M_dev);
   const int Keff = eff_dim(g.K, g.K_dev);
-  const int S = split_for(Meff, g.N, Keff);
+  const int S = g.prec ? split_x3(Meff, g.N, Keff) : split_for(Meff, g.N, Keff);
   if (S == 1) return;
   const long total = (long)Meff * g.N;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
@@ -258,13 +524,24 @@ __global__ void __launch_bounds__(256) k_gemm_reduce(GemmArgs g) {
   }
 }
 
-__global__ void k_colsum(const float* __restrict__ X, int M, int N, int ldx, const int32_t* __restrict__ M_dev,
-                         float* __restrict__ out) {
+// Column sums (bias gradients): block = 64 columns x 16 row groups; each thread
+// sums rows m = g, g+16, ... (coalesced 256 B rows), the 16 partials are then
+// added in fixed order (deterministic).
+__global__ void __launch_bounds__(1024) k_colsum(const float* __restrict__ X, int M, int N, int ldx,
+                                                 const int32_t* __restrict__ M_dev, float* __restrict__ out) {
+  __shared__ float part[16][65];
   const int Meff = eff_dim(M, M_dev);
-  for (int n = blockIdx.x * blockDim.x + threadIdx.x; n < N; n += gridDim.x * blockDim.x) {
-    float s = 0.f;
-    for (int m = 0; m < Meff; m++) s += X[(size_t)m * ldx + n];
-    out[n] = s;
+  const int col = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const int n = blockIdx.x * 64 + col;
+  float s = 0.f;
+  if (n < N)
+    for (int m = grp; m < Meff; m += 16) s += X[(size_t)m * ldx + n];
+  part[grp][col] = s;
+  __syncthreads();
+  if (grp == 0 && n < N) {
+    float t = 0.f;
+    for (int g = 0; g < 16; g++) t += part[g][col];
+    out[n] = t;
   }
 }
 
@@ -337,10 +614,9 @@ __global__ void __launch_bounds__(256) k_head_bwd(const float* __restrict__ dpre
 }  // namespace
 
 extern "C" size_t pcnn_gemm_workspace_size(int M, int N, int K, int m_dynamic, int precision) {
-  (void)precision;
   if (M <= 0 || N <= 0) return 256;
   // split-K partial slabs; the split only grows when the device-side M shrinks
-  const int s = split_for(m_dynamic ? 1 : M, N, K);
+  const int s = precision == 1 ? split_x3(m_dynamic ? 1 : M, N, K) : split_for(m_dynamic ? 1 : M, N, K);
   return s > 1 ? pcnn::align_up((size_t)s * M * N * sizeof(float), 256) + 256 : 256;
 }
 
@@ -349,24 +625,49 @@ extern "C" int pcnn_gemm(int M, int N, int K, const float* A, const float* A2, i
                          int ldm, const int32_t* M_dev, const int32_t* K_dev, int precision, void* workspace,
                          size_t workspace_bytes, void* stream) {
   PCNN_REQUIRE(M >= 0 && N > 0 && K >= 0 && A && B && Cm);
-  PCNN_REQUIRE(precision == 0);
+  PCNN_REQUIRE(precision == 0 || precision == 1);
   PCNN_REQUIRE(lda >= (a_trans ? M : K) && ldb >= (b_trans ? K : N) && ldc >= N);
   PCNN_REQUIRE(!mask || ldm >= N);
   PCNN_REQUIRE(act == 0 || act == 1);
+  // split-bf16 path: 16-B vector staging loads, 32-bit buffer offsets
+  PCNN_REQUIRE(precision == 0 || (lda % 4 == 0 && ldb % 4 == 0 && ((uintptr_t)A & 15) == 0 &&
+                                  ((uintptr_t)B & 15) == 0 && (!A2 || ((uintptr_t)A2 & 15) == 0)));
+  PCNN_REQUIRE(precision == 0 || ((long)(a_trans ? K : M) * lda < (1l << 29) && (long)(b_trans ? N : K) * ldb < (1l << 29)));
   if (M == 0) return PCNN_OK;
   if (workspace_bytes < pcnn_gemm_workspace_size(M, N, K, M_dev != nullptr, precision) || !workspace)
     return PCNN_ECAPACITY;
-  GemmArgs g{M, N, K, A, A2, lda, B, ldb, Cm, ldc, bias, act, mask, ldm, M_dev, K_dev, (float*)workspace};
+  GemmArgs g{M, N, K, A, A2, lda, B, ldb, Cm, ldc, bias, act, mask, ldm, M_dev, K_dev, (float*)workspace, precision};
   hipStream_t st = (hipStream_t)stream;
-  const int mt = (M + BM - 1) / BM, nt = (N + BN - 1) / BN;
-  // persistent grid sized for the capacity shape at its split
-  const long items = (long)mt * nt * split_for(M, N, K);
-  long grid = items < 2048 ? items : 2048;
-  if (grid < 512) grid = 512;
-  if (!a_trans && !b_trans) hipLaunchKernelGGL((k_gemm_f32<false, false>), dim3(grid), dim3(kGemmThreads), 0, st, g);
-  else if (!a_trans && b_trans) hipLaunchKernelGGL((k_gemm_f32<false, true>), dim3(grid), dim3(kGemmThreads), 0, st, g);
-  else if (a_trans && !b_trans) hipLaunchKernelGGL((k_gemm_f32<true, false>), dim3(grid), dim3(kGemmThreads), 0, st, g);
-  else hipLaunchKernelGGL((k_gemm_f32<true, true>), dim3(grid), dim3(kGemmThreads), 0, st, g);
+  if (precision == 1) {
+    // persistent grid: one workgroup per CU (a multiple of 8 for the XCD-aware
+    // item order); the device-side M can only shrink the item count
+    static bool attr_set = false;
+    if (!attr_set) {
+      hipFuncSetAttribute((const void*)k_gemm_x3<false, false>, hipFuncAttributeMaxDynamicSharedMemorySize, kXLds);
+      hipFuncSetAttribute((const void*)k_gemm_x3<false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, kXLds);
+      hipFuncSetAttribute((const void*)k_gemm_x3<true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, kXLds);
+      hipFuncSetAttribute((const void*)k_gemm_x3<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, kXLds);
+      attr_set = true;
+    }
+    const int mt = (M + XBM - 1) / XBM, nt = (N + XBN - 1) / XBN;
+    const long cap_items = (long)mt * nt * kMaxSplit;
+    long grid = cap_items < kXMaxGrid ? cap_items : kXMaxGrid;
+    if (grid >= 8) grid -= grid % 8;
+    if (!a_trans && !b_trans) hipLaunchKernelGGL((k_gemm_x3<false, false>), dim3(grid), dim3(kXThreads), kXLds, st, g);
+    else if (!a_trans && b_trans) hipLaunchKernelGGL((k_gemm_x3<false, true>), dim3(grid), dim3(kXThreads), kXLds, st, g);
+    else if (a_trans && !b_trans) hipLaunchKernelGGL((k_gemm_x3<true, false>), dim3(grid), dim3(kXThreads), kXLds, st, g);
+    else hipLaunchKernelGGL((k_gemm_x3<true, true>), dim3(grid), dim3(kXThreads), kXLds, st, g);
+  } else {
+    const int mt = (M + BM - 1) / BM, nt = (N + BN - 1) / BN;
+    // persistent grid sized for the capacity shape at its split
+    const long items = (long)mt * nt * split_for(M, N, K);
+    long grid = items < 2048 ? items : 2048;
+    if (grid < 512) grid = 512;
+    if (!a_trans && !b_trans) hipLaunchKernelGGL((k_gemm_f32<false, false>), dim3(grid), dim3(kGemmThreads), 0, st, g);
+    else if (!a_trans && b_trans) hipLaunchKernelGGL((k_gemm_f32<false, true>), dim3(grid), dim3(kGemmThreads), 0, st, g);
+    else if (a_trans && !b_trans) hipLaunchKernelGGL((k_gemm_f32<true, false>), dim3(grid), dim3(kGemmThreads), 0, st, g);
+    else hipLaunchKernelGGL((k_gemm_f32<true, true>), dim3(grid), dim3(kGemmThreads), 0, st, g);
+  }
   hipLaunchKernelGGL(k_gemm_reduce, dim3(1024), dim3(256), 0, st, g);
   PCNN_CHECK_LAUNCH();
   return PCNN_OK;
@@ -374,7 +675,7 @@ extern "C" int pcnn_gemm(int M, int N, int K, const float* A, const float* A2, i
 
 extern "C" int pcnn_colsum(const float* X, int M, int N, int ldx, const int32_t* M_dev, float* out, void* stream) {
   PCNN_REQUIRE(X && out && M >= 0 && N > 0 && ldx >= N);
-  hipLaunchKernelGGL(k_colsum, dim3((N + 255) / 256), dim3(256), 0, (hipStream_t)stream, X, M, N, ldx, M_dev, out);
+  hipLaunchKernelGGL(k_colsum, dim3((N + 63) / 64), dim3(1024), 0, (hipStream_t)stream, X, M, N, ldx, M_dev, out);
   PCNN_CHECK_LAUNCH();
   return PCNN_OK;
 }

@@ -30,7 +30,7 @@ CAP = hv.CAPACITY
 class PoseStep:
     def __init__(self, B, H, W, num_classes, device, conv4_hw=None, conv5_hw=None, channels=512, units=4096,
                  is_train=1, skip_pixels=10, vote_threshold=-1.0, vote_percentage=0.02, margin=0.01,
-                 global_batch=None, batch_base=0, weights=None, dist=None, backward=True):
+                 global_batch=None, batch_base=0, weights=None, dist=None, backward=True, precision=1):
         self.B, self.H, self.W, self.C = B, H, W, num_classes
         self.dev = device
         self.is_train, self.skip, self.vthr, self.vper, self.margin = is_train, skip_pixels, vote_threshold, \
@@ -39,6 +39,7 @@ class PoseStep:
         self.batch_base = batch_base
         self.dist = dist  # torch.distributed module (initialised) or None
         self.backward = backward
+        self.prec = precision  # FC GEMMs: 1 = split-bf16 x3 MFMA (fp32-class), 0 = exact fp32 MFMA
         self.h4, self.w4 = conv4_hw or (H // 8, W // 8)
         self.h5, self.w5 = conv5_hw or (H // 16, W // 16)
         self.Ch = channels
@@ -130,10 +131,10 @@ class PoseStep:
         x5 = self.pool5.view(CAP, K6)
         x4 = self.pool4.view(CAP, K6)
         with self._t("gemm_fc6_fwd"):
-            ph.gemm(x5, w.w6, self.y6, A2=x4, bias=w.b6, act=1, M_dev=nr)
+            ph.gemm(x5, w.w6, self.y6, A2=x4, bias=w.b6, act=1, M_dev=nr, precision=self.prec)
         with self._t("gemm_fc7_fc8_fwd"):
-            ph.gemm(self.y6, w.w7, self.y7, bias=w.b7, act=1, M_dev=nr)
-            ph.gemm(self.y7, w.w8, self.y8, bias=w.b8, act=0, M_dev=nr)
+            ph.gemm(self.y6, w.w7, self.y7, bias=w.b7, act=1, M_dev=nr, precision=self.prec)
+            ph.gemm(self.y7, w.w8, self.y8, bias=w.b8, act=0, M_dev=nr, precision=self.prec)
         with self._t("head_add_loss_fwd"):
             ph.head_fwd(self.y8, h["weight"], self.t8, self.pred, num_rois=nr)
             adl.average_distance_loss(self.pred, h["target"], h["weight"], points, symmetry, self.margin,
@@ -152,19 +153,19 @@ class PoseStep:
             adl.average_distance_loss_grad(self.diff, self.one, num_rois=nr, out=self.dpred)
             ph.head_bwd(self.dpred, self.t8, h["weight"], self.pred, self.dy8, num_rois=nr)
         with self._t("gemm_fc8_fc7_bwd"):
-            ph.gemm(self.y7, self.dy8, g["w8"], a_trans=1, K_dev=nr, M=w.units, N=self.D, K=CAP)
+            ph.gemm(self.y7, self.dy8, g["w8"], a_trans=1, K_dev=nr, M=w.units, N=self.D, K=CAP, precision=self.prec)
             ph.colsum(self.dy8, g["b8"], M_dev=nr)
-            ph.gemm(self.dy8, w.w8, self.dy7, b_trans=1, mask=self.y7, M_dev=nr)
-            ph.gemm(self.y6, self.dy7, g["w7"], a_trans=1, K_dev=nr, M=w.units, N=w.units, K=CAP)
+            ph.gemm(self.dy8, w.w8, self.dy7, b_trans=1, mask=self.y7, M_dev=nr, precision=self.prec)
+            ph.gemm(self.y6, self.dy7, g["w7"], a_trans=1, K_dev=nr, M=w.units, N=w.units, K=CAP, precision=self.prec)
             ph.colsum(self.dy7, g["b7"], M_dev=nr)
-            ph.gemm(self.dy7, w.w7, self.dy6, b_trans=1, mask=self.y6, M_dev=nr)
+            ph.gemm(self.dy7, w.w7, self.dy6, b_trans=1, mask=self.y6, M_dev=nr, precision=self.prec)
         x5 = self.pool5.view(CAP, K6)
         x4 = self.pool4.view(CAP, K6)
         with self._t("gemm_fc6_dw"):  # A = pool5 + pool4, fused
-            ph.gemm(x5, self.dy6, g["w6"], a_trans=1, A2=x4, K_dev=nr, M=K6, N=w.units, K=CAP)
+            ph.gemm(x5, self.dy6, g["w6"], a_trans=1, A2=x4, K_dev=nr, M=K6, N=w.units, K=CAP, precision=self.prec)
             ph.colsum(self.dy6, g["b6"], M_dev=nr)
         with self._t("gemm_fc6_dx"):
-            ph.gemm(self.dy6, w.w6, self.dx, b_trans=1, M_dev=nr)
+            ph.gemm(self.dy6, w.w6, self.dx, b_trans=1, M_dev=nr, precision=self.prec)
         dxp = self.dx.view(CAP, 7, 7, self.Ch)
         with self._t("roi_pool_bwd"):  # both pools receive d(pool5 + pool4) = dx
             rp.roi_pool_grad(conv5, h["box"], self.arg5, dxp, 7, 7, 1.0 / 16.0, 0, num_rois=nr, out=self.dconv5)

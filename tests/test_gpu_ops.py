@@ -117,8 +117,18 @@ def test_backproject(hip, orc):
     np.testing.assert_array_equal(gd.cpu().numpy(), orc.backproject_bwd(g, depth, meta, H, W, G))
 
 
+# Tolerances: precision 0 is fp32 MFMA (fp32 products, fp32 accumulation);
+# precision 1 is the split-bf16 x3 MFMA (hi*hi + hi*lo + lo*hi, fp32
+# accumulation): per-product relative error <= ~2^-16, so the error of a
+# K-term dot product of O(1) values is ~2^-16 * sqrt(K).  Both are held to
+# the north-star 1e-4 relative bound, with atol scaled by sqrt(K).
+def _gemm_tol(prec, K):
+    return dict(rtol=2e-5, atol=2e-4) if prec == 0 else dict(rtol=1e-4, atol=1e-4 * np.sqrt(K))
+
+
+@pytest.mark.parametrize("prec", [0, 1])
 @pytest.mark.parametrize("at,bt", [(0, 0), (0, 1), (1, 0), (1, 1)])
-def test_gemm_layouts(hip, at, bt):
+def test_gemm_layouts(hip, at, bt, prec):
     rng = np.random.default_rng(5)
     M, N, K = 200, 300, 1000
     A = rng.normal(size=(M, K)).astype(np.float32)
@@ -129,12 +139,13 @@ def test_gemm_layouts(hip, at, bt):
     A2s = A2.T.copy() if at else A2
     Bs = B.T.copy() if bt else B
     C = torch.empty((M, N), dtype=torch.float32, device=D)
-    ph.gemm(T(As), T(Bs), C, a_trans=at, b_trans=bt, A2=T(A2s), bias=T(bias), act=1)
+    ph.gemm(T(As), T(Bs), C, a_trans=at, b_trans=bt, A2=T(A2s), bias=T(bias), act=1, precision=prec)
     ref = np.maximum((A.astype(np.float64) + A2) @ B + bias, 0)
-    np.testing.assert_allclose(C.cpu().numpy(), ref, rtol=2e-5, atol=2e-4)
+    np.testing.assert_allclose(C.cpu().numpy(), ref, **_gemm_tol(prec, 2 * K))
 
 
-def test_gemm_device_dims_split(hip):
+@pytest.mark.parametrize("prec", [0, 1])
+def test_gemm_device_dims_split(hip, prec):
     rng = np.random.default_rng(6)
     M, N, K = 1152, 256, 8192
     A = rng.normal(size=(M, K)).astype(np.float32)
@@ -142,13 +153,33 @@ def test_gemm_device_dims_split(hip):
     mask = rng.normal(size=(M, N)).astype(np.float32)
     Mdev = torch.tensor([333], dtype=torch.int32, device=D)
     C = torch.zeros((M, N), dtype=torch.float32, device=D)
-    ph.gemm(T(A), T(B), C, mask=T(mask), M_dev=Mdev)
+    ph.gemm(T(A), T(B), C, mask=T(mask), M_dev=Mdev, precision=prec)
     ref = (A[:333].astype(np.float64) @ B) * (mask[:333] > 0)
-    np.testing.assert_allclose(C[:333].cpu().numpy(), ref, rtol=2e-5, atol=5e-4)
+    np.testing.assert_allclose(C[:333].cpu().numpy(), ref, **(dict(rtol=2e-5, atol=5e-4) if prec == 0 else _gemm_tol(1, K)))
     assert not C[333:].cpu().numpy().any()
     # K on device (weight-gradient form: C = A^T B over the first 77 rows)
     Kdev = torch.tensor([77], dtype=torch.int32, device=D)
     C2 = torch.empty((K, N), dtype=torch.float32, device=D)
-    ph.gemm(T(A), T(B[:M].copy()), C2, a_trans=1, K_dev=Kdev, M=K, N=N, K=M)
+    ph.gemm(T(A), T(B[:M].copy()), C2, a_trans=1, K_dev=Kdev, M=K, N=N, K=M, precision=prec)
     ref2 = A[:77].T.astype(np.float64) @ B[:77]
-    np.testing.assert_allclose(C2.cpu().numpy(), ref2, rtol=2e-5, atol=5e-4)
+    np.testing.assert_allclose(C2.cpu().numpy(), ref2, **(dict(rtol=2e-5, atol=5e-4) if prec == 0 else _gemm_tol(1, 77)))
+
+
+@pytest.mark.parametrize("prec", [0, 1])
+@pytest.mark.parametrize("at,bt", [(0, 0), (0, 1), (1, 0), (1, 1)])
+def test_gemm_ragged_padded(hip, at, bt, prec):
+    """Ragged M/N/K (no multiple of 4 or of the tile) through padded leading dims."""
+    rng = np.random.default_rng(8)
+    M, N, K = 203, 301, 999
+    A = rng.normal(size=(M, K)).astype(np.float32)
+    B = rng.normal(size=(K, N)).astype(np.float32)
+
+    def padded(X, trans):
+        X = X.T if trans else X
+        buf = torch.zeros((X.shape[0], (X.shape[1] + 7) // 4 * 4), dtype=torch.float32, device=D)
+        buf[:, :X.shape[1]] = T(X)
+        return buf[:, :X.shape[1]]
+    C = torch.empty((M, N), dtype=torch.float32, device=D)
+    ph.gemm(padded(A, at), padded(B, bt), C, a_trans=at, b_trans=bt, M=M, N=N, K=K, precision=prec)
+    ref = A.astype(np.float64) @ B
+    np.testing.assert_allclose(C.cpu().numpy(), ref, **_gemm_tol(prec, K))
