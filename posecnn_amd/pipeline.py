@@ -23,6 +23,7 @@ from . import pose_head as ph
 from .hough_voting_gpu_layer import hough_voting_gpu_op as hv
 from .roi_pooling_layer import roi_pooling_op as rp
 from .average_distance_loss import average_distance_loss_op as adl
+from .exchange import RoiExchange
 
 CAP = hv.CAPACITY
 
@@ -74,11 +75,7 @@ class PoseStep:
         self.dconv5 = torch.zeros((B, self.h5, self.w5, channels), **f32)
         self.norm_rows = torch.zeros((1,), **i32)
         self.timer = None  # optional {name: [(start_event, end_event), ...]} (bench.py)
-        if dist is not None:
-            ws = dist.get_world_size()
-            self.g_counts = torch.zeros((ws * 2,), **i32)
-            self.g_rows = torch.zeros((ws * CAP, 14), **f32)
-            self.l_rows = torch.zeros((CAP, 14), **f32)
+        self.xchg = RoiExchange(dist, CAP, device) if dist is not None else None
 
     # ------------------------------------------------------------------
     def _t(self, name):
@@ -105,20 +102,16 @@ class PoseStep:
                                                 batch_base=self.batch_base, out=self.hough)
 
     def exchange(self):
-        """RCCL all-gather of the detected RoIs + initial poses and row counts;
-        global loss normaliser = max(sum of per-rank rows, 1)."""
+        """RCCL all-gather of the detected RoIs + initial poses (global rows in
+        single-device order, posecnn_amd/exchange.py); global loss normaliser
+        = max(sum of per-rank rows, 1)."""
         h = self.hough
-        if self.dist is None:
+        if self.xchg is None:
             self.norm_rows.copy_(h["num_rois"][1:2])
             return
-        d = self.dist
         with self._t("allgather_rois"):
-            self.l_rows[:, :7].copy_(h["box"])
-            self.l_rows[:, 7:].copy_(h["pose"])
-            d.all_gather_into_tensor(self.g_counts, h["num_rois"])
-            d.all_gather_into_tensor(self.g_rows, self.l_rows)
-            tot = self.g_counts.view(-1, 2)[:, 0].sum(dtype=torch.int32).clamp_(min=1)
-            self.norm_rows.copy_(tot.view(1))
+            _, total = self.xchg(h["box"], h["pose"], h["num_rois"])
+            self.norm_rows.copy_(total.clamp(min=1))
 
     def forward(self, conv4, conv5, points, symmetry):
         h = self.hough
