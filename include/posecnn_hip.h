@@ -91,6 +91,14 @@ int pcnn_roi_pool_fwd(const float* data, int B, int H, int W, int C, int layout,
                       int roi_stride, const int32_t* num_rois_dev, float spatial_scale, int pooled_h, int pooled_w,
                       int pool_channel, float* top, int32_t* argmax, void* stream);
 
+/* As pcnn_roi_pool_fwd but top += pooled (argmax is written as usual): the
+ * second pool of vgg16_convs.py:178-184 produces pool5 + pool4 in place, so
+ * the fc6 contraction reads one operand.  Same sum as tf.add(pool5, pool4). */
+int pcnn_roi_pool_fwd_accumulate(const float* data, int B, int H, int W, int C, int layout, const float* rois,
+                                 int R_cap, int roi_stride, const int32_t* num_rois_dev, float spatial_scale,
+                                 int pooled_h, int pooled_w, int pool_channel, float* top, int32_t* argmax,
+                                 void* stream);
+
 size_t pcnn_roi_pool_bwd_workspace_size(int B, int R_cap);
 
 int pcnn_roi_pool_bwd(const float* top_diff, const int32_t* argmax, int B, int H, int W, int C, int layout,

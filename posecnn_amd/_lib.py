@@ -35,6 +35,8 @@ _SIGS = {
     "pcnn_hough_voting_diag": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_float, c_void_p, c_void_p]),
     "pcnn_roi_pool_fwd": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p,
                                   c_float, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p]),
+    "pcnn_roi_pool_fwd_accumulate": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int,
+                                             c_void_p, c_float, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     "pcnn_roi_pool_bwd_workspace_size": (c_size_t, [c_int, c_int]),
     "pcnn_roi_pool_bwd": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int,
                                   c_void_p, c_float, c_int, c_int, c_int, c_void_p, c_void_p, c_size_t, c_void_p]),

@@ -22,7 +22,8 @@ namespace {
 
 constexpr int BM = 128, BN = 128, BK = 16;
 constexpr int kGemmThreads = 256;
-constexpr int kMaxSplit = 8;
+constexpr int kMaxSplit = 8;   // fp32 kernel
+constexpr int kMaxSplitX = 16; // split-bf16 kernel (small-tile shapes such as fc8)
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
@@ -283,7 +284,7 @@ __host__ __device__ __forceinline__ int split_x3(int M, int N, int K) {
   int s = kXMaxGrid / tiles;
   const int smax = K / 128;
   if (s > smax) s = smax;
-  if (s > kMaxSplit) s = kMaxSplit;
+  if (s > kMaxSplitX) s = kMaxSplitX;
   return s < 1 ? 1 : s;
 }
 
@@ -315,58 +316,66 @@ __device__ __forceinline__ xf4 x_ld4(const XOp& o, unsigned voff, int soff) {
 // Staging of one 256-row x 32-k operand tile into 16 fp32 registers.
 // KC (operand stored k-contiguous): lane -> k quad t & 7 of rows (t >> 3) + 64 i
 // (8 full 128-B lines per load instruction).  NC (stored row-contiguous, k
-// rows of ld): lane -> 4 consecutive rows 4 (t & 63), 4 k rows 4 (t >> 6) + j
-// (1 KiB per load instruction).  Rows past rlim and k past ke load as 0.
-template <bool KC>
+// rows of ld): wave w takes rows 64 (w >> 1) .. +63 and k 16 (w & 1) .. +15;
+// lane l -> row quad l >> 2 (float4 along the row direction) and k quad l & 3,
+// so each load instruction reads four 256-B runs and the transposed LDS
+// writes of a 16-lane group spread over both halves of each chunk.
+// Rows past rlim and k past ke load as 0.  RAGGED: some float4 may straddle
+// the K edge (KC) or the row edge (NC) -> element-wise fallback; the common
+// instantiation has no divergent branch, so a K step is one basic block.
+template <bool KC, bool RAGGED, bool A2>
 __device__ __forceinline__ void x_load(const XOp& P, const XOp& P2, int r0, int rlim, int k0, int ke,
                                        float (&v)[16]) {
+  // Every mask is applied to the load ADDRESS (out-of-range voffset -> the
+  // hardware returns 0), never to the loaded data: nothing consumes a loaded
+  // register before the staging store of the next step, so all loads of a
+  // step stay in flight together.  (A2: the summed operand of the generic
+  // A + A2 form adds right after its loads.)
   const int t = threadIdx.x;
   if (KC) {
     const int kq = t & 7;
     const int row0 = r0 + (t >> 3);
     const int kl = k0 + 4 * kq;
-    const bool kfull = kl + 4 <= ke;
 #pragma unroll
     for (int i = 0; i < 4; i++) {
       const int row = row0 + 64 * i;
       const bool ok = row < rlim && kl < ke;
       const unsigned vo = ok ? (unsigned)(row * P.ld + kl) * 4u : kXOob;
       xf4 x;
-      if (kfull || !ok) {
+      if (!RAGGED || kl + 4 <= ke || !ok) {
         x = x_ld4(P, vo, 0);
-        if (P2.valid) x += x_ld4(P2, vo, 0);
-      } else {  // ragged K tail (K % 4 != 0): element-wise
+        if (A2) x += x_ld4(P2, vo, 0);
+      } else {
 #pragma unroll
         for (int e = 0; e < 4; e++) {
           const unsigned ve = kl + e < ke ? vo + 4u * e : kXOob;
           x[e] = x_ld1(P, ve, 0);
-          if (P2.valid) x[e] += x_ld1(P2, ve, 0);
+          if (A2) x[e] += x_ld1(P2, ve, 0);
         }
       }
       v[4 * i + 0] = x[0]; v[4 * i + 1] = x[1]; v[4 * i + 2] = x[2]; v[4 * i + 3] = x[3];
     }
   } else {
-    // lane -> rows 4 (t & 63) .. +3 (float4 along the row direction), k = 4 (t >> 6) + j
-    const int rq = r0 + 4 * (t & 63), kg = k0 + 4 * (t >> 6);  // kg: wave-uniform
-    const bool rfull = rq + 4 <= rlim;
-    const unsigned vo = rq < rlim ? (unsigned)rq * 4u : kXOob;
+    const int w = t >> 6, l = t & 63;
+    const int rq = r0 + 64 * (w >> 1) + 4 * (l >> 2);
+    const int kg = k0 + 16 * (w & 1) + 4 * (l & 3);
 #pragma unroll
     for (int j = 0; j < 4; j++) {
       const int k = kg + j;
-      const int kc = k < ke ? k : ke - 1;  // keep soffset inside the extent
+      const bool ok = rq < rlim && k < ke;
+      const unsigned vo = ok ? (unsigned)(k * P.ld + rq) * 4u : kXOob;
       xf4 x;
-      if (rfull || rq >= rlim) {
-        x = x_ld4(P, vo, kc * P.ld * 4);
-        if (P2.valid) x += x_ld4(P2, vo, kc * P2.ld * 4);
-      } else {  // ragged row tail
+      if (!RAGGED || rq + 4 <= rlim || !ok) {
+        x = x_ld4(P, vo, 0);
+        if (A2) x += x_ld4(P2, vo, 0);
+      } else {
 #pragma unroll
         for (int e = 0; e < 4; e++) {
           const unsigned ve = rq + e < rlim ? vo + 4u * e : kXOob;
-          x[e] = x_ld1(P, ve, kc * P.ld * 4);
-          if (P2.valid) x[e] += x_ld1(P2, ve, kc * P2.ld * 4);
+          x[e] = x_ld1(P, ve, 0);
+          if (A2) x[e] += x_ld1(P2, ve, 0);
         }
       }
-      if (k >= ke) x = (xf4){0.f, 0.f, 0.f, 0.f};
       v[4 * j + 0] = x[0]; v[4 * j + 1] = x[1]; v[4 * j + 2] = x[2]; v[4 * j + 3] = x[3];
     }
   }
@@ -391,26 +400,28 @@ __device__ __forceinline__ void x_store(const float (&v)[16], char* hi, char* lo
       *(bf16x4*)(hi + o) = h;
       *(bf16x4*)(lo + o) = l;
     }
-  } else {  // v[4 j + e] = (k = 4 kgrp + j, row = 4 q + e): transpose into k-contiguous rows
-    const int q = t & 63, kgrp = t >> 6;
+  } else {  // v[4 j + e] = (k = k-quad base + j, row = row-quad base + e): transpose into k-contiguous rows
+    const int w = t >> 6, l = t & 63;
+    const int rb = 64 * (w >> 1) + 4 * (l >> 2);
+    const int kq = 4 * (w & 1) + (l & 3);  // k quad index 0..7 within the 32-k step
 #pragma unroll
     for (int e = 0; e < 4; e++) {
-      const int row = 4 * q + e;
-      bf16x4 h, l;
+      const int row = rb + e;
+      bf16x4 h, lo4;
 #pragma unroll
       for (int j = 0; j < 4; j++) {
         const __bf16 b = (__bf16)v[4 * j + e];
         h[j] = b;
-        l[j] = (__bf16)(v[4 * j + e] - (float)b);
+        lo4[j] = (__bf16)(v[4 * j + e] - (float)b);
       }
-      const int o = x_off(row, kgrp >> 1) + (kgrp & 1) * 8;
+      const int o = x_off(row, kq >> 1) + (kq & 1) * 8;
       *(bf16x4*)(hi + o) = h;
-      *(bf16x4*)(lo + o) = l;
+      *(bf16x4*)(lo + o) = lo4;
     }
   }
 }
 
-template <bool A_T, bool B_T>
+template <bool A_T, bool B_T, bool RAGGED, bool A2>
 __global__ void __launch_bounds__(kXThreads, 1) k_gemm_x3(GemmArgs g) {
   extern __shared__ __attribute__((aligned(16))) char xl[];
   constexpr bool A_KC = !A_T, B_KC = B_T;
@@ -426,13 +437,24 @@ __global__ void __launch_bounds__(kXThreads, 1) k_gemm_x3(GemmArgs g) {
   // operand extents (elements): A (M,K) or (K,M); B (K,N) or (N,K)
   const long a_el = A_T ? (long)(g.K - 1) * g.lda + g.M : (long)(g.M - 1) * g.lda + g.K;
   const long b_el = B_T ? (long)(g.N - 1) * g.ldb + g.K : (long)(g.K - 1) * g.ldb + g.N;
-  const XOp oa = x_op(g.A, g.lda, a_el), oa2 = x_op(g.A2, g.lda, a_el), ob = x_op(g.B, g.ldb, b_el), onull = x_op(nullptr, 0, 0);
+  const XOp oa = x_op(g.A, g.lda, a_el), oa2 = x_op(g.A2, g.lda, a_el), ob = x_op(g.B, g.ldb, b_el),
+            onull = x_op(nullptr, 0, 0);
+
   // XCD-aware order: the G/8 workgroups of one XCD take consecutive items —
   // the m/n tiles of one K slice — so shared operand rows meet in one L2.
   const int G = gridDim.x;
   const int wg = (G % 8 == 0) ? (int)(blockIdx.x % 8) * (G / 8) + (int)(blockIdx.x / 8) : (int)blockIdx.x;
   const bool m_fast = mt <= nt;  // the dimension with fewer tiles runs fastest: its
                                  // neighbours share the other operand's tile in L2
+  // fragment offsets (bytes) inside an operand half, per k16 sub-step
+  int a_off[2][4], b_off[2][2];
+#pragma unroll
+  for (int ks = 0; ks < 2; ks++) {
+#pragma unroll
+    for (int i = 0; i < 4; i++) a_off[ks][i] = x_off(wm * 128 + i * 32 + r, 2 * ks + hsel);
+#pragma unroll
+    for (int j = 0; j < 2; j++) b_off[ks][j] = x_off(wn * 64 + j * 32 + r, 2 * ks + hsel);
+  }
   for (int item = wg; item < items; item += G) {
     const int tile = item % (mt * nt), z = item / (mt * nt);
     const int mi = m_fast ? tile % mt : tile / nt;
@@ -445,68 +467,91 @@ __global__ void __launch_bounds__(kXThreads, 1) k_gemm_x3(GemmArgs g) {
     for (int i = 0; i < 4; i++)
 #pragma unroll
       for (int j = 0; j < 2; j++) acc[i][j] = (f32x16){};
-    float va[16], vb[16];
     if (nsteps > 0) {
-      x_load<A_KC>(oa, oa2, m0, Meff, kb, ke, va);
-      x_load<B_KC>(ob, onull, n0, g.N, kb, ke, vb);
-    }
-    for (int s = 0; s < nsteps; s++) {
-      char* cur = xl + (s & 1) * kXStage;
-      if (s == 0) {
-        x_store<A_KC>(va, cur, cur + kXPart);
-        x_store<B_KC>(vb, cur + 2 * kXPart, cur + 3 * kXPart);
-        if (nsteps > 1) {
-          x_load<A_KC>(oa, oa2, m0, Meff, kb + XBK, ke, va);
-          x_load<B_KC>(ob, onull, n0, g.N, kb + XBK, ke, vb);
-        }
-        __syncthreads();
-      }
+      float va[16], vb[16];
+      // prologue: stage 0 -> LDS buffer 0, stage 1 -> registers
+      x_load<A_KC, RAGGED, A2>(oa, oa2, m0, Meff, kb, ke, va);
+      x_load<B_KC, RAGGED, false>(ob, onull, n0, g.N, kb, ke, vb);
+      x_store<A_KC>(va, xl, xl + kXPart);
+      x_store<B_KC>(vb, xl + 2 * kXPart, xl + 3 * kXPart);
+      const int k1 = kb + (nsteps > 1 ? XBK : 0);
+      x_load<A_KC, RAGGED, A2>(oa, oa2, m0, Meff, k1, ke, va);
+      x_load<B_KC, RAGGED, false>(ob, onull, n0, g.N, k1, ke, vb);
+      __syncthreads();
+      // steady state, one basic block per step: MFMAs on buffer s & 1, stage
+      // s+1 (registers) -> the other buffer, loads of stage s+2 (clamped to
+      // the last stage: the surplus stores land in a buffer nobody reads)
+      for (int s = 0; s < nsteps; s++) {
+        const char* cur = xl + (s & 1) * kXStage;
+        char* nxt = xl + ((s + 1) & 1) * kXStage;
 #pragma unroll
-      for (int ks = 0; ks < 2; ks++) {
-        bf16x8 bh[2], bl[2];
-#pragma unroll
-        for (int j = 0; j < 2; j++) {
-          const int o = x_off(wn * 64 + j * 32 + r, 2 * ks + hsel);
-          bh[j] = *(const bf16x8*)(cur + 2 * kXPart + o);
-          bl[j] = *(const bf16x8*)(cur + 3 * kXPart + o);
-        }
-#pragma unroll
-        for (int i = 0; i < 4; i++) {  // A fragments streamed per sub-tile (register budget)
-          const int o = x_off(wm * 128 + i * 32 + r, 2 * ks + hsel);
-          const bf16x8 ah = *(const bf16x8*)(cur + o);
-          const bf16x8 al = *(const bf16x8*)(cur + kXPart + o);
+        for (int ks = 0; ks < 2; ks++) {
+          bf16x8 bh[2], bl[2];
 #pragma unroll
           for (int j = 0; j < 2; j++) {
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh[j], acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl[j], acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh[j], acc[i][j], 0, 0, 0);
+            bh[j] = *(const bf16x8*)(cur + 2 * kXPart + b_off[ks][j]);
+            bl[j] = *(const bf16x8*)(cur + 3 * kXPart + b_off[ks][j]);
+          }
+#pragma unroll
+          for (int i = 0; i < 4; i++) {
+            const bf16x8 ah = *(const bf16x8*)(cur + a_off[ks][i]);
+            const bf16x8 al = *(const bf16x8*)(cur + kXPart + a_off[ks][i]);
+#pragma unroll
+            for (int j = 0; j < 2; j++) {
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh[j], acc[i][j], 0, 0, 0);
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl[j], acc[i][j], 0, 0, 0);
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh[j], acc[i][j], 0, 0, 0);
+            }
           }
         }
-      }
-      if (s + 1 < nsteps) {  // stage s+1 into the other buffer (read at step s-1, released by its barrier)
-        char* nxt = xl + ((s + 1) & 1) * kXStage;
         x_store<A_KC>(va, nxt, nxt + kXPart);
         x_store<B_KC>(vb, nxt + 2 * kXPart, nxt + 3 * kXPart);
-        if (s + 2 < nsteps) {
-          x_load<A_KC>(oa, oa2, m0, Meff, kb + (s + 2) * XBK, ke, va);
-          x_load<B_KC>(ob, onull, n0, g.N, kb + (s + 2) * XBK, ke, vb);
-        }
+        const int s2 = s + 2 < nsteps ? s + 2 : nsteps - 1;
+        x_load<A_KC, RAGGED, A2>(oa, oa2, m0, Meff, kb + s2 * XBK, ke, va);
+        x_load<B_KC, RAGGED, false>(ob, onull, n0, g.N, kb + s2 * XBK, ke, vb);
+        __syncthreads();
       }
-      __syncthreads();
     }
+    // epilogue, branch-free: bias / mask come in through buffer loads and
+    // results leave through buffer stores, out-of-range lanes masked by an
+    // out-of-extent offset (loads return 0, stores are dropped)
+    const XOp oc = x_op(g.C, g.ldc, (long)(g.M - 1) * g.ldc + g.N);
+    const XOp oslab = x_op(g.slab, g.N, (long)S * g.M * g.N);
+    const XOp obias = x_op(g.bias, 0, g.N);
+    const XOp omask = x_op(g.mask, g.ldm, g.mask ? (long)(g.M - 1) * g.ldm + g.N : 0);
 #pragma unroll
-    for (int i = 0; i < 4; i++)
+    for (int j = 0; j < 2; j++) {
+      const int n = n0 + wn * 64 + j * 32 + r;
+      const bool nok = n < g.N;
+      const float bv = (S == 1 && g.bias) ? x_ld1(obias, nok ? (unsigned)n * 4u : kXOob, 0) : 0.f;
 #pragma unroll
-      for (int j = 0; j < 2; j++)
+      for (int i = 0; i < 4; i++) {
+        float mv[16];
+        if (S == 1 && g.mask) {
+#pragma unroll
+          for (int q = 0; q < 16; q++) {
+            const int m = m0 + wm * 128 + i * 32 + (q & 3) + 8 * (q >> 2) + 4 * hsel;
+            mv[q] = x_ld1(omask, (nok && m < Meff) ? (unsigned)(m * g.ldm + n) * 4u : kXOob, 0);
+          }
+        }
 #pragma unroll
         for (int q = 0; q < 16; q++) {
           const int m = m0 + wm * 128 + i * 32 + (q & 3) + 8 * (q >> 2) + 4 * hsel;
-          const int n = n0 + wn * 64 + j * 32 + r;
-          if (m < Meff && n < g.N) {
-            if (S == 1) g.C[(size_t)m * g.ldc + n] = epilogue(acc[i][j][q], g, m, n);
-            else g.slab[((size_t)z * g.M + m) * g.N + n] = acc[i][j][q];
+          const bool ok = nok && m < Meff;
+          float v = acc[i][j][q];
+          if (S == 1) {
+            v += bv;
+            if (g.act == 1) v = v > 0.f ? v : 0.f;
+            if (g.mask && !(mv[q] > 0.f)) v = 0.f;
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), oc.rs,
+                                                  ok ? (unsigned)(m * g.ldc + n) * 4u : kXOob, 0, 0);
+          } else {
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), oslab.rs,
+                                                  ok ? (unsigned)((z * g.M + m) * g.N + n) * 4u : kXOob, 0, 0);
           }
         }
+      }
+    }
   }
 }
 
@@ -632,7 +677,11 @@ extern "C" int pcnn_gemm(int M, int N, int K, const float* A, const float* A2, i
   // split-bf16 path: 16-B vector staging loads, 32-bit buffer offsets
   PCNN_REQUIRE(precision == 0 || (lda % 4 == 0 && ldb % 4 == 0 && ((uintptr_t)A & 15) == 0 &&
                                   ((uintptr_t)B & 15) == 0 && (!A2 || ((uintptr_t)A2 & 15) == 0)));
-  PCNN_REQUIRE(precision == 0 || ((long)(a_trans ? K : M) * lda < (1l << 29) && (long)(b_trans ? N : K) * ldb < (1l << 29)));
+  PCNN_REQUIRE(precision == 0 || ((long)(a_trans ? K : M) * lda < (1l << 29) && (long)(b_trans ? N : K) * ldb < (1l << 29) &&
+                                  (long)M * ldc < (1l << 29) &&
+                                  (split_x3(M_dev ? 1 : M, N, K) == 1 ||
+                                   (long)split_x3(M_dev ? 1 : M, N, K) * M * N < (1l << 29)) &&
+                                  (!mask || (long)M * ldm < (1l << 29))));
   if (M == 0) return PCNN_OK;
   if (workspace_bytes < pcnn_gemm_workspace_size(M, N, K, M_dev != nullptr, precision) || !workspace)
     return PCNN_ECAPACITY;
@@ -641,22 +690,38 @@ extern "C" int pcnn_gemm(int M, int N, int K, const float* A, const float* A2, i
   if (precision == 1) {
     // persistent grid: one workgroup per CU (a multiple of 8 for the XCD-aware
     // item order); the device-side M can only shrink the item count
-    static bool attr_set = false;
-    if (!attr_set) {
-      hipFuncSetAttribute((const void*)k_gemm_x3<false, false>, hipFuncAttributeMaxDynamicSharedMemorySize, kXLds);
-      hipFuncSetAttribute((const void*)k_gemm_x3<false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, kXLds);
-      hipFuncSetAttribute((const void*)k_gemm_x3<true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, kXLds);
-      hipFuncSetAttribute((const void*)k_gemm_x3<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, kXLds);
-      attr_set = true;
-    }
+    // ragged edges: a KC operand whose K (or device-side K) is not a multiple of
+    // 4, or an NC operand whose row count is not -> element-wise edge loads
+    const bool a_kc = !a_trans, b_kc = b_trans;
+    const bool ragged = ((a_kc || b_kc) && (K % 4 != 0 || K_dev != nullptr)) || (!a_kc && M % 4 != 0) ||
+                        (!b_kc && N % 4 != 0);
     const int mt = (M + XBM - 1) / XBM, nt = (N + XBN - 1) / XBN;
-    const long cap_items = (long)mt * nt * kMaxSplit;
+    const long cap_items = (long)mt * nt * kMaxSplitX;
     long grid = cap_items < kXMaxGrid ? cap_items : kXMaxGrid;
     if (grid >= 8) grid -= grid % 8;
-    if (!a_trans && !b_trans) hipLaunchKernelGGL((k_gemm_x3<false, false>), dim3(grid), dim3(kXThreads), kXLds, st, g);
-    else if (!a_trans && b_trans) hipLaunchKernelGGL((k_gemm_x3<false, true>), dim3(grid), dim3(kXThreads), kXLds, st, g);
-    else if (a_trans && !b_trans) hipLaunchKernelGGL((k_gemm_x3<true, false>), dim3(grid), dim3(kXThreads), kXLds, st, g);
-    else hipLaunchKernelGGL((k_gemm_x3<true, true>), dim3(grid), dim3(kXThreads), kXLds, st, g);
+#define PCNN_X3_LAUNCH(AT, BT, RG, S2)                                                                  \
+  do {                                                                                                 \
+    static bool attr_set = false;                                                                      \
+    if (!attr_set) {                                                                                   \
+      hipFuncSetAttribute((const void*)k_gemm_x3<AT, BT, RG, S2>,                                      \
+                          hipFuncAttributeMaxDynamicSharedMemorySize, kXLds);                          \
+      attr_set = true;                                                                                 \
+    }                                                                                                  \
+    hipLaunchKernelGGL((k_gemm_x3<AT, BT, RG, S2>), dim3(grid), dim3(kXThreads), kXLds, st, g);        \
+  } while (0)
+#define PCNN_X3_LAYOUT(RG, S2)                                     \
+  do {                                                            \
+    if (!a_trans && !b_trans) PCNN_X3_LAUNCH(false, false, RG, S2); \
+    else if (!a_trans && b_trans) PCNN_X3_LAUNCH(false, true, RG, S2); \
+    else if (a_trans && !b_trans) PCNN_X3_LAUNCH(true, false, RG, S2); \
+    else PCNN_X3_LAUNCH(true, true, RG, S2);                       \
+  } while (0)
+    if (!ragged && !A2) PCNN_X3_LAYOUT(false, false);
+    else if (!ragged) PCNN_X3_LAYOUT(false, true);
+    else if (!A2) PCNN_X3_LAYOUT(true, false);
+    else PCNN_X3_LAYOUT(true, true);
+#undef PCNN_X3_LAYOUT
+#undef PCNN_X3_LAUNCH
   } else {
     const int mt = (M + BM - 1) / BM, nt = (N + BN - 1) / BN;
     // persistent grid sized for the capacity shape at its split

@@ -84,7 +84,10 @@ __device__ __forceinline__ void upd(float v, int idx, float& m, int& a) {
   if (v > m) { m = v; a = idx; }
 }
 
-// NHWC, all channels, C % 4 == 0: block (roi, bin), lane -> 4 channels
+// NHWC, all channels, C % 4 == 0: block (roi, bin), lane -> 4 channels.
+// ACC: top += pooled (the pool5 + pool4 sum of vgg16_convs.py:184 produced in
+// place by the second pool; the argmax of each map is still written).
+template <bool ACC>
 __global__ void __launch_bounds__(128) k_roi_fwd_nhwc4(const float* __restrict__ data, int B, int H, int W, int C,
                                                         const float* __restrict__ rois, int R_cap, int stride,
                                                         const int32_t* __restrict__ num_rois_dev, float scale, int PH,
@@ -121,7 +124,12 @@ __global__ void __launch_bounds__(128) k_roi_fwd_nhwc4(const float* __restrict__
         }
       }
     }
-    *(float4*)(to + c) = make_float4(m0, m1, m2, m3);
+    if (ACC) {
+      const float4 p = *(const float4*)(to + c);
+      *(float4*)(to + c) = make_float4(p.x + m0, p.y + m1, p.z + m2, p.w + m3);
+    } else {
+      *(float4*)(to + c) = make_float4(m0, m1, m2, m3);
+    }
     *(int4*)(ao + c) = make_int4(a0, a1, a2, a3);
   }
 }
@@ -130,7 +138,7 @@ __global__ void __launch_bounds__(128) k_roi_fwd_nhwc4(const float* __restrict__
 __global__ void k_roi_fwd_generic(const float* __restrict__ data, int B, int H, int W, int C, int layout,
                                   const float* __restrict__ rois, int R_cap, int stride,
                                   const int32_t* __restrict__ num_rois_dev, float scale, int PH, int PW,
-                                  int pool_channel, float* __restrict__ top, int32_t* __restrict__ argmax) {
+                                  int pool_channel, int acc, float* __restrict__ top, int32_t* __restrict__ argmax) {
   const int R = rows_of(num_rois_dev, R_cap);
   const int Co = pool_channel ? 1 : C;
   const long n_out = (long)R * PH * PW * Co;
@@ -164,7 +172,7 @@ __global__ void k_roi_fwd_generic(const float* __restrict__ data, int B, int H, 
           if (v > maxval) { maxval = v; maxidx = bi; }
         }
     }
-    top[idx] = maxval;
+    top[idx] = acc ? top[idx] + maxval : maxval;
     argmax[idx] = maxidx;
   }
 }
@@ -388,10 +396,9 @@ __global__ void k_roi_bwd_generic(const float* __restrict__ top_diff, const int3
 
 }  // namespace
 
-extern "C" int pcnn_roi_pool_fwd(const float* data, int B, int H, int W, int C, int layout, const float* rois,
-                                 int R_cap, int roi_stride, const int32_t* num_rois_dev, float spatial_scale,
-                                 int pooled_h, int pooled_w, int pool_channel, float* top, int32_t* argmax,
-                                 void* stream) {
+static int roi_pool_fwd(const float* data, int B, int H, int W, int C, int layout, const float* rois, int R_cap,
+                        int roi_stride, const int32_t* num_rois_dev, float spatial_scale, int pooled_h, int pooled_w,
+                        int pool_channel, int acc, float* top, int32_t* argmax, void* stream) {
   PCNN_REQUIRE(data && rois && top && argmax && B > 0 && H > 0 && W > 0 && C > 0 && R_cap >= 0);
   PCNN_REQUIRE(pooled_h > 0 && pooled_w > 0 && (layout == 0 || layout == 1));
   PCNN_REQUIRE(roi_stride >= 6 || (roi_stride == 5 && !pool_channel));
@@ -402,16 +409,37 @@ extern "C" int pcnn_roi_pool_fwd(const float* data, int B, int H, int W, int C, 
                                                                     (uintptr_t)argmax) & 15) == 0;
   if (vec) {
     const int threads = C / 4 >= 128 ? 128 : ((C / 4 + 63) / 64) * 64;
-    hipLaunchKernelGGL(k_roi_fwd_nhwc4, dim3(R_cap, pooled_h * pooled_w), dim3(threads), 0, st, data, B, H, W, C,
-                       rois, R_cap, roi_stride, num_rois_dev, spatial_scale, pooled_h, pooled_w, top, argmax);
+    if (acc)
+      hipLaunchKernelGGL(k_roi_fwd_nhwc4<true>, dim3(R_cap, pooled_h * pooled_w), dim3(threads), 0, st, data, B, H,
+                         W, C, rois, R_cap, roi_stride, num_rois_dev, spatial_scale, pooled_h, pooled_w, top, argmax);
+    else
+      hipLaunchKernelGGL(k_roi_fwd_nhwc4<false>, dim3(R_cap, pooled_h * pooled_w), dim3(threads), 0, st, data, B, H,
+                         W, C, rois, R_cap, roi_stride, num_rois_dev, spatial_scale, pooled_h, pooled_w, top, argmax);
   } else {
     const long n = (long)R_cap * pooled_h * pooled_w * (pool_channel ? 1 : C);
     const int blocks = (int)((n + 255) / 256 < 8192 ? (n + 255) / 256 : 8192);
     hipLaunchKernelGGL(k_roi_fwd_generic, dim3(blocks), dim3(256), 0, st, data, B, H, W, C, layout, rois, R_cap,
-                       roi_stride, num_rois_dev, spatial_scale, pooled_h, pooled_w, pool_channel, top, argmax);
+                       roi_stride, num_rois_dev, spatial_scale, pooled_h, pooled_w, pool_channel, acc, top, argmax);
   }
   PCNN_CHECK_LAUNCH();
   return PCNN_OK;
+}
+
+extern "C" int pcnn_roi_pool_fwd(const float* data, int B, int H, int W, int C, int layout, const float* rois,
+                                 int R_cap, int roi_stride, const int32_t* num_rois_dev, float spatial_scale,
+                                 int pooled_h, int pooled_w, int pool_channel, float* top, int32_t* argmax,
+                                 void* stream) {
+  return roi_pool_fwd(data, B, H, W, C, layout, rois, R_cap, roi_stride, num_rois_dev, spatial_scale, pooled_h,
+                      pooled_w, pool_channel, 0, top, argmax, stream);
+}
+
+extern "C" int pcnn_roi_pool_fwd_accumulate(const float* data, int B, int H, int W, int C, int layout,
+                                            const float* rois, int R_cap, int roi_stride,
+                                            const int32_t* num_rois_dev, float spatial_scale, int pooled_h,
+                                            int pooled_w, int pool_channel, float* top, int32_t* argmax,
+                                            void* stream) {
+  return roi_pool_fwd(data, B, H, W, C, layout, rois, R_cap, roi_stride, num_rois_dev, spatial_scale, pooled_h,
+                      pooled_w, pool_channel, 1, top, argmax, stream);
 }
 
 extern "C" size_t pcnn_roi_pool_bwd_workspace_size(int B, int R_cap) {

@@ -53,9 +53,8 @@ class PoseStep:
         self.hough = dict(box=torch.zeros((CAP, 7), **f32), pose=torch.zeros((CAP, 7), **f32),
                           target=torch.zeros((CAP, D), **f32), weight=torch.zeros((CAP, D), **f32),
                           domain=torch.zeros((CAP,), **i32), num_rois=torch.zeros((2,), **i32))
-        self.pool5 = torch.zeros((CAP, 7, 7, channels), **f32)
+        self.pool = torch.zeros((CAP, 7, 7, channels), **f32)  # pool5 + pool4 (vgg16_convs.py:184)
         self.arg5 = torch.zeros((CAP, 7, 7, channels), **i32)
-        self.pool4 = torch.zeros((CAP, 7, 7, channels), **f32)
         self.arg4 = torch.zeros((CAP, 7, 7, channels), **i32)
         self.y6 = torch.zeros((CAP, units), **f32)
         self.y7 = torch.zeros((CAP, units), **f32)
@@ -119,12 +118,12 @@ class PoseStep:
         w = self.weights
         K6 = 49 * self.Ch
         with self._t("roi_pool_fwd"):
-            rp.roi_pool(conv5, h["box"], 7, 7, 1.0 / 16.0, 0, num_rois=nr, out=(self.pool5, self.arg5))
-            rp.roi_pool(conv4, h["box"], 7, 7, 1.0 / 8.0, 0, num_rois=nr, out=(self.pool4, self.arg4))
-        x5 = self.pool5.view(CAP, K6)
-        x4 = self.pool4.view(CAP, K6)
+            rp.roi_pool(conv5, h["box"], 7, 7, 1.0 / 16.0, 0, num_rois=nr, out=(self.pool, self.arg5))
+            rp.roi_pool(conv4, h["box"], 7, 7, 1.0 / 8.0, 0, num_rois=nr, out=(self.pool, self.arg4),
+                        accumulate=True)  # pool = pool5 + pool4
+        x = self.pool.view(CAP, K6)
         with self._t("gemm_fc6_fwd"):
-            ph.gemm(x5, w.w6, self.y6, A2=x4, bias=w.b6, act=1, M_dev=nr, precision=self.prec)
+            ph.gemm(x, w.w6, self.y6, bias=w.b6, act=1, M_dev=nr, precision=self.prec)
         with self._t("gemm_fc7_fc8_fwd"):
             ph.gemm(self.y6, w.w7, self.y7, bias=w.b7, act=1, M_dev=nr, precision=self.prec)
             ph.gemm(self.y7, w.w8, self.y8, bias=w.b8, act=0, M_dev=nr, precision=self.prec)
@@ -152,10 +151,9 @@ class PoseStep:
             ph.gemm(self.y6, self.dy7, g["w7"], a_trans=1, K_dev=nr, M=w.units, N=w.units, K=CAP, precision=self.prec)
             ph.colsum(self.dy7, g["b7"], M_dev=nr)
             ph.gemm(self.dy7, w.w7, self.dy6, b_trans=1, mask=self.y6, M_dev=nr, precision=self.prec)
-        x5 = self.pool5.view(CAP, K6)
-        x4 = self.pool4.view(CAP, K6)
-        with self._t("gemm_fc6_dw"):  # A = pool5 + pool4, fused
-            ph.gemm(x5, self.dy6, g["w6"], a_trans=1, A2=x4, K_dev=nr, M=K6, N=w.units, K=CAP, precision=self.prec)
+        x = self.pool.view(CAP, K6)
+        with self._t("gemm_fc6_dw"):  # A = pool5 + pool4
+            ph.gemm(x, self.dy6, g["w6"], a_trans=1, K_dev=nr, M=K6, N=w.units, K=CAP, precision=self.prec)
             ph.colsum(self.dy6, g["b6"], M_dev=nr)
         with self._t("gemm_fc6_dx"):
             ph.gemm(self.dy6, w.w6, self.dx, b_trans=1, M_dev=nr, precision=self.prec)

@@ -14,7 +14,8 @@ from .. import _lib
 
 
 def roi_pool(bottom_data, bottom_rois, pooled_height, pooled_width, spatial_scale, pool_channel=0, name=None,
-             num_rois=None, layout=0, out=None):
+             num_rois=None, layout=0, out=None, accumulate=False):
+    """accumulate=True: out[0] += pooled (out required), argmax written to out[1]."""
     _lib.require_gpu(bottom_data, bottom_rois)
     if bottom_data.dim() != 4:
         raise ValueError("data must be 4-dimensional")  # roi_pooling_op.cc:92-93
@@ -30,11 +31,15 @@ def roi_pool(bottom_data, bottom_rois, pooled_height, pooled_width, spatial_scal
     Co = 1 if pool_channel else C
     shape = (R, pooled_height, pooled_width, Co) if layout == 0 else (R, Co, pooled_height, pooled_width)
     if out is None:
+        if accumulate:
+            raise ValueError("accumulate=True needs out=(top, argmax)")
         top = torch.empty(shape, dtype=torch.float32, device=data.device)
         arg = torch.empty(shape, dtype=torch.int32, device=data.device)
     else:
         top, arg = out
-    rc = _lib.load().pcnn_roi_pool_fwd(_lib.ptr(data), B, H, W, C, layout, _lib.ptr(rois), R, stride,
+    lib = _lib.load()
+    fn = lib.pcnn_roi_pool_fwd_accumulate if accumulate else lib.pcnn_roi_pool_fwd
+    rc = fn(_lib.ptr(data), B, H, W, C, layout, _lib.ptr(rois), R, stride,
                                        _lib.ptr(num_rois), float(spatial_scale), int(pooled_height),
                                        int(pooled_width), int(pool_channel), _lib.ptr(top), _lib.ptr(arg),
                                        _lib.stream_ptr())

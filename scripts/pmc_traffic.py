@@ -1,0 +1,82 @@
+"""Per-launch HBM traffic from rocprofv3 FETCH_SIZE / WRITE_SIZE passes
+(scripts/gpu_pmc.sh) -> profiles/pmc_traffic.json.
+
+FETCH_SIZE / WRITE_SIZE are in KiB per dispatch.  On gfx950 FETCH_SIZE
+counts half the bytes of wide coalesced reads (MI355X_MICROARCH.md, HBM
+section), so reads are doubled.  GEMM dispatches of one template are told
+apart by their fixed order inside a pose step (pipeline.py):
+  k_gemm_x3<false,false>: fc6_fwd, fc7_fwd, fc8_fwd
+  k_gemm_x3<true,false>:  fc8_dw, fc7_dw, fc6_dw
+  k_gemm_x3<false,true>:  fc8_dx, fc7_dx, fc6_dx
+"""
+import csv
+import json
+import os
+import re
+import sys
+from collections import defaultdict
+
+ROLES = {"k_gemm_x3<false, false>": ["fc6_fwd", "fc7_fwd", "fc8_fwd"],
+         "k_gemm_x3<true, false>": ["fc8_dw", "fc7_dw", "fc6_dw"],
+         "k_gemm_x3<false, true>": ["fc8_dx", "fc7_dx", "fc6_dx"]}
+HOUGH = ("k_label_hist", "k_label_scan", "k_label_scatter", "k_voter_setup", "k_hough_vote", "k_hough_peak",
+         "k_hough_emit")
+
+
+def short(name):
+    m = re.search(r"(k_\w+(?:<[^>]*>)?)", name)
+    return m.group(1) if m else name.split("(")[0]
+
+
+def load(path, counter):
+    per = defaultdict(list)
+    for row in csv.DictReader(open(path)):
+        if row["Counter_Name"] != counter:
+            continue
+        per[short(row["Kernel_Name"])].append((int(row["Dispatch_Id"]), float(row["Counter_Value"]) * 1024.0))
+    for k in per:
+        per[k].sort()
+    return per
+
+
+def summarize(fetch_csv, write_csv):
+    f, w = load(fetch_csv, "FETCH_SIZE"), load(write_csv, "WRITE_SIZE")
+    out = {}
+    for k in f:
+        fv = [v for _, v in f[k]]
+        wv = [v for _, v in w.get(k, [])]
+        roles = ROLES.get(k)
+        if roles:
+            for i, role in enumerate(roles):
+                fr, wr = fv[i::len(roles)], wv[i::len(roles)]
+                if fr:
+                    out[f"{k}:{role}"] = {"read_bytes": 2 * sum(fr) / len(fr),
+                                          "write_bytes": sum(wr) / max(len(wr), 1),
+                                          "dispatches": len(fr)}
+        out[k] = {"read_bytes": 2 * sum(fv) / len(fv), "write_bytes": sum(wv) / max(len(wv), 1),
+                  "dispatches": len(fv)}
+    for v in out.values():
+        v["traffic_bytes"] = v["read_bytes"] + v["write_bytes"]
+    hk = [k for k in HOUGH if k in out]
+    if hk:
+        out["hough_voting_gpu op"] = {"traffic_bytes": sum(out[k]["traffic_bytes"] for k in hk),
+                                      "kernels": hk}
+    return out
+
+
+def main():
+    root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out"
+    res = {"full": summarize(f"{root}/pmc_fetch/run_counter_collection.csv",
+                             f"{root}/pmc_write/run_counter_collection.csv"),
+           "vote_roi": summarize(f"{root}/pmc_fetch_vr/run_counter_collection.csv",
+                                 f"{root}/pmc_write_vr/run_counter_collection.csv"),
+           "note": "bytes per launch; read = 2 x FETCH_SIZE (gfx950 half-count), write = WRITE_SIZE"}
+    os.makedirs("profiles", exist_ok=True)
+    json.dump(res, open("profiles/pmc_traffic.json", "w"), indent=1, sort_keys=True)
+    for wl in ("full", "vote_roi"):
+        for k, v in sorted(res[wl].items(), key=lambda kv: -kv[1]["traffic_bytes"])[:14]:
+            print(wl, k.ljust(40), f"{v['traffic_bytes'] / 1e6:10.2f} MB")
+
+
+if __name__ == "__main__":
+    main()

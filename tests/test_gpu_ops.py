@@ -183,3 +183,22 @@ def test_gemm_ragged_padded(hip, at, bt, prec):
     ph.gemm(padded(A, at), padded(B, bt), C, a_trans=at, b_trans=bt, M=M, N=N, K=K, precision=prec)
     ref = A.astype(np.float64) @ B
     np.testing.assert_allclose(C.cpu().numpy(), ref, **_gemm_tol(prec, K))
+
+
+def test_roi_pool_accumulate(hip, orc):
+    """pool5 + pool4 produced in place by the second pool (both argmaxes kept)."""
+    rng = np.random.default_rng(9)
+    B = 2
+    c5 = rng.normal(size=(B, 30, 40, 64)).astype(np.float32)
+    c4 = rng.normal(size=(B, 60, 80, 64)).astype(np.float32)
+    rois = _rois(rng, 17, B, 30, 40, 16)
+    top = torch.empty((17, 7, 7, 64), dtype=torch.float32, device=D)
+    a5 = torch.empty((17, 7, 7, 64), dtype=torch.int32, device=D)
+    a4 = torch.empty_like(a5)
+    rp.roi_pool(T(c5), T(rois), 7, 7, 1 / 16, 0, out=(top, a5))
+    rp.roi_pool(T(c4), T(rois), 7, 7, 1 / 8, 0, out=(top, a4), accumulate=True)
+    o5, oa5 = orc.roi_pool_fwd(c5, rois, 7, 7, 1 / 16)
+    o4, oa4 = orc.roi_pool_fwd(c4, rois, 7, 7, 1 / 8)
+    np.testing.assert_array_equal(top.cpu().numpy(), o5 + o4)
+    np.testing.assert_array_equal(a5.cpu().numpy(), oa5)
+    np.testing.assert_array_equal(a4.cpu().numpy(), oa4)
