@@ -8,12 +8,11 @@
 // gradient into a (R, P, 4C) scratch (~0.64 GB at R = 432), sums both
 // sequentially per row, and reduces the row losses with thrust + a host copy.
 //
-// Here a workgroup owns (row, chunk of kPts points) with kSplit lanes per
-// point: the matrices live in registers; for symmetric classes the
-// GT-rotated model points are staged once per workgroup in LDS (float4) and
-// each point's nearest-point scan (cu.cc:150-172) is split over kSplit lanes
-// and merged as a lexicographic (distance, index) minimum — exactly the
-// reference's first minimum.  Per-point loss and the four gradient terms use
+// Here a workgroup owns (row, chunk of kPts points), one lane per point: the
+// matrices live in registers; for symmetric classes the GT-rotated model
+// points are staged once per workgroup in LDS (float4) and each lane scans
+// them in index order as wave-uniform broadcasts (cu.cc:150-172, first
+// minimum, strict <) — the reference's per-point loop, vectorised over points.  Per-point loss and the four gradient terms use
 // the reference's expressions and operation order (cu.cc:174-203) and are
 // reduced in a fixed tree -> (R, chunks, 5) partials; one workgroup folds the
 // partials per row and the rows into the scalar loss, in fixed order
@@ -25,8 +24,9 @@
 namespace {
 
 constexpr int kAddThreads = 256;
-constexpr int kSplit = 4;                      // lanes per point (symmetric search split)
-constexpr int kPts = kAddThreads / kSplit;     // points per workgroup
+constexpr int kPtsPlain = kAddThreads;         // points per partial slot (plain rows: strided)
+constexpr int kPPL = 2;                        // symmetric rows: query points per lane
+constexpr int kPts = kAddThreads * kPPL;       // points per (row, chunk) item
 constexpr int kMaxPointsLds = 8192;            // float4 candidates in LDS (128 KB)
 
 __device__ __forceinline__ int rows_of(const int32_t* dev, int cap) {
@@ -64,15 +64,17 @@ __global__ void __launch_bounds__(kAddThreads) k_add_rows(const float* __restric
                                                            float margin, int norm_rows,
                                                            const int32_t* __restrict__ norm_rows_dev, int nchunk,
                                                            const int32_t* __restrict__ rcls,
+                                                           const int32_t* __restrict__ sym_rows,
+                                                           const int32_t* __restrict__ nsym,
                                                            float* __restrict__ partial) {
-  extern __shared__ __attribute__((aligned(16))) float4 gpts[];  // [P] GT-rotated points (symmetric rows)
+  extern __shared__ __attribute__((aligned(16))) float4 gpts[];  // [P] GT-rotated points
   __shared__ float red[kAddThreads / 64][5];
-  const int n = blockIdx.y, chunk = blockIdx.x;
   const int R = rows_of(num_rois_dev, R_cap);
-  if (n >= R) return;
+  const int items = *nsym * nchunk;
+  for (int item = blockIdx.x; item < items; item += gridDim.x) {
+  const int n = sym_rows[item / nchunk], chunk = item % nchunk;
   const int PC = 4 * C;
   const int cls = rcls[n];
-  if (cls < 0 || !(symmetry[cls] > 0)) return;  // k_add_rows_plain handles these rows
   float* out = partial + ((size_t)n * nchunk + chunk) * 5;
   const float* tq = target + (size_t)n * PC + 4 * cls;
   const float* pq = pred + (size_t)n * PC + 4 * cls;
@@ -90,45 +92,65 @@ __global__ void __launch_bounds__(kAddThreads) k_add_rows(const float* __restric
     }
     __syncthreads();
   }
-  const int sub = threadIdx.x & (kSplit - 1);
-  const int p = chunk * kPts + (threadIdx.x / kSplit);
-  const bool live = p < P;
-  const int pp = live ? p : 0;
-  const float X0 = pts[pp * 3 + 0], X1 = pts[pp * 3 + 1], X2 = pts[pp * 3 + 2];
-  const float x1 = Rp[0] * X0 + Rp[1] * X1 + Rp[2] * X2;
-  const float y1 = Rp[3] * X0 + Rp[4] * X1 + Rp[5] * X2;
-  const float z1 = Rp[6] * X0 + Rp[7] * X1 + Rp[8] * X2;
-  float x2, y2, z2;
-  if (sym) {
-    float dmin = FLT_MAX;
-    int imin = 0x7fffffff;
-    for (int i = sub; i < P; i += kSplit) {
-      const float4 a = gpts[i];
-      const float dist = (x1 - a.x) * (x1 - a.x) + (y1 - a.y) * (y1 - a.y) + (z1 - a.z) * (z1 - a.z);
-      if (dist < dmin) { dmin = dist; imin = i; }  // first minimum within this lane's stride
-    }
+  // kPPL query points per lane (points p0 + k*kAddThreads): each broadcast
+  // candidate read serves kPPL distances and the lane carries kPPL
+  // independent first-minimum chains
+  float qx[kPPL], qy[kPPL], qz[kPPL], Xq[kPPL][3];
+  int pq_[kPPL];
 #pragma unroll
-    for (int o = 1; o < kSplit; o <<= 1) {  // lexicographic (dist, index) min over the point's lanes
-      const float od = __shfl_xor(dmin, o, 64);
-      const int oi = __shfl_xor(imin, o, 64);
-      if (od < dmin || (od == dmin && oi < imin)) { dmin = od; imin = oi; }
+  for (int k = 0; k < kPPL; k++) {
+    const int p = chunk * kPts + k * kAddThreads + threadIdx.x;
+    pq_[k] = p;
+    const int pp = p < P ? p : 0;
+    Xq[k][0] = pts[pp * 3 + 0]; Xq[k][1] = pts[pp * 3 + 1]; Xq[k][2] = pts[pp * 3 + 2];
+    qx[k] = Rp[0] * Xq[k][0] + Rp[1] * Xq[k][1] + Rp[2] * Xq[k][2];
+    qy[k] = Rp[3] * Xq[k][0] + Rp[4] * Xq[k][1] + Rp[5] * Xq[k][2];
+    qz[k] = Rp[6] * Xq[k][0] + Rp[7] * Xq[k][1] + Rp[8] * Xq[k][2];
+  }
+  // nearest GT-rotated model point, scanned in index order with a strict <
+  // (cu.cc:150-172: the first minimum); candidates are wave-uniform LDS
+  // broadcasts, eight in flight per iteration
+  float dmin[kPPL];
+  int imin[kPPL];
+#pragma unroll
+  for (int k = 0; k < kPPL; k++) { dmin[k] = FLT_MAX; imin[k] = -1; }
+  int i = 0;
+  for (; i + 8 <= P; i += 8) {
+    float4 c[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) c[j] = gpts[i + j];
+#pragma unroll
+    for (int j = 0; j < 8; j++)
+#pragma unroll
+      for (int k = 0; k < kPPL; k++) {
+        const float dist = (qx[k] - c[j].x) * (qx[k] - c[j].x) + (qy[k] - c[j].y) * (qy[k] - c[j].y) +
+                           (qz[k] - c[j].z) * (qz[k] - c[j].z);
+        if (dist < dmin[k]) { dmin[k] = dist; imin[k] = i + j; }
+      }
+  }
+  for (; i < P; i++) {
+    const float4 c = gpts[i];
+#pragma unroll
+    for (int k = 0; k < kPPL; k++) {
+      const float dist = (qx[k] - c.x) * (qx[k] - c.x) + (qy[k] - c.y) * (qy[k] - c.y) + (qz[k] - c.z) * (qz[k] - c.z);
+      if (dist < dmin[k]) { dmin[k] = dist; imin[k] = i; }
     }
-    if (imin == 0x7fffffff) imin = pp;  // no finite distance (reference leaves index_min unset)
-    const float4 a = gpts[imin];
-    x2 = a.x; y2 = a.y; z2 = a.z;
-  } else {
-    x2 = Rg[0] * X0 + Rg[1] * X1 + Rg[2] * X2;
-    y2 = Rg[3] * X0 + Rg[4] * X1 + Rg[5] * X2;
-    z2 = Rg[6] * X0 + Rg[7] * X1 + Rg[8] * X2;
   }
   float acc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
-  if (live && sub == 0) {
+#pragma unroll
+  for (int k = 0; k < kPPL; k++) {
+    if (pq_[k] >= P) continue;
+    const int im = imin[k] < 0 ? pq_[k] : imin[k];  // no finite distance (index_min unset in the reference)
+    const float4 cm = gpts[im];
+    const float x1 = qx[k], y1 = qy[k], z1 = qz[k], x2 = cm.x, y2 = cm.y, z2 = cm.z;
+    const float X0 = Xq[k][0], X1 = Xq[k][1], X2 = Xq[k][2];
+    {
     const int Rn = norm_rows_dev ? *norm_rows_dev : (norm_rows > 0 ? norm_rows : R);
     const float bn = (float)(Rn * P);
     const double ln = 2.0 * (double)Rn * (double)P;
     const float dist = (x1 - x2) * (x1 - x2) + (y1 - y2) * (y1 - y2) + (z1 - z2) * (z1 - z2);
     if (!(dist < margin)) {  // cu.cc:178-179
-      acc[0] = (float)((double)(dist - margin) / ln);  // cu.cc:181
+      acc[0] += (float)((double)(dist - margin) / ln);  // cu.cc:181
       // derivative matrices of Rp w.r.t. (s, u, v, w) (cu.cc:97-139)
       const float d0[9] = {2 * s, -2 * w, 2 * v, 2 * w, 2 * s, -2 * u, -2 * v, 2 * u, 2 * s};
       const float d1[9] = {2 * u, 2 * v, 2 * w, 2 * v, -2 * u, -2 * s, 2 * w, 2 * s, -2 * u};
@@ -136,16 +158,19 @@ __global__ void __launch_bounds__(kAddThreads) k_add_rows(const float* __restric
       const float d3[9] = {-2 * w, -2 * s, 2 * u, 2 * s, -2 * w, 2 * v, 2 * u, 2 * v, 2 * w};
       const float X[3] = {X0, X1, X2};
       const float df[3] = {x1 - x2, y1 - y2, z1 - z2};
+      float e0 = 0.f, e1 = 0.f, e2 = 0.f, e3 = 0.f;  // this point's terms, reference order
 #pragma unroll
-      for (int j = 0; j < 3; j++)
+      for (int a = 0; a < 3; a++)
 #pragma unroll
-        for (int k = 0; k < 3; k++) {  // cu.cc:183-203, same operation order
-          acc[1] += df[j] * X[k] * d0[j * 3 + k] / bn;
-          acc[2] += df[j] * X[k] * d1[j * 3 + k] / bn;
-          acc[3] += df[j] * X[k] * d2[j * 3 + k] / bn;
-          acc[4] += df[j] * X[k] * d3[j * 3 + k] / bn;
+        for (int b = 0; b < 3; b++) {  // cu.cc:183-203, same operation order
+          e0 += df[a] * X[b] * d0[a * 3 + b] / bn;
+          e1 += df[a] * X[b] * d1[a * 3 + b] / bn;
+          e2 += df[a] * X[b] * d2[a * 3 + b] / bn;
+          e3 += df[a] * X[b] * d3[a * 3 + b] / bn;
         }
+      acc[1] += e0; acc[2] += e1; acc[3] += e2; acc[4] += e3;
     }
+  }
   }
 #pragma unroll
   for (int q = 0; q < 5; q++) acc[q] = pcnn::wave_sum(acc[q]);
@@ -158,13 +183,45 @@ __global__ void __launch_bounds__(kAddThreads) k_add_rows(const float* __restric
     for (int i = 0; i < (int)(blockDim.x >> 6); i++) t += red[i][threadIdx.x];
     out[threadIdx.x] = t;
   }
+  __syncthreads();  // red / gpts reused by the next item
+  }
 }
 
-// Row classes once (first class with weight > 0, cu.cc:47-52).
-__global__ void k_add_prep(const float* __restrict__ weight, int R_cap, const int32_t* __restrict__ num_rois_dev,
-                           int C, int32_t* __restrict__ rcls) {
+// Row classes once (first class with weight > 0, cu.cc:47-52) and the
+// ascending list of symmetric rows (ballot scan, one workgroup: deterministic).
+__global__ void __launch_bounds__(1024) k_add_prep(const float* __restrict__ weight, const float* __restrict__ symmetry,
+                                                    int R_cap, const int32_t* __restrict__ num_rois_dev, int C,
+                                                    int32_t* __restrict__ rcls, int32_t* __restrict__ sym_rows,
+                                                    int32_t* __restrict__ nsym) {
+  __shared__ int wcount[16];
+  __shared__ int base;
   const int R = rows_of(num_rois_dev, R_cap);
-  for (int n = blockIdx.x * blockDim.x + threadIdx.x; n < R; n += gridDim.x * blockDim.x) rcls[n] = row_class(weight, n, C);
+  const int lane = pcnn::lane_id(), wave = threadIdx.x >> 6;
+  if (threadIdx.x == 0) base = 0;
+  __syncthreads();
+  for (int n0 = 0; n0 < R; n0 += blockDim.x) {
+    const int n = n0 + threadIdx.x;
+    int cls = -1;
+    if (n < R) {
+      cls = row_class(weight, n, C);
+      rcls[n] = cls;
+    }
+    const bool sym = n < R && cls >= 0 && symmetry[cls] > 0;
+    const uint64_t m = __ballot(sym);
+    if (lane == 0) wcount[wave] = __popcll(m);
+    __syncthreads();
+    int off = base;
+    for (int w = 0; w < wave; w++) off += wcount[w];
+    if (sym) sym_rows[off + __popcll(m & pcnn::lanemask_lt())] = n;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int t = 0;
+      for (int w = 0; w < (int)(blockDim.x >> 6); w++) t += wcount[w];
+      base += t;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *nsym = base;
 }
 
 // Non-symmetric rows (and rows without weight): one workgroup per row, points
@@ -303,8 +360,8 @@ extern "C" size_t pcnn_add_loss_workspace_size(int R_cap, int C, int P) {
   (void)C;
   const int nchunk = (P + kPts - 1) / kPts;
   const size_t R = (size_t)(R_cap > 0 ? R_cap : 1);
-  return pcnn::align_up(R * nchunk * 5 * sizeof(float), 256) + pcnn::align_up(R * sizeof(int32_t), 256) +
-         pcnn::align_up(R * sizeof(float), 256) + 256;
+  return pcnn::align_up(R * nchunk * 5 * sizeof(float), 256) + 2 * pcnn::align_up(R * sizeof(int32_t), 256) +
+         pcnn::align_up(R * sizeof(float), 256) + 2 * 256;
 }
 
 extern "C" int pcnn_add_loss_fwd(const float* pred, const float* target, const float* weight, const float* points,
@@ -319,13 +376,19 @@ extern "C" int pcnn_add_loss_fwd(const float* pred, const float* target, const f
   pcnn::Carve cv(workspace);
   float* partial = cv.take<float>((size_t)R_cap * nchunk * 5);
   int32_t* rcls = cv.take<int32_t>(R_cap);
+  int32_t* sym_rows = cv.take<int32_t>(R_cap);
+  int32_t* nsym = cv.take<int32_t>(1);
   float* row_loss = cv.take<float>(R_cap);
-  hipLaunchKernelGGL(k_add_prep, dim3((R_cap + 255) / 256), dim3(256), 0, st, weight, R_cap, num_rois_dev, C, rcls);
+  hipLaunchKernelGGL(k_add_prep, dim3(1), dim3(1024), 0, st, weight, symmetry, R_cap, num_rois_dev, C, rcls,
+                     sym_rows, nsym);
   hipLaunchKernelGGL(k_add_rows_plain, dim3(R_cap), dim3(kAddThreads), 0, st, pred, target, points, symmetry, R_cap,
                      num_rois_dev, C, P, margin, loss_norm_rows, loss_norm_rows_dev, nchunk, rcls, partial);
-  hipLaunchKernelGGL(k_add_rows, dim3(nchunk, R_cap), dim3(kAddThreads), (size_t)P * sizeof(float4), st, pred,
+  // symmetric rows: persistent grid over (row, chunk) items of the device-side list
+  const long sym_items = (long)R_cap * nchunk;
+  const int sym_grid = (int)(sym_items < 1024 ? sym_items : 1024);
+  hipLaunchKernelGGL(k_add_rows, dim3(sym_grid), dim3(kAddThreads), (size_t)P * sizeof(float4), st, pred,
                      target, weight, points, symmetry, R_cap, num_rois_dev, C, P, margin, loss_norm_rows,
-                     loss_norm_rows_dev, nchunk, rcls, partial);
+                     loss_norm_rows_dev, nchunk, rcls, sym_rows, nsym, partial);
   hipLaunchKernelGGL(k_add_finish_rows, dim3((R_cap + 3) / 4), dim3(256), 0, st, R_cap, num_rois_dev, C, nchunk,
                      rcls, partial, row_loss, bottom_diff);
   hipLaunchKernelGGL(k_add_total, dim3(1), dim3(1024), 0, st, R_cap, num_rois_dev, row_loss, loss);
