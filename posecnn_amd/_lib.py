@@ -12,7 +12,7 @@ import threading
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libposecnn_hip.so")
+LIB_PATH = os.environ.get("POSECNN_HIP_LIB") or os.path.join(_HERE, "libposecnn_hip.so")  # override: experiments
 
 _lib = None
 _lock = threading.Lock()

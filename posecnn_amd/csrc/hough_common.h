@@ -37,9 +37,12 @@ struct HoughWs {
   int32_t* vcount;    // [B][C] voters of class c (0 when not voted)
   float4* vdat;       // [B][VCAP] (u, v, d, T)
   int32_t* vpos;      // [B][VCAP] y*W + x
-  double4* vcone;     // [B][VCAP] row-bound slopes (outer s1, s2, inner s1, s2)
+  float4* vcone;      // [B][VCAP] row-bound slopes (outer s1, s2, inner s1, s2), |s| <= 1e30
   int32_t* vcode;     // [B][VCAP] bound codes | kSlowVoter | kDeadVoter
   unsigned long long* key;  // [B][C] argmax key per slot
+  int32_t* rowstart;  // [B][C][H+1] per slot: first voter (slot-relative) with row >= r
+  int32_t* kmax;      // [B][C] per slot: largest box radius of its voters
+  int32_t* yspan;     // [B][C][2] per slot: rows of its first and last voter (rowstart valid in between)
   float* peak;        // [B][PKS][8] count, distance, 2bb_h, 2bb_w, cx, cy, slot
   int32_t* counts;    // [B][C-1][H*W] (NMS path)
   int32_t* ncand;     // [B]
@@ -67,9 +70,12 @@ inline HoughWs carve_ws(void* base, int B, int H, int W, int C, int skip, bool n
   ws.vcount = cv.take<int32_t>((size_t)B * C);
   ws.vdat = cv.take<float4>((size_t)B * ws.vcap);
   ws.vpos = cv.take<int32_t>((size_t)B * ws.vcap);
-  ws.vcone = cv.take<double4>((size_t)B * ws.vcap);
+  ws.vcone = cv.take<float4>((size_t)B * ws.vcap);
   ws.vcode = cv.take<int32_t>((size_t)B * ws.vcap);
   ws.key = cv.take<unsigned long long>((size_t)B * C);
+  ws.rowstart = cv.take<int32_t>((size_t)B * C * (H + 1));
+  ws.kmax = cv.take<int32_t>((size_t)B * C);
+  ws.yspan = cv.take<int32_t>((size_t)B * C * 2);
   ws.peak = cv.take<float>((size_t)B * ws.pks * 8);
   ws.ncand = cv.take<int32_t>(B);
   if (nms) {
@@ -174,6 +180,122 @@ __device__ __forceinline__ float box_overlap(int cls, const float* __restrict__ 
   return iou4(box, gtb);
 }
 
+// ---------------------------------------------------------------------------
+// RoI rows of one kept maximum (compute_rois_kernel, cu.cc:386-576), written
+// by all threads of the calling workgroup: `rpm` rows (9 in train mode) from
+// output row r0.  Box = x -+ bb * (0.5 + 0.05) in double (cu.cc:417-420);
+// pose from the mean distance (cu.cc:404-410); train mode: the first
+// same-(image, class) GT whose projected box overlaps > 0.2 (cu.cc:440-466,
+// found as a min over the qualifying GT indices) sets targets / weights on
+// all rows, 8 jittered boxes of 0.05 w/h (cu.cc:468-554), domain = (no GT).
+struct EmitShared {
+  float box[4], pose[3];
+  int gsel;
+};
+
+__device__ __forceinline__ void emit_max(EmitShared& sh, int r0, int cap, int batch_index, int cls, float score,
+                                         float bb_distance, float bb_height, float bb_width, int x, int y,
+                                         int is_train, int C, const float* __restrict__ extents,
+                                         const float* __restrict__ mb, const float* __restrict__ gt, int num_gt,
+                                         float* __restrict__ top_box, float* __restrict__ top_pose,
+                                         float* __restrict__ top_target, float* __restrict__ top_weight,
+                                         int32_t* __restrict__ top_domain, int32_t* __restrict__ diag) {
+  const int rpm = is_train ? 9 : 1;
+  const int PC = 4 * C;
+  if (threadIdx.x == 0) {
+    const float fx = mb[0], fy = mb[4], px = mb[2], py = mb[5];
+    const float rx = ((float)x - px) / fx;  // cu.cc:404-405
+    const float ry = ((float)y - py) / fy;
+    const double sc = 0.5 + (double)0.05f;
+    sh.box[0] = (float)((double)x - (double)bb_width * sc);
+    sh.box[1] = (float)((double)y - (double)bb_height * sc);
+    sh.box[2] = (float)((double)x + (double)bb_width * sc);
+    sh.box[3] = (float)((double)y + (double)bb_height * sc);
+    sh.pose[0] = rx * bb_distance;
+    sh.pose[1] = ry * bb_distance;
+    sh.pose[2] = bb_distance;
+    sh.gsel = 0x7fffffff;
+  }
+  __syncthreads();
+  if (is_train) {
+    for (int i = threadIdx.x; i < num_gt; i += blockDim.x) {
+      const int gt_batch = (int)gt[i * 13 + 0];
+      const int gt_id = (int)gt[i * 13 + 1];
+      if (cls == gt_id && batch_index == gt_batch) {
+        const float ov = box_overlap(cls, extents, mb, gt + (size_t)i * 13, sh.box);
+        if ((double)ov > 0.2) atomicMin(&sh.gsel, i);
+      }
+    }
+  }
+  __syncthreads();
+  const int g = sh.gsel == 0x7fffffff ? -1 : sh.gsel;
+  // jitter order of cu.cc:476-554: (0,0) then (-,-) (+,-) (-,+) (+,+) (0,-) (-,0) (0,+) (+,0)
+  const int jx[9] = {0, -1, 1, -1, 1, 0, -1, 0, 1};
+  const int jy[9] = {0, -1, -1, 1, 1, -1, 0, 1, 0};
+  for (int j = threadIdx.x; j < rpm; j += blockDim.x) {
+    const int r = r0 + j;
+    if (r >= cap) {
+      atomicAdd(&diag[2], 1);
+      continue;
+    }
+    float* bo = top_box + (size_t)r * 7;
+    const float x1 = sh.box[0], y1 = sh.box[1];
+    bo[0] = (float)batch_index;
+    bo[1] = (float)cls;
+    if (j == 0) {
+      bo[2] = x1; bo[3] = y1; bo[4] = sh.box[2]; bo[5] = sh.box[3];
+    } else {
+      const float ww = sh.box[2] - x1, hh = sh.box[3] - y1;
+      const float nx = jx[j] == 0 ? x1 : (float)((double)x1 + (jx[j] < 0 ? -0.05 : 0.05) * (double)ww);
+      const float ny = jy[j] == 0 ? y1 : (float)((double)y1 + (jy[j] < 0 ? -0.05 : 0.05) * (double)hh);
+      bo[2] = nx;
+      bo[3] = ny;
+      bo[4] = nx + ww;
+      bo[5] = ny + hh;
+    }
+    bo[6] = score;
+    float* po = top_pose + (size_t)r * 7;
+    po[0] = 1.f; po[1] = 0.f; po[2] = 0.f; po[3] = 0.f;
+    po[4] = sh.pose[0];
+    po[5] = sh.pose[1];
+    po[6] = sh.pose[2];
+    top_domain[r] = is_train ? (num_gt == 0 ? 1 : 0) : 0;
+  }
+  const int ncol = rpm * PC;
+  for (int idx = threadIdx.x; idx < ncol; idx += blockDim.x) {
+    const int j = idx / PC, col = idx % PC;
+    const int r = r0 + j;
+    if (r >= cap) continue;
+    const bool on = g >= 0 && col >= 4 * cls && col < 4 * cls + 4;
+    top_target[(size_t)r * PC + col] = on ? gt[g * 13 + 6 + (col - 4 * cls)] : 0.f;
+    top_weight[(size_t)r * PC + col] = on ? 1.f : 0.f;
+  }
+}
+
+// Row count (+ the dummy all-zero row when no RoI, hough_voting_gpu_op.cc:382-383).
+__device__ __forceinline__ void emit_count(int total, int cap, int C, float* __restrict__ top_box,
+                                           float* __restrict__ top_pose, float* __restrict__ top_target,
+                                           float* __restrict__ top_weight, int32_t* __restrict__ top_domain,
+                                           int32_t* __restrict__ num_rois) {
+  const int PC = 4 * C;
+  if (threadIdx.x == 0) {
+    const int n = total < cap ? total : cap;
+    num_rois[0] = n;
+    num_rois[1] = n > 0 ? n : 1;
+  }
+  if (total == 0) {
+    for (int t = threadIdx.x; t < 7; t += blockDim.x) {
+      top_box[t] = 0.f;
+      top_pose[t] = 0.f;
+    }
+    for (int t = threadIdx.x; t < PC; t += blockDim.x) {
+      top_target[t] = 0.f;
+      top_weight[t] = 0.f;
+    }
+    if (threadIdx.x == 0) top_domain[0] = 0;
+  }
+}
+
 // largest integer k with k < T (the box test |dx| < T on integer dx), or -1.
 __device__ __forceinline__ int box_radius(float T) {
   if (!(T > 0.f)) return -1;
@@ -202,10 +324,14 @@ __global__ void k_label_scan(int C, int label_thr, int index_size, int nms, int 
 __global__ void k_label_scatter(const int32_t* __restrict__ label, const float* __restrict__ vertex,
                                 const float* __restrict__ extents, const float* __restrict__ meta, int num_meta,
                                 int H, int W, int C, int skip, HoughWs ws);
-__global__ void k_voter_setup(float inlier, double so, double si, HoughWs ws);
+__global__ void k_voter_setup(int H, int W, int C, float inlier, double so, double si, HoughWs ws);
 __global__ void k_hough_vote(int H, int W, int C, float inlier, HoughWs ws, int32_t* __restrict__ counts_out);
-__global__ void k_hough_peak(int H, int W, int C, float inlier, const float* __restrict__ extents,
-                             const float* __restrict__ meta, int num_meta, HoughWs ws);
+__global__ void k_hough_peak(int B, int H, int W, int C, float inlier, const float* __restrict__ extents,
+                             const float* __restrict__ meta, int num_meta, HoughWs ws, int is_train, int batch_base,
+                             const float* __restrict__ gt, int num_gt, float* __restrict__ top_box,
+                             float* __restrict__ top_pose, float* __restrict__ top_target,
+                             float* __restrict__ top_weight, int32_t* __restrict__ top_domain,
+                             int32_t* __restrict__ num_rois, int cap);
 __global__ void k_hough_nms_cand(int H, int W, int C, float vote_thr, HoughWs ws);
 __global__ void k_hough_cand_data(int H, int W, int C, float inlier, const float* __restrict__ extents,
                                   const float* __restrict__ meta, int num_meta, HoughWs ws);

@@ -83,6 +83,7 @@ __global__ void __launch_bounds__(1024) k_label_scan(int C, int label_thr, int i
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
     ws.total[(size_t)b * C + c] = tot[c];
     ws.key[(size_t)b * C + c] = 0ull;
+    ws.kmax[(size_t)b * C + c] = -1;
     ws.vcount[(size_t)b * C + c] = 0;
     ws.vbase[(size_t)b * C + c] = 0;
   }
@@ -183,33 +184,79 @@ __global__ void __launch_bounds__(kCompactThreads) k_label_scatter(const int32_t
 
 // Cone row-bound slopes of every voter (one thread per voter): outer / inner
 // cone at the inlier threshold -/+ kConeEps (so / si = sqrt(1 - c^2) of each).
-__global__ void __launch_bounds__(256) k_voter_setup(float inlier, double so, double si, HoughWs ws) {
+// Also the per-slot row index of the (raster-ordered) voter list, rowstart[r]
+// = first voter with row >= r for rows r in [yfirst, ylast] (yspan), and the
+// slot's largest box radius: a vote band [y0, y1) then only visits voters
+// with rows in [y0 - kmax, y1 - 1 + kmax].
+__global__ void __launch_bounds__(256) k_voter_setup(int H, int W, int C, float inlier, double so, double si,
+                                                      HoughWs ws) {
   const int b = blockIdx.y;
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= ws.nvtot[b]) return;
-  const size_t vi = (size_t)b * ws.vcap + i;
-  const float4 q = ws.vdat[vi];
-  const double c = (double)inlier;
-  const bool fast_ok = c > 0.05 && c < 0.999;
-  const float u = q.x, v = q.y;
-  const float n1f = sqrtf(u * u + v * v);
-  int code = 0;
-  double4 sl = make_double4(0.0, 0.0, 0.0, 0.0);
-  if (box_radius(q.w) < 0) {
-    code = kDeadVoter;
-  } else if (!fast_ok || !(n1f >= 1e-18f && n1f <= 1e18f)) {
-    code = kSlowVoter;
-  } else {
-    const double ud = u, vd = v;
-    const double nd = sqrt(ud * ud + vd * vd);
-    const double ex = ud / nd, ey = vd / nd;
-    int c0, c1, c2, c3;
-    bound_setup(ex, ey, c - kConeEps, so, sl.x, c0, sl.y, c1);  // outer cone
-    bound_setup(ex, ey, c + kConeEps, si, sl.z, c2, sl.w, c3);  // inner cone
-    code = c0 | (c1 << 2) | (c2 << 4) | (c3 << 6);
+  const bool in = i < ws.nvtot[b];
+  int k = -1, kslot = 0;
+  if (in) {
+    const size_t vi = (size_t)b * ws.vcap + i;
+    const float4 q = ws.vdat[vi];
+    const double c = (double)inlier;
+    const bool fast_ok = c > 0.05 && c < 0.999;
+    const float u = q.x, v = q.y;
+    const float n1f = sqrtf(u * u + v * v);
+    int code = 0;
+    double sl[4] = {0.0, 0.0, 0.0, 0.0};
+    k = box_radius(q.w);
+    if (k < 0) {
+      code = kDeadVoter;
+    } else if (!fast_ok || !(n1f >= 1e-18f && n1f <= 1e18f)) {
+      code = kSlowVoter;
+    } else {
+      const double ud = u, vd = v;
+      const double nd = sqrt(ud * ud + vd * vd);
+      const double ex = ud / nd, ey = vd / nd;
+      int c0, c1, c2, c3;
+      bound_setup(ex, ey, c - kConeEps, so, sl[0], c0, sl[1], c1);  // outer cone
+      bound_setup(ex, ey, c + kConeEps, si, sl[2], c2, sl[3], c3);  // inner cone
+      code = c0 | (c1 << 2) | (c2 << 4) | (c3 << 6);
+    }
+    // slopes are evaluated in float per row (hough_vote.hip): the float error
+    // of an interval end is <= ~2.6% of the +-kConeEps margin in x there
+    auto cl = [](double v) { return (float)(v > 1e30 ? 1e30 : (v < -1e30 ? -1e30 : v)); };
+    ws.vcone[vi] = make_float4(cl(sl[0]), cl(sl[1]), cl(sl[2]), cl(sl[3]));
+    ws.vcode[vi] = code;
+    // slot of voter i (slots occupy consecutive voter ranges in slot order)
+    const int nvote = ws.nvote[b];
+    int slot = 0, base = 0, cnt = 0;
+    for (int s = 0; s < nvote; s++) {
+      const int cls = ws.slot_cls[(size_t)b * C + s];
+      base = ws.vbase[(size_t)b * C + cls];
+      cnt = ws.vcount[(size_t)b * C + cls];
+      slot = s;
+      if (i < base + cnt) break;
+    }
+    const int j = i - base;
+    const int y = ws.vpos[vi] / W;
+    const int yprev = j > 0 ? ws.vpos[vi - 1] / W : -1;
+    int32_t* rs = ws.rowstart + ((size_t)b * C + slot) * (H + 1);
+    if (j == 0) {
+      rs[y] = 0;
+      ws.yspan[((size_t)b * C + slot) * 2] = y;
+    } else {
+      for (int r = yprev + 1; r <= y; r++) rs[r] = j;  // rows (yprev, y]: usually 0 or 1
+    }
+    if (j == cnt - 1) ws.yspan[((size_t)b * C + slot) * 2 + 1] = y;
+    kslot = slot;
   }
-  ws.vcone[vi] = sl;
-  ws.vcode[vi] = code;
+  // slot max of k: lanes grouped by slot (a wave spans at most a few slots),
+  // one atomic per (wave, slot) group
+  uint64_t active = __ballot(in && k >= 0);
+  while (active) {
+    const int leader = __ffsll((long long)active) - 1;
+    const int s0 = __shfl(kslot, leader, 64);
+    const uint64_t m = __ballot(in && k >= 0 && kslot == s0);
+    int kk = (in && k >= 0 && kslot == s0) ? k : -1;
+    kk = pcnn::wave_max(kk);
+    if (pcnn::lane_id() == leader) atomicMax(ws.kmax + (size_t)b * C + s0, kk);
+    active &= ~m;
+  }
 }
 
 }  // namespace pcnn_hough

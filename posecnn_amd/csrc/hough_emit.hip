@@ -17,10 +17,8 @@
 
 namespace pcnn_hough {
 
-constexpr int kEmitMax = 256;  // maxima per image (>= pks)
-
-// One workgroup per image: per-max geometry first (box, GT match), then the
-// image's rows written by all threads (coalesced target / weight rows).
+// Multi-instance (NMS) path and the no-slot case: one workgroup per image,
+// its kept maxima in selection order (ascending flat (slot, y, x), cu.cc:351-380).
 __global__ void __launch_bounds__(kEmitThreads) k_hough_emit(int B, int H, int W, int C, int is_train,
                                                               int batch_base, int nms,
                                                               const float* __restrict__ extents,
@@ -32,14 +30,10 @@ __global__ void __launch_bounds__(kEmitThreads) k_hough_emit(int B, int H, int W
                                                               float* __restrict__ top_weight,
                                                               int32_t* __restrict__ top_domain,
                                                               int32_t* __restrict__ num_rois, int cap) {
-  __shared__ float s_box[kEmitMax][4];
-  __shared__ float s_pose[kEmitMax][3];
-  __shared__ float s_score[kEmitMax];
-  __shared__ int s_cls[kEmitMax], s_gsel[kEmitMax];
+  __shared__ EmitShared esh;
   __shared__ int s_off, s_total;
   const int b = blockIdx.x;
   const int rpm = is_train ? 9 : 1;
-  const int PC = 4 * C;
   if (threadIdx.x == 0) {
     int off = 0, tot = 0;
     for (int i = 0; i < B; i++) {
@@ -49,111 +43,18 @@ __global__ void __launch_bounds__(kEmitThreads) k_hough_emit(int B, int H, int W
     s_off = off;
     s_total = tot;
   }
-  const int nk = min(ws.nvote[b], kEmitMax);
+  __syncthreads();
+  const int nk = ws.nvote[b];
   const float* mb = meta + (size_t)b * num_meta;
-  const int batch_index = batch_base + b;
-  for (int k = threadIdx.x; k < nk; k += blockDim.x) {
+  for (int k = 0; k < nk; k++) {
     const float* pk = ws.peak + ((size_t)b * ws.pks + k) * 8;
     const int slot = nms ? (int)pk[6] : k;
     const int cls = ws.slot_cls[(size_t)b * C + slot];
-    const float bb_distance = pk[1], bb_height = pk[2], bb_width = pk[3];
-    const int x = (int)pk[4], y = (int)pk[5];
-    const float fx = mb[0], fy = mb[4], px = mb[2], py = mb[5];
-    const float rx = ((float)x - px) / fx;  // cu.cc:404-405
-    const float ry = ((float)y - py) / fy;
-    const double sc = 0.5 + (double)0.05f;  // x - bb_width * (0.5 + scale), evaluated in double (cu.cc:417-420)
-    float bx[4];
-    bx[0] = (float)((double)x - (double)bb_width * sc);
-    bx[1] = (float)((double)y - (double)bb_height * sc);
-    bx[2] = (float)((double)x + (double)bb_width * sc);
-    bx[3] = (float)((double)y + (double)bb_height * sc);
-    int gsel = -1;
-    if (is_train) {  // first same-(b, cls) GT whose projected box overlaps > 0.2 (cu.cc:440-466)
-      for (int i = 0; i < num_gt; i++) {
-        const int gt_batch = (int)gt[i * 13 + 0];
-        const int gt_id = (int)gt[i * 13 + 1];
-        if (cls == gt_id && batch_index == gt_batch) {
-          const float ov = box_overlap(cls, extents, mb, gt + (size_t)i * 13, bx);
-          if ((double)ov > 0.2) {
-            gsel = i;
-            break;
-          }
-        }
-      }
-    }
-    for (int t = 0; t < 4; t++) s_box[k][t] = bx[t];
-    s_pose[k][0] = rx * bb_distance;
-    s_pose[k][1] = ry * bb_distance;
-    s_pose[k][2] = bb_distance;
-    s_score[k] = pk[0];
-    s_cls[k] = cls;
-    s_gsel[k] = gsel;
+    emit_max(esh, s_off + k * rpm, cap, batch_base + b, cls, pk[0], pk[1], pk[2], pk[3], (int)pk[4], (int)pk[5],
+             is_train, C, extents, mb, gt, num_gt, top_box, top_pose, top_target, top_weight, top_domain, ws.diag);
+    __syncthreads();
   }
-  __syncthreads();
-  const int off = s_off, total = s_total;
-  const int nrows = nk * rpm;
-  // jitter order of cu.cc:476-554: (0,0) then (-,-) (+,-) (-,+) (+,+) (0,-) (-,0) (0,+) (+,0)
-  const int jx[9] = {0, -1, 1, -1, 1, 0, -1, 0, 1};
-  const int jy[9] = {0, -1, -1, 1, 1, -1, 0, 1, 0};
-  for (int i = threadIdx.x; i < nrows; i += blockDim.x) {
-    const int k = i / rpm, j = i % rpm;
-    const int r = off + i;
-    if (r >= cap) {
-      atomicAdd(&ws.diag[2], 1);
-      continue;
-    }
-    float* bo = top_box + (size_t)r * 7;
-    const float x1 = s_box[k][0], y1 = s_box[k][1];
-    bo[0] = (float)batch_index;
-    bo[1] = (float)s_cls[k];
-    if (j == 0) {
-      bo[2] = x1; bo[3] = y1; bo[4] = s_box[k][2]; bo[5] = s_box[k][3];
-    } else {
-      const float ww = s_box[k][2] - x1, hh = s_box[k][3] - y1;
-      const float nx = jx[j] == 0 ? x1 : (float)((double)x1 + (jx[j] < 0 ? -0.05 : 0.05) * (double)ww);
-      const float ny = jy[j] == 0 ? y1 : (float)((double)y1 + (jy[j] < 0 ? -0.05 : 0.05) * (double)hh);
-      bo[2] = nx;
-      bo[3] = ny;
-      bo[4] = nx + ww;
-      bo[5] = ny + hh;
-    }
-    bo[6] = s_score[k];
-    float* po = top_pose + (size_t)r * 7;
-    po[0] = 1.f; po[1] = 0.f; po[2] = 0.f; po[3] = 0.f;
-    po[4] = s_pose[k][0];
-    po[5] = s_pose[k][1];
-    po[6] = s_pose[k][2];
-    top_domain[r] = is_train ? (num_gt == 0 ? 1 : 0) : 0;
-  }
-  const long ncol = (long)nrows * PC;
-  for (long idx = threadIdx.x; idx < ncol; idx += blockDim.x) {
-    const int i = (int)(idx / PC), col = (int)(idx % PC);
-    const int r = off + i;
-    if (r >= cap) continue;
-    const int k = i / rpm;
-    const int g = s_gsel[k], cls = s_cls[k];
-    const bool on = g >= 0 && col >= 4 * cls && col < 4 * cls + 4;
-    top_target[(size_t)r * PC + col] = on ? gt[g * 13 + 6 + (col - 4 * cls)] : 0.f;
-    top_weight[(size_t)r * PC + col] = on ? 1.f : 0.f;
-  }
-  if (b == 0) {
-    if (threadIdx.x == 0) {
-      const int n = total < cap ? total : cap;
-      num_rois[0] = n;
-      num_rois[1] = n > 0 ? n : 1;
-    }
-    if (total == 0) {  // dummy all-zero row (hough_voting_gpu_op.cc:382-383)
-      for (int t = threadIdx.x; t < 7; t += blockDim.x) {
-        top_box[t] = 0.f;
-        top_pose[t] = 0.f;
-      }
-      for (int t = threadIdx.x; t < PC; t += blockDim.x) {
-        top_target[t] = 0.f;
-        top_weight[t] = 0.f;
-      }
-      if (threadIdx.x == 0) top_domain[0] = 0;
-    }
-  }
+  if (b == 0) emit_count(s_total, cap, C, top_box, top_pose, top_target, top_weight, top_domain, num_rois);
 }
 
 }  // namespace pcnn_hough
@@ -199,7 +100,8 @@ extern "C" int pcnn_hough_voting(const int32_t* label, const float* vertex, cons
   {
     const double c = (double)inlier_thr, co = c - kConeEps, ci = c + kConeEps;
     const double so = std::sqrt(std::max(0.0, 1.0 - co * co)), si = std::sqrt(std::max(0.0, 1.0 - ci * ci));
-    hipLaunchKernelGGL(k_voter_setup, dim3((ws.vcap + 255) / 256, B), dim3(256), 0, st, inlier_thr, so, si, ws);
+    hipLaunchKernelGGL(k_voter_setup, dim3((ws.vcap + 255) / 256, B), dim3(256), 0, st, H, W, C, inlier_thr, so, si,
+                       ws);
   }
   PCNN_CHECK_LAUNCH();
   int32_t* counts_out = nms ? ws.counts : debug_counts;
@@ -211,8 +113,9 @@ extern "C" int pcnn_hough_voting(const int32_t* label, const float* vertex, cons
                        inlier_thr, ws, counts_out);
     PCNN_CHECK_LAUNCH();
     if (!nms) {
-      hipLaunchKernelGGL(k_hough_peak, dim3(slots, B), dim3(kPeakThreads), 0, st, H, W, C, inlier_thr, extents,
-                         meta, num_meta, ws);
+      hipLaunchKernelGGL(k_hough_peak, dim3(slots, B), dim3(kPeakThreads), 0, st, B, H, W, C, inlier_thr, extents,
+                         meta, num_meta, ws, is_train, batch_base, gt, num_gt, top_box, top_pose, top_target,
+                         top_weight, top_domain, num_rois, cap);
     } else {
       hipLaunchKernelGGL(k_hough_nms_cand, dim3((HW + 255) / 256 < 64 ? (HW + 255) / 256 : 64, C - 1, B),
                          dim3(256), 0, st, H, W, C, vote_thr, ws);
@@ -228,9 +131,10 @@ extern "C" int pcnn_hough_voting(const int32_t* label, const float* vertex, cons
   } else if (hipMemsetAsync(ws.nvote, 0, B * sizeof(int32_t), st) != hipSuccess) {
     return PCNN_EHIP;
   }
-  hipLaunchKernelGGL(k_hough_emit, dim3(B), dim3(kEmitThreads), 0, st, B, H, W, C, is_train, batch_base,
-                     nms ? 1 : 0, extents, meta, num_meta, gt, num_gt, ws, top_box, top_pose, top_target,
-                     top_weight, top_domain, num_rois, cap);
+  if (nms || slots <= 0)  // the default path emits its rows in k_hough_peak
+    hipLaunchKernelGGL(k_hough_emit, dim3(B), dim3(kEmitThreads), 0, st, B, H, W, C, is_train, batch_base,
+                       nms ? 1 : 0, extents, meta, num_meta, gt, num_gt, ws, top_box, top_pose, top_target,
+                       top_weight, top_domain, num_rois, cap);
   PCNN_CHECK_LAUNCH();
   return PCNN_OK;
 }

@@ -26,38 +26,59 @@ __device__ PeakOut exact_cell(int cx, int cy, int cls, float count_f, const floa
   PeakOut o;
   float dsum = 0.f;  // meaningful in thread 0
   int cnt = 0;
-  for (int start = 0; start < nv; start += kPeakChunk) {
-    const int n = min(kPeakChunk, nv - start);
-    if (threadIdx.x < 4) sh_d[n + threadIdx.x] = 0.f;  // pad to a float4 multiple (+0.0f is exact)
-    for (int j = threadIdx.x; j < n; j += blockDim.x) {
-      const float4 q = vd[start + j];
-      const int p = vp[start + j];
-      const int x = p % W, y = p / W;
-      bool f = cone_pred(cx, cy, x, y, q.x, q.y, inlier);
-      if (f) {
-        float dx = fabsf((float)(x - cx));
-        float dy = fabsf((float)(y - cy));
-        f = dx < q.w && dy < q.w;  // cu.cc:288
+  __shared__ int wcnt[kPeakThreads / 64];
+  const int lane = pcnn::lane_id(), wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  // Voters that vote for (cx, cy) are compacted in voter order into sh_d
+  // (ballot ranks + per-wave offsets); the others would add +0.0f to a
+  // non-negative sum, which leaves it unchanged, so thread 0's in-order sum
+  // over the compacted terms equals the reference's loop (cu.cc:269-294).
+  int start = 0;
+  while (start < nv) {
+    int fill = 0;  // compacted terms in sh_d (block-uniform)
+    int j0 = start;
+    for (; j0 < nv && fill + (int)blockDim.x <= kPeakChunk; j0 += blockDim.x) {
+      const int j = j0 + threadIdx.x;
+      bool f = false;
+      float d = 0.f;
+      if (j < nv) {
+        const float4 q = vd[j];
+        const int p = vp[j];
+        const int x = p % W, y = p / W;
+        f = cone_pred(cx, cy, x, y, q.x, q.y, inlier);
+        if (f) {
+          float dx = fabsf((float)(x - cx));
+          float dy = fabsf((float)(y - cy));
+          f = dx < q.w && dy < q.w;  // cu.cc:288
+        }
+        d = q.z;
       }
-      sh_d[j] = f ? q.z : 0.f;  // adding +0.0f leaves a non-negative sum unchanged
+      const uint64_t m = __ballot(f);
+      if (lane == 0) wcnt[wave] = __popcll(m);
+      __syncthreads();
+      int off = fill;
+      for (int w = 0; w < wave; w++) off += wcnt[w];
+      if (f) sh_d[off + __popcll(m & pcnn::lanemask_lt())] = d;
+      int tot = 0;
+      for (int w = 0; w < nw; w++) tot += wcnt[w];
       cnt += f ? 1 : 0;
+      fill += tot;
+      __syncthreads();
     }
-    __syncthreads();
-    if (threadIdx.x == 0) {  // distance += d in voter order (cu.cc:291); loads batched, adds in order
-      const float4* p4 = (const float4*)sh_d;
-      const int n4 = (n + 3) / 4;
+    start = j0;
+    if (threadIdx.x == 0) {  // distance += d in voter order (cu.cc:291), reads prefetched ahead of the adds
       int i = 0;
-      for (; i + 4 <= n4; i += 4) {
-        const float4 a = p4[i], bb = p4[i + 1], cc = p4[i + 2], dd = p4[i + 3];
-        dsum += a.x; dsum += a.y; dsum += a.z; dsum += a.w;
-        dsum += bb.x; dsum += bb.y; dsum += bb.z; dsum += bb.w;
-        dsum += cc.x; dsum += cc.y; dsum += cc.z; dsum += cc.w;
-        dsum += dd.x; dsum += dd.y; dsum += dd.z; dsum += dd.w;
+      float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+      if (fill >= 4) { a0 = sh_d[0]; a1 = sh_d[1]; a2 = sh_d[2]; a3 = sh_d[3]; }
+      for (; i + 8 <= fill; i += 4) {
+        const float b0 = sh_d[i + 4], b1 = sh_d[i + 5], b2 = sh_d[i + 6], b3 = sh_d[i + 7];
+        dsum += a0; dsum += a1; dsum += a2; dsum += a3;
+        a0 = b0; a1 = b1; a2 = b2; a3 = b3;
       }
-      for (; i < n4; i++) {
-        const float4 a = p4[i];
-        dsum += a.x; dsum += a.y; dsum += a.z; dsum += a.w;
+      if (i + 4 <= fill) {
+        dsum += a0; dsum += a1; dsum += a2; dsum += a3;
+        i += 4;
       }
+      for (; i < fill; i++) dsum += sh_d[i];
     }
     __syncthreads();
   }
@@ -114,14 +135,44 @@ __device__ PeakOut exact_cell(int cx, int cy, int cls, float count_f, const floa
   return o;
 }
 
-__global__ void __launch_bounds__(kPeakThreads) k_hough_peak(int H, int W, int C, float inlier,
+// Default path: one workgroup per (slot, image) = one maximum.  Exact
+// hough_data at the argmax, then the slot's RoI rows (emit_max) at output row
+// (rows of images < b) + slot * rpm: image-major, ascending slot order.
+// Workgroup (0, 0) also writes the row count (+ dummy row) for the batch.
+__global__ void __launch_bounds__(kPeakThreads) k_hough_peak(int B, int H, int W, int C, float inlier,
                                                               const float* __restrict__ extents,
                                                               const float* __restrict__ meta, int num_meta,
-                                                              HoughWs ws) {
+                                                              HoughWs ws, int is_train, int batch_base,
+                                                              const float* __restrict__ gt, int num_gt,
+                                                              float* __restrict__ top_box,
+                                                              float* __restrict__ top_pose,
+                                                              float* __restrict__ top_target,
+                                                              float* __restrict__ top_weight,
+                                                              int32_t* __restrict__ top_domain,
+                                                              int32_t* __restrict__ num_rois, int cap) {
   __shared__ __attribute__((aligned(16))) float sh_d[kPeakChunk + 4];
   __shared__ float sh_red[16];
+  __shared__ int s_off[2];
+  __shared__ EmitShared esh;
   const int b = blockIdx.y, slot = blockIdx.x;
+  const int rpm = is_train ? 9 : 1;
+  if (slot == 0 && b == 0) {  // batch row count: sum over images of nvote * rpm
+    if (threadIdx.x == 0) s_off[1] = 0;
+    __syncthreads();
+    int t = 0;
+    for (int i = threadIdx.x; i < B; i += blockDim.x) t += ws.nvote[i] * rpm;
+    if (t) atomicAdd(&s_off[1], t);
+    __syncthreads();
+    emit_count(s_off[1], cap, C, top_box, top_pose, top_target, top_weight, top_domain, num_rois);
+  }
   if (slot >= ws.nvote[b]) return;
+  if (threadIdx.x == 0) s_off[0] = 0;
+  __syncthreads();
+  {
+    int t = 0;
+    for (int i = threadIdx.x; i < b; i += blockDim.x) t += ws.nvote[i] * rpm;
+    if (t) atomicAdd(&s_off[0], t);
+  }
   const int cls = ws.slot_cls[(size_t)b * C + slot];
   const unsigned long long key = ws.key[(size_t)b * C + slot];
   const unsigned cnt = (unsigned)(key >> 32);
@@ -129,9 +180,9 @@ __global__ void __launch_bounds__(kPeakThreads) k_hough_peak(int H, int W, int C
   const int cx = (int)(idx % (unsigned)W), cy = (int)(idx / (unsigned)W);
   const int vb = ws.vbase[(size_t)b * C + cls];
   const int nv = ws.vcount[(size_t)b * C + cls];
+  const float* mb = meta + (size_t)b * num_meta;
   PeakOut o = exact_cell(cx, cy, cls, (float)cnt, ws.vdat + (size_t)b * ws.vcap + vb,
-                         ws.vpos + (size_t)b * ws.vcap + vb, nv, W, inlier, extents, meta + (size_t)b * num_meta,
-                         sh_d, sh_red);
+                         ws.vpos + (size_t)b * ws.vcap + vb, nv, W, inlier, extents, mb, sh_d, sh_red);
   if (threadIdx.x == 0) {
     float* pk = ws.peak + ((size_t)b * ws.pks + slot) * 8;
     pk[0] = o.count;
@@ -142,6 +193,9 @@ __global__ void __launch_bounds__(kPeakThreads) k_hough_peak(int H, int W, int C
     pk[5] = (float)cy;
     if (o.mismatch) atomicAdd(&ws.diag[0], 1);
   }
+  __syncthreads();  // s_off[0] complete
+  emit_max(esh, s_off[0] + slot * rpm, cap, batch_base + b, cls, o.count, o.distance, o.bbh2, o.bbw2, cx, cy,
+           is_train, C, extents, mb, gt, num_gt, top_box, top_pose, top_target, top_weight, top_domain, ws.diag);
 }
 
 // multi-instance (NMS) path

@@ -21,30 +21,39 @@
 
 namespace pcnn_hough {
 
-__device__ __forceinline__ bool row_interval(int code1, double s1, int code2, double s2, double dy, double& lo,
-                                             double& hi) {
+// Float is enough here: the outer / inner cones sit +-kConeEps (in cos) from
+// the reference threshold, which at row dy is dx = |dy| * 4.6e-6 / sin^2(phi)
+// away from the exact boundary (phi = boundary angle to the row); the float
+// error of s * dy is |dy * cot(phi)| * 2^-24 (+ the slope's own rounding),
+// i.e. at most ~2.6% of that margin.  The bracket stays conservative.
+__device__ __forceinline__ bool row_interval(int code1, float s1, int code2, float s2, float dy, float& lo,
+                                             float& hi) {
   // branch-free (the codes differ across the lanes of a wave)
-  const double b1 = s1 * dy, b2 = s2 * dy;
-  lo = fmax(code1 == kBoundLower ? b1 : -1e30, code2 == kBoundLower ? b2 : -1e30);
-  hi = fmin(code1 == kBoundUpper ? b1 : 1e30, code2 == kBoundUpper ? b2 : 1e30);
-  const bool ok1 = code1 == kNeedPosDy ? dy > 0.0 : (code1 == kNeedNegDy ? dy < 0.0 : true);
-  const bool ok2 = code2 == kNeedPosDy ? dy > 0.0 : (code2 == kNeedNegDy ? dy < 0.0 : true);
+  const float b1 = s1 * dy, b2 = s2 * dy;
+  lo = fmaxf(code1 == kBoundLower ? b1 : -1e30f, code2 == kBoundLower ? b2 : -1e30f);
+  hi = fminf(code1 == kBoundUpper ? b1 : 1e30f, code2 == kBoundUpper ? b2 : 1e30f);
+  const bool ok1 = code1 == kNeedPosDy ? dy > 0.f : (code1 == kNeedNegDy ? dy < 0.f : true);
+  const bool ok2 = code2 == kNeedPosDy ? dy > 0.f : (code2 == kNeedNegDy ? dy < 0.f : true);
   return ok1 && ok2 && lo < hi;
 }
 
 // integer cell range [a, b] of x + dx for dx strictly inside (lo, hi), clipped
-__device__ __forceinline__ void int_range(double lo, double hi, int x, int cx0, int cx1, int& a, int& b) {
-  lo = fmax(lo, -1e9);
-  hi = fmin(hi, 1e9);
-  const long la = (long)floor(lo) + 1 + x;
-  const long lb = (long)ceil(hi) - 1 + x;
-  a = (int)(la < cx0 ? cx0 : la);
-  b = (int)(lb > cx1 ? cx1 : lb);
+__device__ __forceinline__ void int_range(float lo, float hi, int x, int cx0, int cx1, int& a, int& b) {
+  lo = fmaxf(lo, -1e9f);
+  hi = fminf(hi, 1e9f);
+  const int la = (int)floorf(lo) + 1 + x;
+  const int lb = (int)ceilf(hi) - 1 + x;
+  a = la < cx0 ? cx0 : la;
+  b = lb > cx1 ? cx1 : lb;
 }
 
 __device__ __forceinline__ void add_run(int* row, int a, int b) {
+#ifndef PCNN_ABLATE_ATOMICS
   atomicAdd(&row[a], 1);
   atomicAdd(&row[b + 1], -1);
+#else
+  if (a == 12345678) row[b] = 1;
+#endif
 }
 
 // exact reference predicate over cells [a, b] of one row, runs merged
@@ -69,16 +78,32 @@ __global__ void __launch_bounds__(kVoteThreads) k_hough_vote(int H, int W, int C
   const int b = blockIdx.z, slot = blockIdx.y, band = blockIdx.x;
   if (slot >= ws.nvote[b]) return;
   const int cls = ws.slot_cls[(size_t)b * C + slot];
-  const int nv = ws.vcount[(size_t)b * C + cls];
   const int vb = ws.vbase[(size_t)b * C + cls];
   const int y0 = band * kBand;
   const int y1 = min(y0 + kBand, H);
   const int Wp = W + 1;
+  // only voters whose +-k rows can reach the band (rows in [y0 - kmax, y1 - 1 + kmax])
+  const int kx = ws.kmax[(size_t)b * C + slot];
+  int ibeg = 0, iend = 0;
+  if (kx >= 0) {
+    const int32_t* rs = ws.rowstart + ((size_t)b * C + slot) * (H + 1);
+    const int yf = ws.yspan[((size_t)b * C + slot) * 2], yl = ws.yspan[((size_t)b * C + slot) * 2 + 1];
+    const int cnt = ws.vcount[(size_t)b * C + cls];
+    const int ylo = max(0, y0 - kx), yhi1 = (int)min((long)H, (long)y1 + kx);  // rows [ylo, yhi1)
+    ibeg = ylo <= yf ? 0 : (ylo > yl ? cnt : rs[ylo]);
+    iend = yhi1 > yl ? cnt : (yhi1 <= yf ? 0 : rs[yhi1]);
+  }
+  if (ibeg >= iend && !counts_out) {
+    // no voter reaches the band: all its counts are 0; its first-max key is
+    // (0, first cell) — needed only when the whole slot has no vote
+    if (threadIdx.x == 0) atomicMax(ws.key + (size_t)b * C + slot, 0xFFFFFFFFull - (unsigned)(y0 * W));
+    return;
+  }
   for (int i = threadIdx.x; i < kBand * Wp; i += blockDim.x) diff[i] = 0;
   __syncthreads();
 
   const size_t v0 = (size_t)b * ws.vcap + vb;
-  for (int i = threadIdx.x; i < nv; i += blockDim.x) {
+  for (int i = ibeg + (int)threadIdx.x; i < iend; i += blockDim.x) {
     const float4 q = ws.vdat[v0 + i];
     const int p = ws.vpos[v0 + i];
     const int x = p % W, y = p / W;
@@ -86,6 +111,10 @@ __global__ void __launch_bounds__(kVoteThreads) k_hough_vote(int H, int W, int C
     if (k < 0) continue;
     const int ry0 = max(y - k, y0), ry1 = min(y + k, y1 - 1);
     if (ry0 > ry1) continue;
+#ifdef PCNN_ABLATE_ROWS
+    if (ry0 == -12345) diff[0] = 1;
+    continue;
+#endif
     const int bx0 = max(x - k, 0), bx1 = min(x + k, W - 1);
     const int code = ws.vcode[v0 + i];
     const float u = q.x, v = q.y;
@@ -93,28 +122,35 @@ __global__ void __launch_bounds__(kVoteThreads) k_hough_vote(int H, int W, int C
       for (int r = ry0; r <= ry1; r++) exact_cells(diff + (r - y0) * Wp, bx0, bx1, r, x, y, u, v, inlier);
       continue;
     }
-    const double4 s = ws.vcone[v0 + i];
+    const float4 s = ws.vcone[v0 + i];
     const int co1 = code & 3, co2 = (code >> 2) & 3, ci1 = (code >> 4) & 3, ci2 = (code >> 6) & 3;
     for (int r = ry0; r <= ry1; r++) {
       int* row = diff + (r - y0) * Wp;
-      const double dy = (double)(r - y);
-      double lo, hi;
+      const float dy = (float)(r - y);
+      float lo, hi;
       if (!row_interval(co1, s.x, co2, s.y, dy, lo, hi)) continue;
       int oa, ob;
       int_range(lo, hi, x, bx0, bx1, oa, ob);
       if (oa > ob) continue;
       int ia = 1, ib = 0;
+#ifdef PCNN_ABLATE_INNER
+      ia = oa; ib = ob;
+      if (false) {
+#else
       if (row_interval(ci1, s.z, ci2, s.w, dy, lo, hi)) {
+#endif
         int_range(lo, hi, x, bx0, bx1, ia, ib);
         ia = max(ia, oa);
         ib = min(ib, ob);
       }
       if (ia <= ib) {
         add_run(row, ia, ib);
+#ifndef PCNN_ABLATE_EXACT
         if (oa < ia) exact_cells(row, oa, ia - 1, r, x, y, u, v, inlier);
         if (ib < ob) exact_cells(row, ib + 1, ob, r, x, y, u, v, inlier);
       } else {
         exact_cells(row, oa, ob, r, x, y, u, v, inlier);
+#endif
       }
     }
   }

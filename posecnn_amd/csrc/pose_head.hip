@@ -703,7 +703,7 @@ extern "C" int pcnn_gemm(int M, int N, int K, const float* A, const float* A2, i
   do {                                                                                                 \
     static bool attr_set = false;                                                                      \
     if (!attr_set) {                                                                                   \
-      hipFuncSetAttribute((const void*)k_gemm_x3<AT, BT, RG, S2>,                                      \
+      (void)hipFuncSetAttribute((const void*)k_gemm_x3<AT, BT, RG, S2>,                                    \
                           hipFuncAttributeMaxDynamicSharedMemorySize, kXLds);                          \
       attr_set = true;                                                                                 \
     }                                                                                                  \
