@@ -189,23 +189,35 @@ def main():
         dom = max(gem, key=lambda k: ops.get(k, 0.0))
         tf = gem[dom] / (ops[dom] / 1e3) / 1e12
         if args.precision == 1:
-            # algorithmic fp32 flops against the rate of the 3 bf16 MFMA passes that produce them
-            peak, kname = BF16_MFMA_PEAK_TFS / 3, f"k_gemm_b3 ({dom}, split-bf16 x3 MFMA 32x32x16, R={R})"
+            # algorithmic fp32 flops against the rate of the 3 bf16 MFMA passes that produce them;
+            # fc6_fwd runs split-K (k_gemm_x3 + k_gemm_reduce), fc6_dw / fc6_dx one k_gemm_x3 launch
+            peak, kname = BF16_MFMA_PEAK_TFS / 3, (f"k_gemm_x3 ({dom}{' + k_gemm_reduce' if dom == 'gemm_fc6_fwd' else ''}"
+                                                   f", split-bf16 x3 MFMA 32x32x16, R={R})")
         else:
             peak, kname = FP32_MFMA_PEAK_TFS, f"k_gemm_f32 ({dom}, fp32 MFMA 32x32x2, R={R})"
         roof = {"bound": "mfma", "achieved": round(tf, 2), "peak": round(peak, 1), "unit": "TFLOP/s",
                 "frac": round(tf / peak, 4), "traffic": None, "kernel": kname, "flops_per_launch": gem[dom]}
     else:
         roof = roof_vote
+    # HBM traffic of the same launches from the committed rocprofv3 FETCH_SIZE /
+    # WRITE_SIZE passes (scripts/gpu_pmc.sh -> scripts/pmc_traffic.py)
     pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(pmc_path) and roof is not None:
+    if os.path.exists(pmc_path):
         try:
             pmc = json.load(open(pmc_path))
-            key = roof["kernel"].split(" ")[0]
-            if key in pmc:
-                roof["traffic"] = pmc[key]
-        except Exception:
-            pass
+            wl = pmc.get("full" if full else "vote_roi", {})
+            if roof is not None and full and args.precision == 1:
+                tmpl = {"gemm_fc6_fwd": "<false, false, false, false>", "gemm_fc6_dw": "<true, false, false, false>",
+                        "gemm_fc6_dx": "<false, true, false, false>"}[dom]
+                ent = wl.get(f"k_gemm_x3{tmpl}:{dom.replace('gemm_', '')}")
+                if ent:
+                    roof["traffic"] = round(ent["traffic_bytes"])
+                    roof["traffic_unit"] = "bytes/launch (rocprofv3 2*FETCH_SIZE + WRITE_SIZE)"
+            if roof_vote is not None and "hough_voting_gpu op" in wl:
+                roof_vote["traffic"] = round(wl["hough_voting_gpu op"]["traffic_bytes"])
+                roof_vote["traffic_unit"] = "bytes/launch (rocprofv3 2*FETCH_SIZE + WRITE_SIZE)"
+        except Exception as e:  # pragma: no cover - a stale file must not break the bench
+            log(f"pmc traffic unavailable: {e}")
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

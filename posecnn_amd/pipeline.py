@@ -146,15 +146,16 @@ class PoseStep:
             ph.head_bwd(self.dpred, self.t8, h["weight"], self.pred, self.dy8, num_rois=nr)
         with self._t("gemm_fc8_fc7_bwd"):
             ph.gemm(self.y7, self.dy8, g["w8"], a_trans=1, K_dev=nr, M=w.units, N=self.D, K=CAP, precision=self.prec)
-            ph.colsum(self.dy8, g["b8"], M_dev=nr)
             ph.gemm(self.dy8, w.w8, self.dy7, b_trans=1, mask=self.y7, M_dev=nr, precision=self.prec)
             ph.gemm(self.y6, self.dy7, g["w7"], a_trans=1, K_dev=nr, M=w.units, N=w.units, K=CAP, precision=self.prec)
-            ph.colsum(self.dy7, g["b7"], M_dev=nr)
             ph.gemm(self.dy7, w.w7, self.dy6, b_trans=1, mask=self.y6, M_dev=nr, precision=self.prec)
+        with self._t("bias_grads"):
+            ph.colsum(self.dy8, g["b8"], M_dev=nr)
+            ph.colsum(self.dy7, g["b7"], M_dev=nr)
+            ph.colsum(self.dy6, g["b6"], M_dev=nr)
         x = self.pool.view(CAP, K6)
         with self._t("gemm_fc6_dw"):  # A = pool5 + pool4
             ph.gemm(x, self.dy6, g["w6"], a_trans=1, K_dev=nr, M=K6, N=w.units, K=CAP, precision=self.prec)
-            ph.colsum(self.dy6, g["b6"], M_dev=nr)
         with self._t("gemm_fc6_dx"):
             ph.gemm(self.dy6, w.w6, self.dx, b_trans=1, M_dev=nr, precision=self.prec)
         dxp = self.dx.view(CAP, 7, 7, self.Ch)

@@ -1,5 +1,4 @@
 cd $GRAFT_REPO_ROOT
-timeout -k 10 120 python scripts/hough_bench.py > gpurun_out/abl.log 2>&1 &&
-for v in rows inner atomexact; do POSECNN_HIP_LIB=$GRAFT_REPO_ROOT/scratch/abl_$v.so timeout -k 10 120 python scripts/hough_bench.py >> gpurun_out/abl.log 2>&1 || exit 1; done
-cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/profh -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/scripts/hough_bench.py > $GRAFT_REPO_ROOT/gpurun_out/profh.log 2>&1
+timeout -k 10 120 python scripts/gemm_bench.py --only fc6_fwd,fc6_dw,fc6_dx > gpurun_out/abl.log 2>&1 &&
+for v in gload store gs; do echo "== $v" >> gpurun_out/abl.log; POSECNN_HIP_LIB=$GRAFT_REPO_ROOT/scratch/abl_$v.so timeout -k 10 120 python scripts/gemm_bench.py --only fc6_fwd,fc6_dw,fc6_dx >> gpurun_out/abl.log 2>&1 || exit 1; done
 echo "exit=$?"

@@ -5,9 +5,9 @@ FETCH_SIZE / WRITE_SIZE are in KiB per dispatch.  On gfx950 FETCH_SIZE
 counts half the bytes of wide coalesced reads (MI355X_MICROARCH.md, HBM
 section), so reads are doubled.  GEMM dispatches of one template are told
 apart by their fixed order inside a pose step (pipeline.py):
-  k_gemm_x3<false,false>: fc6_fwd, fc7_fwd, fc8_fwd
-  k_gemm_x3<true,false>:  fc8_dw, fc7_dw, fc6_dw
-  k_gemm_x3<false,true>:  fc8_dx, fc7_dx, fc6_dx
+  k_gemm_x3<false, false, ...>: fc6_fwd, fc7_fwd, fc8_fwd
+  k_gemm_x3<true, false, ...>:  fc8_dw, fc7_dw, fc6_dw
+  k_gemm_x3<false, true, ...>:  fc8_dx, fc7_dx, fc6_dx
 """
 import csv
 import json
@@ -16,11 +16,11 @@ import re
 import sys
 from collections import defaultdict
 
-ROLES = {"k_gemm_x3<false, false>": ["fc6_fwd", "fc7_fwd", "fc8_fwd"],
-         "k_gemm_x3<true, false>": ["fc8_dw", "fc7_dw", "fc6_dw"],
-         "k_gemm_x3<false, true>": ["fc8_dx", "fc7_dx", "fc6_dx"]}
+ROLES = {"k_gemm_x3<false, false, false, false>": ["fc6_fwd", "fc7_fwd", "fc8_fwd"],
+         "k_gemm_x3<true, false, false, false>": ["fc8_dw", "fc7_dw", "fc6_dw"],
+         "k_gemm_x3<false, true, false, false>": ["fc8_dx", "fc7_dx", "fc6_dx"]}
 HOUGH = ("k_label_hist", "k_label_scan", "k_label_scatter", "k_voter_setup", "k_hough_vote", "k_hough_peak",
-         "k_hough_emit")
+         "k_hough_emit", "k_hough_nms_cand", "k_hough_cand_data", "k_hough_nms_select")
 
 
 def short(name):
