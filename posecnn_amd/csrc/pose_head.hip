@@ -44,6 +44,7 @@ struct GemmArgs {
   const int32_t* K_dev;
   float* slab;  // split-K partials [kMaxSplit][M][N]
   int prec;     // 0 fp32 MFMA, 1 split-bf16 x3 (selects the split rule)
+  int tile;     // x3 tile edge (256 or 128), chosen on the host
 };
 
 __device__ __forceinline__ int eff_dim(int full, const int32_t* dev) {
@@ -259,13 +260,27 @@ __global__ void __launch_bounds__(kGemmThreads) k_gemm_f32(GemmArgs g) {
 // LDS stages: the global loads of step s+2 are in flight (registers) while
 // step s computes and step s+1 sits in LDS.  At 512 flop per staged fp32 byte
 // pair the tile needs ~21 B/clk/CU at the MFMA rate, inside the L2 share.
+// Shapes with an edge <= 128 (the fc8 GEMMs: N = 4C, or K = 4C in dX) use a
+// 128 x 128 instance (256 threads, 2 x 2 waves of 64 x 64, two workgroups per
+// CU): 4x the workgroups of an output- or latency-bound shape.  Measured
+// (scripts/gemm_bench.py): fc8 23-26 us vs 33-40 us at 256; 128 everywhere
+// loses 20-25% on fc6 and is even on fc7.
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-constexpr int XBM = 256, XBN = 256, XBK = 32, kXThreads = 512;
-constexpr int kXPart = 256 * 64;        // one operand half (hi or lo): 256 rows x 32 bf16
-constexpr int kXStage = 4 * kXPart;     // a_hi, a_lo, b_hi, b_lo
-constexpr int kXLds = 2 * kXStage;      // 128 KiB
-constexpr int kXMaxGrid = 256;          // one workgroup per CU
+constexpr int XBK = 32;
+// Tile geometry: T = 256 (the large shapes) or 128 (shapes with an edge of
+// <= 128 or too few 256-tiles to fill the chip: 256 threads as 2 x 2 waves of
+// 64 x 64, 64 KiB LDS, two workgroups per CU).
+template <int T>
+struct XTile {
+  static constexpr int threads = 2 * T;
+  static constexpr int part = T * 64;       // one operand half (hi or lo): T rows x 32 bf16
+  static constexpr int stage = 4 * part;    // a_hi, a_lo, b_hi, b_lo
+  static constexpr int lds = 2 * stage;     // 128 / 64 KiB
+  static constexpr int grid = T == 256 ? 256 : 512;  // workgroups resident on 256 CUs
+  static constexpr int wn = T / 64;         // waves along N (64 columns each); 2 along M
+  static constexpr int am = T / 64;         // 32-row accumulators per wave along M
+};
 
 // LDS image of an operand half: rows of 64 B = 4 chunks of 8 bf16 (k), chunk
 // XOR-swizzled by g(row) = r2 | (r1 ^ r3) << 1 — conflict-free for the
@@ -277,11 +292,20 @@ __device__ __forceinline__ int x_off(int row, int c) {
   return row * 64 + 16 * (c ^ g);
 }
 
+// tile edge of the x3 kernel for a (capacity) shape
+__host__ __device__ __forceinline__ int tile_x3(int M, int N, int K) {
+#ifdef PCNN_FORCE_TILE
+  return PCNN_FORCE_TILE;
+#endif
+  return (M <= 128 || N <= 128 || K <= 128) ? 128 : 256;
+}
+
 // split-K factor of the x3 kernel for the effective shape
-__host__ __device__ __forceinline__ int split_x3(int M, int N, int K) {
-  const int tiles = ((M + XBM - 1) / XBM) * ((N + XBN - 1) / XBN);
-  if (tiles >= 128 || M == 0) return 1;
-  int s = kXMaxGrid / tiles;
+__host__ __device__ __forceinline__ int split_x3(int M, int N, int K, int T) {
+  const int tiles = ((M + T - 1) / T) * ((N + T - 1) / T);
+  const int grid = T == 256 ? XTile<256>::grid : XTile<128>::grid;
+  if (tiles >= grid / 2 || M == 0) return 1;
+  int s = grid / tiles;
   const int smax = K / 128;
   if (s > smax) s = smax;
   if (s > kMaxSplitX) s = kMaxSplitX;
@@ -323,7 +347,7 @@ __device__ __forceinline__ xf4 x_ld4(const XOp& o, unsigned voff, int soff) {
 // Rows past rlim and k past ke load as 0.  RAGGED: some float4 may straddle
 // the K edge (KC) or the row edge (NC) -> element-wise fallback; the common
 // instantiation has no divergent branch, so a K step is one basic block.
-template <bool KC, bool RAGGED, bool A2>
+template <int T, bool KC, bool RAGGED, bool A2>
 __device__ __forceinline__ void x_load(const XOp& P, const XOp& P2, int r0, int rlim, int k0, int ke,
                                        float (&v)[16]) {
   // Every mask is applied to the load ADDRESS (out-of-range voffset -> the
@@ -338,7 +362,7 @@ __device__ __forceinline__ void x_load(const XOp& P, const XOp& P2, int r0, int 
     const int kl = k0 + 4 * kq;
 #pragma unroll
     for (int i = 0; i < 4; i++) {
-      const int row = row0 + 64 * i;
+      const int row = row0 + (T / 4) * i;
       const bool ok = row < rlim && kl < ke;
       const unsigned vo = ok ? (unsigned)(row * P.ld + kl) * 4u : kXOob;
       xf4 x;
@@ -381,14 +405,14 @@ __device__ __forceinline__ void x_load(const XOp& P, const XOp& P2, int r0, int 
   }
 }
 
-template <bool KC>
+template <int T, bool KC>
 __device__ __forceinline__ void x_store(const float (&v)[16], char* hi, char* lo) {
   const int t = threadIdx.x;
   if (KC) {
     const int kq = t & 7;
 #pragma unroll
     for (int i = 0; i < 4; i++) {
-      const int row = (t >> 3) + 64 * i;
+      const int row = (t >> 3) + (T / 4) * i;
       bf16x4 h, l;
 #pragma unroll
       for (int e = 0; e < 4; e++) {
@@ -421,18 +445,20 @@ __device__ __forceinline__ void x_store(const float (&v)[16], char* hi, char* lo
   }
 }
 
-template <bool A_T, bool B_T, bool RAGGED, bool A2>
-__global__ void __launch_bounds__(kXThreads, 1) k_gemm_x3(GemmArgs g) {
+template <int T, bool A_T, bool B_T, bool RAGGED, bool A2>
+__global__ void __launch_bounds__(XTile<T>::threads, T == 256 ? 1 : 2) k_gemm_x3(GemmArgs g) {
+  using X = XTile<T>;
+  constexpr int kXPart = X::part, kXStage = X::stage, AM = X::am;
   extern __shared__ __attribute__((aligned(16))) char xl[];
   constexpr bool A_KC = !A_T, B_KC = B_T;
   const int Meff = eff_dim(g.M, g.M_dev);
   const int Keff = eff_dim(g.K, g.K_dev);
-  const int mt = (Meff + XBM - 1) / XBM, nt = (g.N + XBN - 1) / XBN;
-  const int S = split_x3(Meff, g.N, Keff);
+  const int mt = (Meff + T - 1) / T, nt = (g.N + T - 1) / T;
+  const int S = split_x3(Meff, g.N, Keff, T);
   const int kchunk = ((Keff + S - 1) / S + XBK - 1) / XBK * XBK;
   const int items = mt * nt * S;
   const int lane = pcnn::lane_id(), wave = threadIdx.x >> 6;
-  const int wm = wave >> 2, wn = wave & 3;
+  const int wm = wave / X::wn, wn = wave % X::wn;
   const int r = lane & 31, hsel = lane >> 5;
   // operand extents (elements): A (M,K) or (K,M); B (K,N) or (N,K)
   const long a_el = A_T ? (long)(g.K - 1) * g.lda + g.M : (long)(g.M - 1) * g.lda + g.K;
@@ -447,11 +473,11 @@ __global__ void __launch_bounds__(kXThreads, 1) k_gemm_x3(GemmArgs g) {
   const bool m_fast = mt <= nt;  // the dimension with fewer tiles runs fastest: its
                                  // neighbours share the other operand's tile in L2
   // fragment offsets (bytes) inside an operand half, per k16 sub-step
-  int a_off[2][4], b_off[2][2];
+  int a_off[2][AM], b_off[2][2];
 #pragma unroll
   for (int ks = 0; ks < 2; ks++) {
 #pragma unroll
-    for (int i = 0; i < 4; i++) a_off[ks][i] = x_off(wm * 128 + i * 32 + r, 2 * ks + hsel);
+    for (int i = 0; i < AM; i++) a_off[ks][i] = x_off(wm * (T / 2) + i * 32 + r, 2 * ks + hsel);
 #pragma unroll
     for (int j = 0; j < 2; j++) b_off[ks][j] = x_off(wn * 64 + j * 32 + r, 2 * ks + hsel);
   }
@@ -459,24 +485,24 @@ __global__ void __launch_bounds__(kXThreads, 1) k_gemm_x3(GemmArgs g) {
     const int tile = item % (mt * nt), z = item / (mt * nt);
     const int mi = m_fast ? tile % mt : tile / nt;
     const int ni = m_fast ? tile / mt : tile % nt;
-    const int m0 = mi * XBM, n0 = ni * XBN;
+    const int m0 = mi * T, n0 = ni * T;
     const int kb = z * kchunk, ke = min(Keff, kb + kchunk);
     const int nsteps = kb < ke ? (ke - kb + XBK - 1) / XBK : 0;
-    f32x16 acc[4][2];
+    f32x16 acc[AM][2];
 #pragma unroll
-    for (int i = 0; i < 4; i++)
+    for (int i = 0; i < AM; i++)
 #pragma unroll
       for (int j = 0; j < 2; j++) acc[i][j] = (f32x16){};
     if (nsteps > 0) {
       float va[16], vb[16];
       // prologue: stage 0 -> LDS buffer 0, stage 1 -> registers
-      x_load<A_KC, RAGGED, A2>(oa, oa2, m0, Meff, kb, ke, va);
-      x_load<B_KC, RAGGED, false>(ob, onull, n0, g.N, kb, ke, vb);
-      x_store<A_KC>(va, xl, xl + kXPart);
-      x_store<B_KC>(vb, xl + 2 * kXPart, xl + 3 * kXPart);
+      x_load<T, A_KC, RAGGED, A2>(oa, oa2, m0, Meff, kb, ke, va);
+      x_load<T, B_KC, RAGGED, false>(ob, onull, n0, g.N, kb, ke, vb);
+      x_store<T, A_KC>(va, xl, xl + kXPart);
+      x_store<T, B_KC>(vb, xl + 2 * kXPart, xl + 3 * kXPart);
       const int k1 = kb + (nsteps > 1 ? XBK : 0);
-      x_load<A_KC, RAGGED, A2>(oa, oa2, m0, Meff, k1, ke, va);
-      x_load<B_KC, RAGGED, false>(ob, onull, n0, g.N, k1, ke, vb);
+      x_load<T, A_KC, RAGGED, A2>(oa, oa2, m0, Meff, k1, ke, va);
+      x_load<T, B_KC, RAGGED, false>(ob, onull, n0, g.N, k1, ke, vb);
       __syncthreads();
       // steady state, one basic block per step: MFMAs on buffer s & 1, stage
       // s+1 (registers) -> the other buffer, loads of stage s+2 (clamped to
@@ -493,7 +519,7 @@ __global__ void __launch_bounds__(kXThreads, 1) k_gemm_x3(GemmArgs g) {
             bl[j] = *(const bf16x8*)(cur + 3 * kXPart + b_off[ks][j]);
           }
 #pragma unroll
-          for (int i = 0; i < 4; i++) {
+          for (int i = 0; i < AM; i++) {
             const bf16x8 ah = *(const bf16x8*)(cur + a_off[ks][i]);
             const bf16x8 al = *(const bf16x8*)(cur + kXPart + a_off[ks][i]);
 #pragma unroll
@@ -504,11 +530,11 @@ __global__ void __launch_bounds__(kXThreads, 1) k_gemm_x3(GemmArgs g) {
             }
           }
         }
-        x_store<A_KC>(va, nxt, nxt + kXPart);
-        x_store<B_KC>(vb, nxt + 2 * kXPart, nxt + 3 * kXPart);
+        x_store<T, A_KC>(va, nxt, nxt + kXPart);
+        x_store<T, B_KC>(vb, nxt + 2 * kXPart, nxt + 3 * kXPart);
         const int s2 = s + 2 < nsteps ? s + 2 : nsteps - 1;
-        x_load<A_KC, RAGGED, A2>(oa, oa2, m0, Meff, kb + s2 * XBK, ke, va);
-        x_load<B_KC, RAGGED, false>(ob, onull, n0, g.N, kb + s2 * XBK, ke, vb);
+        x_load<T, A_KC, RAGGED, A2>(oa, oa2, m0, Meff, kb + s2 * XBK, ke, va);
+        x_load<T, B_KC, RAGGED, false>(ob, onull, n0, g.N, kb + s2 * XBK, ke, vb);
         __syncthreads();
       }
     }
@@ -519,30 +545,37 @@ __global__ void __launch_bounds__(kXThreads, 1) k_gemm_x3(GemmArgs g) {
     const XOp oslab = x_op(g.slab, g.N, (long)S * g.M * g.N);
     const XOp obias = x_op(g.bias, 0, g.N);
     const XOp omask = x_op(g.mask, g.ldm, g.mask ? (long)(g.M - 1) * g.ldm + g.N : 0);
+    // Masked epilogue (S == 1): the 16 mask values of group (j, i) are issued
+    // one group ahead of their use, so the tile pays one mask latency, not 8.
+    const bool msk = S == 1 && g.mask;
+    float mv[2][16];
+    auto load_mask = [&](int gi, float (&d)[16]) {
+      const int n = n0 + wn * 64 + (gi / AM) * 32 + r;
+#pragma unroll
+      for (int q = 0; q < 16; q++) {
+        const int m = m0 + wm * (T / 2) + (gi % AM) * 32 + (q & 3) + 8 * (q >> 2) + 4 * hsel;
+        d[q] = x_ld1(omask, (n < g.N && m < Meff) ? (unsigned)(m * g.ldm + n) * 4u : kXOob, 0);
+      }
+    };
+    if (msk) load_mask(0, mv[0]);
 #pragma unroll
     for (int j = 0; j < 2; j++) {
       const int n = n0 + wn * 64 + j * 32 + r;
       const bool nok = n < g.N;
       const float bv = (S == 1 && g.bias) ? x_ld1(obias, nok ? (unsigned)n * 4u : kXOob, 0) : 0.f;
 #pragma unroll
-      for (int i = 0; i < 4; i++) {
-        float mv[16];
-        if (S == 1 && g.mask) {
-#pragma unroll
-          for (int q = 0; q < 16; q++) {
-            const int m = m0 + wm * 128 + i * 32 + (q & 3) + 8 * (q >> 2) + 4 * hsel;
-            mv[q] = x_ld1(omask, (nok && m < Meff) ? (unsigned)(m * g.ldm + n) * 4u : kXOob, 0);
-          }
-        }
+      for (int i = 0; i < AM; i++) {
+        const int gi = AM * j + i;
+        if (msk && gi + 1 < 2 * AM) load_mask(gi + 1, mv[(gi + 1) & 1]);
 #pragma unroll
         for (int q = 0; q < 16; q++) {
-          const int m = m0 + wm * 128 + i * 32 + (q & 3) + 8 * (q >> 2) + 4 * hsel;
+          const int m = m0 + wm * (T / 2) + i * 32 + (q & 3) + 8 * (q >> 2) + 4 * hsel;
           const bool ok = nok && m < Meff;
           float v = acc[i][j][q];
           if (S == 1) {
             v += bv;
             if (g.act == 1) v = v > 0.f ? v : 0.f;
-            if (g.mask && !(mv[q] > 0.f)) v = 0.f;
+            if (msk && !(mv[gi & 1][q] > 0.f)) v = 0.f;
             __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), oc.rs,
                                                   ok ? (unsigned)(m * g.ldc + n) * 4u : kXOob, 0, 0);
           } else {
@@ -558,7 +591,7 @@ __global__ void __launch_bounds__(kXThreads, 1) k_gemm_x3(GemmArgs g) {
 __global__ void __launch_bounds__(256) k_gemm_reduce(GemmArgs g) {
   const int Meff = eff_dim(g.M, g.M_dev);
   const int Keff = eff_dim(g.K, g.K_dev);
-  const int S = g.prec ? split_x3(Meff, g.N, Keff) : split_for(Meff, g.N, Keff);
+  const int S = g.prec ? split_x3(Meff, g.N, Keff, g.tile) : split_for(Meff, g.N, Keff);
   if (S == 1) return;
   const long total = (long)Meff * g.N;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
@@ -661,7 +694,8 @@ __global__ void __launch_bounds__(256) k_head_bwd(const float* __restrict__ dpre
 extern "C" size_t pcnn_gemm_workspace_size(int M, int N, int K, int m_dynamic, int precision) {
   if (M <= 0 || N <= 0) return 256;
   // split-K partial slabs; the split only grows when the device-side M shrinks
-  const int s = precision == 1 ? split_x3(m_dynamic ? 1 : M, N, K) : split_for(m_dynamic ? 1 : M, N, K);
+  const int s = precision == 1 ? split_x3(m_dynamic ? 1 : M, N, K, tile_x3(M, N, K))
+                                : split_for(m_dynamic ? 1 : M, N, K);
   return s > 1 ? pcnn::align_up((size_t)s * M * N * sizeof(float), 256) + 256 : 256;
 }
 
@@ -679,13 +713,13 @@ extern "C" int pcnn_gemm(int M, int N, int K, const float* A, const float* A2, i
                                   ((uintptr_t)B & 15) == 0 && (!A2 || ((uintptr_t)A2 & 15) == 0)));
   PCNN_REQUIRE(precision == 0 || ((long)(a_trans ? K : M) * lda < (1l << 29) && (long)(b_trans ? N : K) * ldb < (1l << 29) &&
                                   (long)M * ldc < (1l << 29) &&
-                                  (split_x3(M_dev ? 1 : M, N, K) == 1 ||
-                                   (long)split_x3(M_dev ? 1 : M, N, K) * M * N < (1l << 29)) &&
+                                  (long)split_x3(M_dev ? 1 : M, N, K, tile_x3(M, N, K)) * M * N < (1l << 29) &&
                                   (!mask || (long)M * ldm < (1l << 29))));
   if (M == 0) return PCNN_OK;
   if (workspace_bytes < pcnn_gemm_workspace_size(M, N, K, M_dev != nullptr, precision) || !workspace)
     return PCNN_ECAPACITY;
-  GemmArgs g{M, N, K, A, A2, lda, B, ldb, Cm, ldc, bias, act, mask, ldm, M_dev, K_dev, (float*)workspace, precision};
+  GemmArgs g{M, N, K, A, A2, lda, B, ldb, Cm, ldc, bias, act, mask, ldm, M_dev, K_dev, (float*)workspace, precision,
+             tile_x3(M, N, K)};
   hipStream_t st = (hipStream_t)stream;
   if (precision == 1) {
     // persistent grid: one workgroup per CU (a multiple of 8 for the XCD-aware
@@ -695,19 +729,27 @@ extern "C" int pcnn_gemm(int M, int N, int K, const float* A, const float* A2, i
     const bool a_kc = !a_trans, b_kc = b_trans;
     const bool ragged = ((a_kc || b_kc) && (K % 4 != 0 || K_dev != nullptr)) || (!a_kc && M % 4 != 0) ||
                         (!b_kc && N % 4 != 0);
-    const int mt = (M + XBM - 1) / XBM, nt = (N + XBN - 1) / XBN;
+    const int T = g.tile;
+    const int mt = (M + T - 1) / T, nt = (N + T - 1) / T;
+    const int max_grid = T == 256 ? XTile<256>::grid : XTile<128>::grid;
     const long cap_items = (long)mt * nt * kMaxSplitX;
-    long grid = cap_items < kXMaxGrid ? cap_items : kXMaxGrid;
+    long grid = cap_items < max_grid ? cap_items : max_grid;
     if (grid >= 8) grid -= grid % 8;
-#define PCNN_X3_LAUNCH(AT, BT, RG, S2)                                                                  \
-  do {                                                                                                 \
-    static bool attr_set = false;                                                                      \
-    if (!attr_set) {                                                                                   \
-      (void)hipFuncSetAttribute((const void*)k_gemm_x3<AT, BT, RG, S2>,                                    \
-                          hipFuncAttributeMaxDynamicSharedMemorySize, kXLds);                          \
-      attr_set = true;                                                                                 \
-    }                                                                                                  \
-    hipLaunchKernelGGL((k_gemm_x3<AT, BT, RG, S2>), dim3(grid), dim3(kXThreads), kXLds, st, g);        \
+#define PCNN_X3_LAUNCH_T(TT, AT, BT, RG, S2)                                                                   \
+  do {                                                                                                          \
+    static bool attr_set = false;                                                                               \
+    if (!attr_set) {                                                                                            \
+      (void)hipFuncSetAttribute((const void*)k_gemm_x3<TT, AT, BT, RG, S2>,                                     \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, XTile<TT>::lds);                    \
+      attr_set = true;                                                                                          \
+    }                                                                                                           \
+    hipLaunchKernelGGL((k_gemm_x3<TT, AT, BT, RG, S2>), dim3(grid), dim3(XTile<TT>::threads), XTile<TT>::lds, st, \
+                       g);                                                                                      \
+  } while (0)
+#define PCNN_X3_LAUNCH(AT, BT, RG, S2)                  \
+  do {                                                  \
+    if (T == 256) PCNN_X3_LAUNCH_T(256, AT, BT, RG, S2); \
+    else PCNN_X3_LAUNCH_T(128, AT, BT, RG, S2);          \
   } while (0)
 #define PCNN_X3_LAYOUT(RG, S2)                                     \
   do {                                                            \
@@ -721,6 +763,7 @@ extern "C" int pcnn_gemm(int M, int N, int K, const float* A, const float* A2, i
     else if (!A2) PCNN_X3_LAYOUT(true, false);
     else PCNN_X3_LAYOUT(true, true);
 #undef PCNN_X3_LAYOUT
+#undef PCNN_X3_LAUNCH_T
 #undef PCNN_X3_LAUNCH
   } else {
     const int mt = (M + BM - 1) / BM, nt = (N + BN - 1) / BN;

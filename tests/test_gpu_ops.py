@@ -185,6 +185,28 @@ def test_gemm_ragged_padded(hip, at, bt, prec):
     np.testing.assert_allclose(C.cpu().numpy(), ref, **_gemm_tol(prec, K))
 
 
+@pytest.mark.parametrize("shape", [(332, 88, 1000), (204, 300, 100), (88, 500, 404), (1152, 4096, 88)])
+@pytest.mark.parametrize("at,bt", [(0, 0), (0, 1), (1, 0), (1, 1)])
+def test_gemm_small_tile(hip, shape, at, bt):
+    """Shapes with an edge <= 128 (the fc8 GEMMs) run the 128 x 128 x3 tile:
+    A + A2, bias, relu, mask and a device-side M (333 live rows)."""
+    rng = np.random.default_rng(10)
+    M, N, K = shape
+    A = rng.normal(size=(M, K)).astype(np.float32)
+    A2 = rng.normal(size=(M, K)).astype(np.float32)
+    B = rng.normal(size=(K, N)).astype(np.float32)
+    bias = rng.normal(size=N).astype(np.float32)
+    mask = rng.normal(size=(M, N)).astype(np.float32)
+    live = min(M, 333)
+    Mdev = torch.tensor([live], dtype=torch.int32, device=D)
+    C = torch.zeros((M, N), dtype=torch.float32, device=D)
+    ph.gemm(T(A.T.copy() if at else A), T(B.T.copy() if bt else B), C, a_trans=at, b_trans=bt,
+            A2=T(A2.T.copy() if at else A2), bias=T(bias), act=1, mask=T(mask), M_dev=Mdev, precision=1)
+    ref = np.maximum((A[:live].astype(np.float64) + A2[:live]) @ B + bias, 0) * (mask[:live] > 0)
+    np.testing.assert_allclose(C[:live].cpu().numpy(), ref, **_gemm_tol(1, 2 * K))
+    assert not C[live:].cpu().numpy().any()
+
+
 def test_roi_pool_accumulate(hip, orc):
     """pool5 + pool4 produced in place by the second pool (both argmaxes kept)."""
     rng = np.random.default_rng(9)
