@@ -445,6 +445,9 @@ __device__ __forceinline__ void x_store(const float (&v)[16], char* hi, char* lo
   }
 }
 
+#ifndef PCNN_APF
+#define PCNN_APF 1
+#endif
 template <int T, bool A_T, bool B_T, bool RAGGED, bool A2>
 __global__ void __launch_bounds__(XTile<T>::threads, T == 256 ? 1 : 2) k_gemm_x3(GemmArgs g) {
   using X = XTile<T>;
@@ -507,34 +510,72 @@ __global__ void __launch_bounds__(XTile<T>::threads, T == 256 ? 1 : 2) k_gemm_x3
       // steady state, one basic block per step: MFMAs on buffer s & 1, stage
       // s+1 (registers) -> the other buffer, loads of stage s+2 (clamped to
       // the last stage: the surplus stores land in a buffer nobody reads)
-      for (int s = 0; s < nsteps; s++) {
-        const char* cur = xl + (s & 1) * kXStage;
-        char* nxt = xl + ((s + 1) & 1) * kXStage;
+#ifndef PCNN_STAGGER
+#define PCNN_STAGGER 0
+#endif
+      // PCNN_STAGGER: the SIMD partners (waves w, w + 4) run a step in
+      // opposite order (MFMAs then staging / staging then MFMAs).
+      const bool late = PCNN_STAGGER && (threadIdx.x >> 6) >= 4;
+      auto compute = [&](const char* cur) {
 #pragma unroll
-        for (int ks = 0; ks < 2; ks++) {
-          bf16x8 bh[2], bl[2];
-#pragma unroll
-          for (int j = 0; j < 2; j++) {
-            bh[j] = *(const bf16x8*)(cur + 2 * kXPart + b_off[ks][j]);
-            bl[j] = *(const bf16x8*)(cur + 3 * kXPart + b_off[ks][j]);
-          }
-#pragma unroll
-          for (int i = 0; i < AM; i++) {
-            const bf16x8 ah = *(const bf16x8*)(cur + a_off[ks][i]);
-            const bf16x8 al = *(const bf16x8*)(cur + kXPart + a_off[ks][i]);
+          for (int ks = 0; ks < 2; ks++) {
+            bf16x8 bh[2], bl[2];
 #pragma unroll
             for (int j = 0; j < 2; j++) {
-              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh[j], acc[i][j], 0, 0, 0);
-              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl[j], acc[i][j], 0, 0, 0);
-              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh[j], acc[i][j], 0, 0, 0);
+              bh[j] = *(const bf16x8*)(cur + 2 * kXPart + b_off[ks][j]);
+              bl[j] = *(const bf16x8*)(cur + 3 * kXPart + b_off[ks][j]);
             }
+#if PCNN_APF
+            // A fragments one accumulator row ahead: the reads of row i + 1 are
+            // in flight while row i's six MFMAs issue
+            bf16x8 ah[2], al[2];
+            ah[0] = *(const bf16x8*)(cur + a_off[ks][0]);
+            al[0] = *(const bf16x8*)(cur + kXPart + a_off[ks][0]);
+#pragma unroll
+            for (int i = 0; i < AM; i++) {
+              if (i + 1 < AM) {
+                ah[(i + 1) & 1] = *(const bf16x8*)(cur + a_off[ks][i + 1]);
+                al[(i + 1) & 1] = *(const bf16x8*)(cur + kXPart + a_off[ks][i + 1]);
+              }
+#pragma unroll
+              for (int j = 0; j < 2; j++) {
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i & 1], bh[j], acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i & 1], bl[j], acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i & 1], bh[j], acc[i][j], 0, 0, 0);
+              }
+            }
+#else
+#pragma unroll
+            for (int i = 0; i < AM; i++) {
+              const bf16x8 ah = *(const bf16x8*)(cur + a_off[ks][i]);
+              const bf16x8 al = *(const bf16x8*)(cur + kXPart + a_off[ks][i]);
+#pragma unroll
+              for (int j = 0; j < 2; j++) {
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh[j], acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl[j], acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh[j], acc[i][j], 0, 0, 0);
+              }
+            }
+#endif
           }
-        }
+      };
+      auto stage = [&](char* nxt, int s) {
         x_store<T, A_KC>(va, nxt, nxt + kXPart);
         x_store<T, B_KC>(vb, nxt + 2 * kXPart, nxt + 3 * kXPart);
         const int s2 = s + 2 < nsteps ? s + 2 : nsteps - 1;
         x_load<T, A_KC, RAGGED, A2>(oa, oa2, m0, Meff, kb + s2 * XBK, ke, va);
         x_load<T, B_KC, RAGGED, false>(ob, onull, n0, g.N, kb + s2 * XBK, ke, vb);
+      };
+      for (int s = 0; s < nsteps; s++) {
+        const char* cur = xl + (s & 1) * kXStage;
+        char* nxt = xl + ((s + 1) & 1) * kXStage;
+        if (late) {
+          stage(nxt, s);
+          compute(cur);
+        } else {
+          compute(cur);
+          stage(nxt, s);
+        }
         __syncthreads();
       }
     }
@@ -576,6 +617,9 @@ __global__ void __launch_bounds__(XTile<T>::threads, T == 256 ? 1 : 2) k_gemm_x3
             v += bv;
             if (g.act == 1) v = v > 0.f ? v : 0.f;
             if (msk && !(mv[gi & 1][q] > 0.f)) v = 0.f;
+#ifdef PCNN_ABL_NOEPI
+            if (v != 1.2345e-30f) continue;
+#endif
             __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), oc.rs,
                                                   ok ? (unsigned)(m * g.ldc + n) * 4u : kXOob, 0, 0);
           } else {
