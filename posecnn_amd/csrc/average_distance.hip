@@ -25,8 +25,9 @@ namespace {
 
 constexpr int kAddThreads = 256;
 constexpr int kPtsPlain = kAddThreads;         // points per partial slot (plain rows: strided)
-constexpr int kPPL = 2;                        // symmetric rows: query points per lane
-constexpr int kPts = kAddThreads * kPPL;       // points per (row, chunk) item
+constexpr int kSymLanes = 128;                 // symmetric rows: lanes per candidate group
+constexpr int kPPL = 4;                        // query points per lane (independent min chains)
+constexpr int kPts = kSymLanes * kPPL;         // query points per (row, chunk) item
 constexpr int kMaxPointsLds = 8192;            // float4 candidates in LDS (128 KB)
 
 __device__ __forceinline__ int rows_of(const int32_t* dev, int cap) {
@@ -55,7 +56,17 @@ __device__ __forceinline__ int row_class(const float* __restrict__ weight, int n
   return -1;
 }
 
-__global__ void __launch_bounds__(kAddThreads) k_add_rows(const float* __restrict__ pred,
+// Symmetric rows: a 1024-thread workgroup owns (row, chunk of kPts query
+// points); its eight 128-lane groups scan disjoint eighths of the candidate
+// list for the same query points (the first-minimum update is a dependent
+// chain, so latency, not issue, bounds a lone wave: 16 waves per item and
+// kPPL chains per lane), then merge in LDS in group order with a strict < —
+// a later range wins only with a strictly smaller distance, which is exactly
+// the reference's sequential first minimum (cu.cc:150-172).
+constexpr int kSymGroups = 8;
+constexpr int kSymThreads = kSymLanes * kSymGroups;
+
+__global__ void __launch_bounds__(kSymThreads) k_add_rows(const float* __restrict__ pred,
                                                            const float* __restrict__ target,
                                                            const float* __restrict__ weight,
                                                            const float* __restrict__ points,
@@ -68,9 +79,14 @@ __global__ void __launch_bounds__(kAddThreads) k_add_rows(const float* __restric
                                                            const int32_t* __restrict__ nsym,
                                                            float* __restrict__ partial) {
   extern __shared__ __attribute__((aligned(16))) float4 gpts[];  // [P] GT-rotated points
-  __shared__ float red[kAddThreads / 64][5];
+  __shared__ float mdist[kSymGroups - 1][kPts];                   // quarter minima of groups 1..3
+  __shared__ int midx[kSymGroups - 1][kPts];
+  __shared__ float red[kSymLanes / 64][5];
   const int R = rows_of(num_rois_dev, R_cap);
   const int items = *nsym * nchunk;
+  const int grp = threadIdx.x / kSymLanes, lt = threadIdx.x % kSymLanes;
+  const int quarter = ((P + kSymGroups - 1) / kSymGroups + 3) / 4 * 4;
+  const int c0 = grp * quarter, c1 = min(P, c0 + quarter);
   for (int item = blockIdx.x; item < items; item += gridDim.x) {
   const int n = sym_rows[item / nchunk], chunk = item % nchunk;
   const int PC = 4 * C;
@@ -83,23 +99,20 @@ __global__ void __launch_bounds__(kAddThreads) k_add_rows(const float* __restric
   const float s = pq[0], u = pq[1], v = pq[2], w = pq[3];
   quat2rot(s, u, v, w, Rp);
   const float* pts = points + (size_t)cls * P * 3;
-  const bool sym = symmetry[cls] > 0;
-  if (sym) {
-    for (int i = threadIdx.x; i < P; i += blockDim.x) {
-      const float X0 = pts[i * 3 + 0], X1 = pts[i * 3 + 1], X2 = pts[i * 3 + 2];
-      gpts[i] = make_float4(Rg[0] * X0 + Rg[1] * X1 + Rg[2] * X2, Rg[3] * X0 + Rg[4] * X1 + Rg[5] * X2,
-                            Rg[6] * X0 + Rg[7] * X1 + Rg[8] * X2, 0.f);
-    }
-    __syncthreads();
+  for (int i = threadIdx.x; i < P; i += blockDim.x) {
+    const float X0 = pts[i * 3 + 0], X1 = pts[i * 3 + 1], X2 = pts[i * 3 + 2];
+    gpts[i] = make_float4(Rg[0] * X0 + Rg[1] * X1 + Rg[2] * X2, Rg[3] * X0 + Rg[4] * X1 + Rg[5] * X2,
+                          Rg[6] * X0 + Rg[7] * X1 + Rg[8] * X2, 0.f);
   }
-  // kPPL query points per lane (points p0 + k*kAddThreads): each broadcast
+  __syncthreads();
+  // kPPL query points per lane (points p0 + k*kSymLanes): each broadcast
   // candidate read serves kPPL distances and the lane carries kPPL
   // independent first-minimum chains
   float qx[kPPL], qy[kPPL], qz[kPPL], Xq[kPPL][3];
   int pq_[kPPL];
 #pragma unroll
   for (int k = 0; k < kPPL; k++) {
-    const int p = chunk * kPts + k * kAddThreads + threadIdx.x;
+    const int p = chunk * kPts + k * kSymLanes + lt;
     pq_[k] = p;
     const int pp = p < P ? p : 0;
     Xq[k][0] = pts[pp * 3 + 0]; Xq[k][1] = pts[pp * 3 + 1]; Xq[k][2] = pts[pp * 3 + 2];
@@ -107,83 +120,132 @@ __global__ void __launch_bounds__(kAddThreads) k_add_rows(const float* __restric
     qy[k] = Rp[3] * Xq[k][0] + Rp[4] * Xq[k][1] + Rp[5] * Xq[k][2];
     qz[k] = Rp[6] * Xq[k][0] + Rp[7] * Xq[k][1] + Rp[8] * Xq[k][2];
   }
-  // nearest GT-rotated model point, scanned in index order with a strict <
-  // (cu.cc:150-172: the first minimum); candidates are wave-uniform LDS
-  // broadcasts, eight in flight per iteration
+  // Nearest GT-rotated model point of this group's range [c0, c1) with the
+  // reference's first-minimum semantics (strict <, index order, NaN never
+  // wins; cu.cc:150-172), in two exact steps: a running minimum over blocks
+  // of 4 candidates (block minimum by v_min3 -- fminf drops NaN like the
+  // strict < does; the running minimum updates only on a strictly smaller
+  // block minimum, remembering the block), then the first index of that block
+  // whose distance, recomputed by the same expression, equals the minimum.
+  // The per-candidate compare/select pair of a direct scan becomes ~1/2 min.
+  auto dist_to = [&](int k, const float4& c) {
+    return (qx[k] - c.x) * (qx[k] - c.x) + (qy[k] - c.y) * (qy[k] - c.y) + (qz[k] - c.z) * (qz[k] - c.z);
+  };
   float dmin[kPPL];
-  int imin[kPPL];
+  int iblk[kPPL];
 #pragma unroll
-  for (int k = 0; k < kPPL; k++) { dmin[k] = FLT_MAX; imin[k] = -1; }
-  int i = 0;
-  for (; i + 8 <= P; i += 8) {
-    float4 c[8];
+  for (int k = 0; k < kPPL; k++) { dmin[k] = FLT_MAX; iblk[k] = -1; }
+  // query points in pairs (k, k + 1): every sub / mul / add of a distance is
+  // one packed-fp32 instruction over two evaluations, in the scalar
+  // expression's association order (bitwise the same as dist_to)
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  f2 px[kPPL / 2], py[kPPL / 2], pz[kPPL / 2];
 #pragma unroll
-    for (int j = 0; j < 8; j++) c[j] = gpts[i + j];
-#pragma unroll
-    for (int j = 0; j < 8; j++)
-#pragma unroll
-      for (int k = 0; k < kPPL; k++) {
-        const float dist = (qx[k] - c[j].x) * (qx[k] - c[j].x) + (qy[k] - c[j].y) * (qy[k] - c[j].y) +
-                           (qz[k] - c[j].z) * (qz[k] - c[j].z);
-        if (dist < dmin[k]) { dmin[k] = dist; imin[k] = i + j; }
-      }
+  for (int h = 0; h < kPPL / 2; h++) {
+    px[h] = (f2){qx[2 * h], qx[2 * h + 1]};
+    py[h] = (f2){qy[2 * h], qy[2 * h + 1]};
+    pz[h] = (f2){qz[2 * h], qz[2 * h + 1]};
   }
-  for (; i < P; i++) {
+  int i = c0;
+  for (; i + 4 <= c1; i += 4) {
+    float4 c[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) c[j] = gpts[i + j];
+#pragma unroll
+    for (int h = 0; h < kPPL / 2; h++) {
+      f2 d[4];
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const f2 ex = px[h] - c[j].x, ey = py[h] - c[j].y, ez = pz[h] - c[j].z;
+        d[j] = ex * ex + ey * ey + ez * ez;
+      }
+#pragma unroll
+      for (int e = 0; e < 2; e++) {
+        const int k = 2 * h + e;
+        const float bm = fminf(fminf(d[0][e], d[1][e]), fminf(d[2][e], d[3][e]));
+        if (bm < dmin[k]) { dmin[k] = bm; iblk[k] = i; }
+      }
+    }
+  }
+  for (; i < c1; i++) {  // ragged tail: blocks of one
     const float4 c = gpts[i];
 #pragma unroll
     for (int k = 0; k < kPPL; k++) {
-      const float dist = (qx[k] - c.x) * (qx[k] - c.x) + (qy[k] - c.y) * (qy[k] - c.y) + (qz[k] - c.z) * (qz[k] - c.z);
-      if (dist < dmin[k]) { dmin[k] = dist; imin[k] = i; }
+      const float d = dist_to(k, c);
+      if (d < dmin[k]) { dmin[k] = d; iblk[k] = i; }
     }
   }
-  float acc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+  if (grp > 0) {
 #pragma unroll
-  for (int k = 0; k < kPPL; k++) {
-    if (pq_[k] >= P) continue;
-    const int im = imin[k] < 0 ? pq_[k] : imin[k];  // no finite distance (index_min unset in the reference)
-    const float4 cm = gpts[im];
-    const float x1 = qx[k], y1 = qy[k], z1 = qz[k], x2 = cm.x, y2 = cm.y, z2 = cm.z;
-    const float X0 = Xq[k][0], X1 = Xq[k][1], X2 = Xq[k][2];
-    {
-    const int Rn = norm_rows_dev ? *norm_rows_dev : (norm_rows > 0 ? norm_rows : R);
-    const float bn = (float)(Rn * P);
-    const double ln = 2.0 * (double)Rn * (double)P;
-    const float dist = (x1 - x2) * (x1 - x2) + (y1 - y2) * (y1 - y2) + (z1 - z2) * (z1 - z2);
-    if (!(dist < margin)) {  // cu.cc:178-179
-      acc[0] += (float)((double)(dist - margin) / ln);  // cu.cc:181
-      // derivative matrices of Rp w.r.t. (s, u, v, w) (cu.cc:97-139)
-      const float d0[9] = {2 * s, -2 * w, 2 * v, 2 * w, 2 * s, -2 * u, -2 * v, 2 * u, 2 * s};
-      const float d1[9] = {2 * u, 2 * v, 2 * w, 2 * v, -2 * u, -2 * s, 2 * w, 2 * s, -2 * u};
-      const float d2[9] = {-2 * v, 2 * u, 2 * s, 2 * u, 2 * v, 2 * w, -2 * s, 2 * w, -2 * v};
-      const float d3[9] = {-2 * w, -2 * s, 2 * u, 2 * s, -2 * w, 2 * v, 2 * u, 2 * v, 2 * w};
-      const float X[3] = {X0, X1, X2};
-      const float df[3] = {x1 - x2, y1 - y2, z1 - z2};
-      float e0 = 0.f, e1 = 0.f, e2 = 0.f, e3 = 0.f;  // this point's terms, reference order
-#pragma unroll
-      for (int a = 0; a < 3; a++)
-#pragma unroll
-        for (int b = 0; b < 3; b++) {  // cu.cc:183-203, same operation order
-          e0 += df[a] * X[b] * d0[a * 3 + b] / bn;
-          e1 += df[a] * X[b] * d1[a * 3 + b] / bn;
-          e2 += df[a] * X[b] * d2[a * 3 + b] / bn;
-          e3 += df[a] * X[b] * d3[a * 3 + b] / bn;
-        }
-      acc[1] += e0; acc[2] += e1; acc[3] += e2; acc[4] += e3;
+    for (int k = 0; k < kPPL; k++) {
+      mdist[grp - 1][k * kSymLanes + lt] = dmin[k];
+      midx[grp - 1][k * kSymLanes + lt] = iblk[k];
     }
   }
-  }
+  __syncthreads();
+  if (grp == 0) {
+    int imin[kPPL];
 #pragma unroll
-  for (int q = 0; q < 5; q++) acc[q] = pcnn::wave_sum(acc[q]);
-  const int wv = threadIdx.x >> 6;
-  if (pcnn::lane_id() == 0)
-    for (int q = 0; q < 5; q++) red[wv][q] = acc[q];
+    for (int k = 0; k < kPPL; k++) {
+#pragma unroll
+      for (int g = 0; g < kSymGroups - 1; g++) {  // group order, strict <: the earliest range wins ties
+        const float d = mdist[g][k * kSymLanes + lt];
+        if (d < dmin[k]) { dmin[k] = d; iblk[k] = midx[g][k * kSymLanes + lt]; }
+      }
+      imin[k] = -1;
+      if (iblk[k] >= 0) {
+        const int e = min(iblk[k] + 4, P);
+        for (int j = iblk[k]; j < e; j++)
+          if (dist_to(k, gpts[j]) == dmin[k]) { imin[k] = j; break; }
+      }
+    }
+    float acc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < kPPL; k++) {
+      if (pq_[k] >= P) continue;
+      const int im = imin[k] < 0 ? pq_[k] : imin[k];  // no finite distance (index_min unset in the reference)
+      const float4 cm = gpts[im];
+      const float x1 = qx[k], y1 = qy[k], z1 = qz[k], x2 = cm.x, y2 = cm.y, z2 = cm.z;
+      const float X0 = Xq[k][0], X1 = Xq[k][1], X2 = Xq[k][2];
+      const int Rn = norm_rows_dev ? *norm_rows_dev : (norm_rows > 0 ? norm_rows : R);
+      const float bn = (float)(Rn * P);
+      const double ln = 2.0 * (double)Rn * (double)P;
+      const float dist = (x1 - x2) * (x1 - x2) + (y1 - y2) * (y1 - y2) + (z1 - z2) * (z1 - z2);
+      if (!(dist < margin)) {  // cu.cc:178-179
+        acc[0] += (float)((double)(dist - margin) / ln);  // cu.cc:181
+        // derivative matrices of Rp w.r.t. (s, u, v, w) (cu.cc:97-139)
+        const float d0[9] = {2 * s, -2 * w, 2 * v, 2 * w, 2 * s, -2 * u, -2 * v, 2 * u, 2 * s};
+        const float d1[9] = {2 * u, 2 * v, 2 * w, 2 * v, -2 * u, -2 * s, 2 * w, 2 * s, -2 * u};
+        const float d2[9] = {-2 * v, 2 * u, 2 * s, 2 * u, 2 * v, 2 * w, -2 * s, 2 * w, -2 * v};
+        const float d3[9] = {-2 * w, -2 * s, 2 * u, 2 * s, -2 * w, 2 * v, 2 * u, 2 * v, 2 * w};
+        const float X[3] = {X0, X1, X2};
+        const float df[3] = {x1 - x2, y1 - y2, z1 - z2};
+        float e0 = 0.f, e1 = 0.f, e2 = 0.f, e3 = 0.f;  // this point's terms, reference order
+#pragma unroll
+        for (int a = 0; a < 3; a++)
+#pragma unroll
+          for (int b = 0; b < 3; b++) {  // cu.cc:183-203, same operation order
+            e0 += df[a] * X[b] * d0[a * 3 + b] / bn;
+            e1 += df[a] * X[b] * d1[a * 3 + b] / bn;
+            e2 += df[a] * X[b] * d2[a * 3 + b] / bn;
+            e3 += df[a] * X[b] * d3[a * 3 + b] / bn;
+          }
+        acc[1] += e0; acc[2] += e1; acc[3] += e2; acc[4] += e3;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 5; q++) acc[q] = pcnn::wave_sum(acc[q]);
+    const int wv = threadIdx.x >> 6;
+    if (pcnn::lane_id() == 0)
+      for (int q = 0; q < 5; q++) red[wv][q] = acc[q];
+  }
   __syncthreads();
   if (threadIdx.x < 5) {
     float t = 0.f;
-    for (int i = 0; i < (int)(blockDim.x >> 6); i++) t += red[i][threadIdx.x];
+    for (int i = 0; i < kSymLanes / 64; i++) t += red[i][threadIdx.x];
     out[threadIdx.x] = t;
   }
-  __syncthreads();  // red / gpts reused by the next item
+  __syncthreads();  // red / gpts / mdist reused by the next item
   }
 }
 
@@ -385,8 +447,8 @@ extern "C" int pcnn_add_loss_fwd(const float* pred, const float* target, const f
                      num_rois_dev, C, P, margin, loss_norm_rows, loss_norm_rows_dev, nchunk, rcls, partial);
   // symmetric rows: persistent grid over (row, chunk) items of the device-side list
   const long sym_items = (long)R_cap * nchunk;
-  const int sym_grid = (int)(sym_items < 1024 ? sym_items : 1024);
-  hipLaunchKernelGGL(k_add_rows, dim3(sym_grid), dim3(kAddThreads), (size_t)P * sizeof(float4), st, pred,
+  const int sym_grid = (int)(sym_items < 512 ? sym_items : 512);
+  hipLaunchKernelGGL(k_add_rows, dim3(sym_grid), dim3(kSymThreads), (size_t)P * sizeof(float4), st, pred,
                      target, weight, points, symmetry, R_cap, num_rois_dev, C, P, margin, loss_norm_rows,
                      loss_norm_rows_dev, nchunk, rcls, sym_rows, nsym, partial);
   hipLaunchKernelGGL(k_add_finish_rows, dim3((R_cap + 3) / 4), dim3(256), 0, st, R_cap, num_rois_dev, C, nchunk,

@@ -97,6 +97,36 @@ def test_add_loss_identity_zero(hip, orc):
     assert float(loss.item()) == 0.0 and not diff.cpu().numpy().any()
 
 
+def test_add_loss_symmetric_ties(hip, orc):
+    """ADD-S first-minimum tie-breaking: lattice model points with pred = identity
+    and target = the unnormalised quaternion (1, 0, 0, 1) (exactly 2 x Rot90z in
+    float) make exact distance ties between different candidates everywhere —
+    across blocks of 4 and across the candidate ranges the lane groups split.
+    The gradient of a row depends on which tied candidate wins, so bitwise
+    agreement with the sequential strict-< scan of the oracle checks it."""
+    rng = np.random.default_rng(11)
+    C, P, R = 3, 1500, 6
+    pts = np.zeros((C, P, 3), np.float32)
+    pts[1] = rng.integers(-3, 4, size=(P, 3)).astype(np.float32)
+    pts[2] = rng.integers(-2, 3, size=(P, 3)).astype(np.float32)
+    sym = np.array([0, 1, 1], np.float32)
+    pred = np.zeros((R, 4 * C), np.float32)
+    target = np.zeros((R, 4 * C), np.float32)
+    weight = np.zeros((R, 4 * C), np.float32)
+    for r in range(R):
+        c = 1 + r % 2
+        pred[r, 4 * c:4 * c + 4] = [1, 0, 0, 0] if r < 4 else [0, 1, 0, 0]
+        target[r, 4 * c:4 * c + 4] = [1, 0, 0, 1] if r % 3 else [0, 0, 1, 1]
+        weight[r, 4 * c:4 * c + 4] = 1
+    loss, diff = adl.average_distance_loss(T(pred), T(target), T(weight), T(pts), T(sym), 0.01)
+    ol, od, _ = orc.average_distance_loss(pred, target, weight, pts, sym, 0.01)
+    # the loss does not depend on which tied candidate wins (equal distances):
+    # its tolerance covers summation order only; a wrong pick moves a row's
+    # gradient by O(1) relative
+    np.testing.assert_allclose(loss.cpu().numpy(), ol, rtol=1e-5)
+    np.testing.assert_allclose(diff.cpu().numpy(), od, rtol=1e-4, atol=1e-6 * np.abs(od).max())
+
+
 def test_backproject(hip, orc):
     rng = np.random.default_rng(4)
     B, H, W, Ch, NC, G = 2, 48, 64, 16, 5, 12
