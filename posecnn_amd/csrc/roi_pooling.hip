@@ -11,19 +11,17 @@
 //
 // Backward: the reference gives every bottom element one thread that loops
 // over ALL RoIs (O(B*H*W*C*R), cu.cc:134-229).  Here the RoI geometry is
-// computed once (k_roi_prep); each workgroup owns a 4x8 pixel tile of one
-// image, stages the (ordered) list of RoIs that intersect the tile in LDS, and
-// one wave per pixel accumulates the argmax-matching top gradients of the 1-4
-// bins containing it, in the reference's order (RoI ascending, ph, pw) — the
-// fp32 sums are bit-equal to the reference kernel's.
+// computed once (k_roi_prep); each workgroup owns a 2x4 pixel tile of one
+// image and a 128-channel chunk, lists the (RoI, ph, pw) entries whose bins
+// can feed the tile in the reference's order (RoI ascending, ph, pw), reads
+// each entry once and accumulates the argmax-matching top gradients per tile
+// pixel in registers — the fp32 sums are bit-equal to the reference kernel's.
 #include "pcnn_common.h"
 #include <math.h>
 #include <cfloat>
 
 namespace {
 
-constexpr int kTileH = 2, kTileW = 4;
-constexpr int kMaxTileRois = 1024;
 
 struct RoiGeo {
   int b, cls, sw, sh, ew, eh;
@@ -209,148 +207,173 @@ __global__ void __launch_bounds__(1024) k_roi_prep(const float* __restrict__ roi
   }
 }
 
-// NHWC all-channel backward, C % 4 == 0: block = kTileH x kTileW pixel tile of
-// one image.  The RoIs touching the tile are compacted (in order) into LDS;
-// then one wave per pixel (1) tests the listed RoIs in parallel across lanes,
-// (2) expands the containing RoIs, in order, into their (ph, pw) bins — the
-// reference's summation order — as a wave-private entry list, and (3) issues
-// the argmax / top-gradient loads of kBatch entries at a time before
-// accumulating them in order (memory-level parallelism instead of one
-// dependent round trip per bin).
-constexpr int kEntCap = 64;
-constexpr int kBatch = 4;
+// NHWC all-channel backward, C % 2 == 0: one wave per (image, 2 x 4 pixel
+// tile, 128-channel chunk), two channels per lane.  The
+// reference gathers, per bottom element, over every RoI and every bin that can
+// hold it (cu.cc:134-229); here the work is turned around.  Wave 0 lists the
+// (RoI, ph, pw) entries whose bins can feed the tile — RoIs ascending, then
+// ph, then pw: the reference's summation order — each with the 8-bit mask of
+// tile pixels that pass the reference's own membership tests for it (inside
+// the RoI box, ph in [phstart, phend), pw in [pwstart, pwend),
+// cu.cc:172-204).  It then reads each listed entry's argmax / top
+// gradient once (8 B per lane per operand, two batches of kBBatch entries in
+// flight: the next batch loads while the current one accumulates) and,
+// for every masked tile pixel, add the top gradient of each channel whose
+// argmax names that pixel to a register accumulator (cu.cc:219-224) — in
+// list order, so the fp32 sums are bit-equal to the reference's.
+constexpr int kBTH = 2, kBTW = 4, kBPix = kBTH * kBTW;
+constexpr int kBWaves = 1;  // one wave per workgroup: a tile's channel chunks land on different CUs
+constexpr int kBChunk = 128 * kBWaves;  // channels per workgroup
+constexpr int kBGroup = 16;             // RoIs expanded per list round (<= 16 * 49 entries)
+constexpr int kBCap = kBGroup * 49;
+constexpr int kBBatch = 8;              // entries per fetch (two fetches in flight per wave)
 
-__global__ void __launch_bounds__(256) k_roi_bwd_tile(const float* __restrict__ top_diff,
-                                                       const int32_t* __restrict__ argmax, int B, int H, int W, int C,
-                                                       const int32_t* __restrict__ geo, const int32_t* __restrict__ lo,
-                                                       const int32_t* __restrict__ hi, int PH, int PW,
-                                                       float* __restrict__ bottom) {
-  __shared__ int lst[kMaxTileRois];
-  __shared__ int4 lgeo[kMaxTileRois];    // sw, sh, ew, eh of listed RoIs
-  __shared__ float2 lbin[kMaxTileRois];  // bin_h, bin_w
-  __shared__ int ent[4][kEntCap];        // per wave: element offsets ((r*PH+ph)*PW+pw)*C
-  __shared__ int wcnt[4];
-  __shared__ int nlist;
-  const int tiles_w = (W + kTileW - 1) / kTileW, tiles_h = (H + kTileH - 1) / kTileH;
-  const int b = blockIdx.x / (tiles_w * tiles_h);
-  const int t = blockIdx.x % (tiles_w * tiles_h);
-  const int h0 = (t / tiles_w) * kTileH, w0 = (t % tiles_w) * kTileW;
-  const int h1 = min(h0 + kTileH, H) - 1, w1 = min(w0 + kTileW, W) - 1;
+__global__ void __launch_bounds__(64 * kBWaves) k_roi_bwd_ent(const float* __restrict__ top_diff,
+                                                               const int32_t* __restrict__ argmax, int B, int H, int W,
+                                                               int C, const int32_t* __restrict__ geo,
+                                                               const int32_t* __restrict__ lo,
+                                                               const int32_t* __restrict__ hi, int PH, int PW,
+                                                               float* __restrict__ bottom) {
+  __shared__ int2 ent[kBCap];  // element offset ((r*PH+ph)*PW+pw)*C, pixel mask
+  __shared__ int sh_total;
+  const int tiles_w = (W + kBTW - 1) / kBTW, tiles_h = (H + kBTH - 1) / kBTH;
+  const int nchunk = (C + kBChunk - 1) / kBChunk;
+  int id = blockIdx.x;
+  const int chunk = id % nchunk;
+  id /= nchunk;
+  const int t = id % (tiles_w * tiles_h), b = id / (tiles_w * tiles_h);
+  const int h0 = (t / tiles_w) * kBTH, w0 = (t % tiles_w) * kBTW;
+  const int th = min(kBTH, H - h0), tw = min(kBTW, W - w0);
   const int lane = pcnn::lane_id(), wave = threadIdx.x >> 6;
-  const int r0 = lo[b], r1 = hi[b];
-  if (threadIdx.x == 0) nlist = 0;
-  __syncthreads();
-  for (int base = r0; base <= r1; base += blockDim.x) {  // ordered compaction
-    const int r = base + threadIdx.x;
-    bool hit = false;
-    if (r <= r1) {
-      const int32_t* g = geo + (size_t)r * 8;
-      hit = g[0] == b && g[3] <= h1 && g[5] >= h0 && g[2] <= w1 && g[4] >= w0;
-    }
-    const uint64_t m = __ballot(hit);
-    if (lane == 0) wcnt[wave] = __popcll(m);
-    __syncthreads();
-    int off = nlist;
-    for (int w = 0; w < wave; w++) off += wcnt[w];
-    if (hit) {
-      const int pos = off + __popcll(m & pcnn::lanemask_lt());
-      if (pos < kMaxTileRois) {
-        const int32_t* g = geo + (size_t)r * 8;
-        lst[pos] = r;
-        lgeo[pos] = make_int4(g[2], g[3], g[4], g[5]);
-        lbin[pos] = make_float2(__int_as_float(g[6]), __int_as_float(g[7]));
-      }
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) nlist += wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
-    __syncthreads();
+  const int c = chunk * kBChunk + 2 * threadIdx.x;  // this lane's channels c, c + 1
+  const bool cok = c < C;
+  float2 acc[kBPix];  // this lane's channels at the tile pixels
+  int expv[kBPix];    // the argmax value that names each tile pixel for channel c (cu.cc:219-224)
+#pragma unroll
+  for (int p = 0; p < kBPix; p++) {
+    acc[p] = make_float2(0.f, 0.f);
+    expv[p] = ((h0 + p / kBTW) * W + w0 + p % kBTW) * C + c;
   }
-  const int n = nlist;
-  const bool use_list = n <= kMaxTileRois;  // else scan the image's RoI range (same order)
-  const int nscan = use_list ? n : (r1 - r0 + 1);
-  int* my = ent[wave];
-  for (int p = wave; p < kTileH * kTileW; p += 4) {
-    const int h = h0 + p / kTileW, w = w0 + p % kTileW;
-    if (h >= H || w >= W) continue;
-    const int pix = (h * W + w) * C;
-    float* dst = bottom + ((size_t)b * H * W) * C + pix;
-    for (int c0 = 0; c0 < C; c0 += 512) {
-      const int ca = c0 + lane * 4, cb = c0 + 256 + lane * 4;
-      const bool va = ca < C, vb = cb < C;
-      float4 accA = make_float4(0.f, 0.f, 0.f, 0.f), accB = accA;
-      int ne = 0;
-      auto flush = [&]() {
-        for (int e0 = 0; e0 < ne; e0 += kBatch) {
-          int4 aa[kBatch], ab[kBatch];
-          float4 da[kBatch], db[kBatch];
-#pragma unroll
-          for (int k = 0; k < kBatch; k++) {
-            const int o = my[min(e0 + k, ne - 1)];
-            aa[k] = va ? *(const int4*)(argmax + o + ca) : make_int4(-1, -1, -1, -1);
-            da[k] = va ? *(const float4*)(top_diff + o + ca) : make_float4(0.f, 0.f, 0.f, 0.f);
-            ab[k] = vb ? *(const int4*)(argmax + o + cb) : make_int4(-1, -1, -1, -1);
-            db[k] = vb ? *(const float4*)(top_diff + o + cb) : make_float4(0.f, 0.f, 0.f, 0.f);
-          }
-#pragma unroll
-          for (int k = 0; k < kBatch; k++) {
-            if (e0 + k >= ne) break;
-            const int ia = pix + ca, ib = pix + cb;
-            if (aa[k].x == ia + 0) accA.x += da[k].x;
-            if (aa[k].y == ia + 1) accA.y += da[k].y;
-            if (aa[k].z == ia + 2) accA.z += da[k].z;
-            if (aa[k].w == ia + 3) accA.w += da[k].w;
-            if (ab[k].x == ib + 0) accB.x += db[k].x;
-            if (ab[k].y == ib + 1) accB.y += db[k].y;
-            if (ab[k].z == ib + 2) accB.z += db[k].z;
-            if (ab[k].w == ib + 3) accB.w += db[k].w;
-          }
+  const int r0 = lo[b], r1 = hi[b];
+  // buffer views: per-lane channel offset in a VGPR, the entry offset as the
+  // scalar soffset; lanes past C read out of range (-> 0 / never a match)
+  const __amdgpu_buffer_rsrc_t rs_t = __builtin_amdgcn_make_buffer_rsrc((void*)top_diff, (short)0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs_a = __builtin_amdgcn_make_buffer_rsrc((void*)argmax, (short)0, 0x7fffffff, 0x00020000);
+  const unsigned voff = cok ? (unsigned)c * 4u : 0x80000000u;
+  for (int rb = r0; rb <= r1; rb += 64) {
+    // wave 0: RoIs of image b whose box meets the tile, in order (cu.cc:154-177),
+    // with per-bin row / column acceptance bits for the tile pixels (cu.cc:196-204)
+    uint32_t rbits = 0;  // bit (ph * kBTH + i): tile row i accepts bin row ph
+    uint32_t cbits = 0;  // bit (pw * kBTW + j): tile col j accepts bin col pw
+    const int r = rb + lane;
+    if (wave == 0 && r <= r1) {
+      const int32_t* gg = geo + (size_t)r * 8;
+      RoiGeo g;
+      g.b = gg[0]; g.sw = gg[2]; g.sh = gg[3]; g.ew = gg[4]; g.eh = gg[5];
+      g.bin_h = __int_as_float(gg[6]);
+      g.bin_w = __int_as_float(gg[7]);
+      if (g.b == b && g.sh <= h0 + th - 1 && g.eh >= h0 && g.sw <= w0 + tw - 1 && g.ew >= w0) {
+        for (int i = 0; i < th; i++) {
+          const int h = h0 + i;
+          if (h < g.sh || h > g.eh) continue;
+          int s0 = (int)floorf((float)(h - g.sh) / g.bin_h), e0 = (int)ceilf((float)(h - g.sh + 1) / g.bin_h);
+          s0 = min(max(s0, 0), PH);
+          e0 = min(max(e0, 0), PH);
+          for (int ph = s0; ph < e0; ph++) rbits |= 1u << (ph * kBTH + i);
         }
-        ne = 0;
-      };
-      for (int l0 = 0; l0 < nscan; l0 += 64) {
-        // lanes test 64 listed RoIs at once (cu.cc:172-177)
-        const int li = l0 + lane;
-        bool in = false;
-        if (li < nscan) {
-          int4 g;
-          if (use_list) {
-            g = lgeo[li];
-          } else {
-            const int32_t* gg = geo + (size_t)(r0 + li) * 8;
-            g = gg[0] == b ? make_int4(gg[2], gg[3], gg[4], gg[5]) : make_int4(1, 1, 0, 0);
-          }
-          in = w >= g.x && w <= g.z && h >= g.y && h <= g.w;
-        }
-        uint64_t m = __ballot(in);
-        while (m) {  // containing RoIs in order
-          const int i = l0 + __ffsll((long long)m) - 1;
-          m &= m - 1;
-          const int r = use_list ? lst[i] : r0 + i;
-          RoiGeo g;
-          if (use_list) {
-            const int4 q = lgeo[i];
-            const float2 bn = lbin[i];
-            g.sw = q.x; g.sh = q.y; g.ew = q.z; g.eh = q.w; g.bin_h = bn.x; g.bin_w = bn.y;
-          } else {
-            const int32_t* gg = geo + (size_t)r * 8;
-            g.sw = gg[2]; g.sh = gg[3]; g.ew = gg[4]; g.eh = gg[5];
-            g.bin_h = __int_as_float(gg[6]);
-            g.bin_w = __int_as_float(gg[7]);
-          }
-          int phs, phe, pws, pwe;
-          bins_of_pixel(g, h, w, PH, PW, phs, phe, pws, pwe);
-          for (int ph = phs; ph < phe; ph++)
-            for (int pw = pws; pw < pwe; pw++) {
-              if (ne == kEntCap) flush();
-              if (lane == 0) my[ne] = ((r * PH + ph) * PW + pw) * C;
-              ne++;
-            }
+        for (int j = 0; j < tw; j++) {
+          const int w = w0 + j;
+          if (w < g.sw || w > g.ew) continue;
+          int s0 = (int)floorf((float)(w - g.sw) / g.bin_w), e0 = (int)ceilf((float)(w - g.sw + 1) / g.bin_w);
+          s0 = min(max(s0, 0), PW);
+          e0 = min(max(e0, 0), PW);
+          for (int pw = s0; pw < e0; pw++) cbits |= 1u << (pw * kBTW + j);
         }
       }
-      flush();
-      if (va) *(float4*)(dst + ca) = accA;
-      if (vb) *(float4*)(dst + cb) = accB;
     }
+    const uint64_t hits = __ballot(rbits && cbits);  // wave 0's view; 0 in the other wave
+    for (int g0 = 0; g0 < 64; g0 += kBGroup) {
+      if (wave == 0) {
+        const uint64_t gm = hits & (((1ull << kBGroup) - 1) << g0);
+        const bool mine = (gm >> lane) & 1;
+        int cnt = 0;
+        if (mine) {
+          int nph = 0, npw = 0;
+          for (int ph = 0; ph < PH; ph++) nph += ((rbits >> (ph * kBTH)) & ((1u << kBTH) - 1)) != 0;
+          for (int pw = 0; pw < PW; pw++) npw += ((cbits >> (pw * kBTW)) & ((1u << kBTW) - 1)) != 0;
+          cnt = nph * npw;
+        }
+        int off = cnt;  // inclusive wave scan
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+          const int v = __shfl_up(off, d, 64);
+          if (lane >= d) off += v;
+        }
+        if (lane == 63) sh_total = off;
+        off -= cnt;
+        if (mine) {
+          const int rbase = r * PH;
+          for (int ph = 0; ph < PH; ph++) {
+            const uint32_t rm = (rbits >> (ph * kBTH)) & ((1u << kBTH) - 1);
+            if (!rm) continue;
+            for (int pw = 0; pw < PW; pw++) {
+              const uint32_t cm = (cbits >> (pw * kBTW)) & ((1u << kBTW) - 1);
+              if (!cm) continue;
+              uint32_t m = 0;
+#pragma unroll
+              for (int i = 0; i < kBTH; i++)
+                if ((rm >> i) & 1) m |= cm << (i * kBTW);
+              ent[off++] = make_int2(((rbase + ph) * PW + pw) * C, (int)m);
+            }
+          }
+        }
+      }
+      __syncthreads();
+      const int total = sh_total;
+      // lane k reads entry e0 + k and hands its offset / mask to the wave
+      auto fetch = [&](int e0, int2& my, int2 (&av)[kBBatch], float2 (&dv)[kBBatch]) {
+        my = ent[min(e0 + (lane & (kBBatch - 1)), total - 1)];
+#pragma unroll
+        for (int k = 0; k < kBBatch; k++) {
+          const int so = __builtin_amdgcn_readlane(my.x, k) * 4;
+          av[k] = __builtin_bit_cast(int2, __builtin_amdgcn_raw_buffer_load_b64(rs_a, voff, so, 0));
+          dv[k] = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rs_t, voff, so, 0));
+        }
+      };
+      auto accumulate = [&](int e0, const int2& my, const int2 (&av)[kBBatch], const float2 (&dv)[kBBatch]) {
+#pragma unroll
+        for (int k = 0; k < kBBatch; k++) {
+          if (e0 + k >= total) break;
+          const uint32_t m = (uint32_t)__builtin_amdgcn_readlane(my.y, k);  // wave-uniform pixel mask
+#pragma unroll
+          for (int q = 0; q < kBPix; q++) {
+            if (!((m >> q) & 1)) continue;
+            // adding +0.0f leaves every partial sum bit-identical (none is ever -0)
+            acc[q].x += av[k].x == expv[q] ? dv[k].x : 0.f;
+            acc[q].y += av[k].y == expv[q] + 1 ? dv[k].y : 0.f;
+          }
+        }
+      };
+      if (total > 0) {
+        int2 myA, myB, avA[kBBatch], avB[kBBatch];
+        float2 dvA[kBBatch], dvB[kBBatch];
+        fetch(0, myA, avA, dvA);
+        for (int e0 = 0; e0 < total; e0 += 2 * kBBatch) {
+          if (e0 + kBBatch < total) fetch(e0 + kBBatch, myB, avB, dvB);
+          accumulate(e0, myA, avA, dvA);
+          if (e0 + 2 * kBBatch < total) fetch(e0 + 2 * kBBatch, myA, avA, dvA);
+          if (e0 + kBBatch < total) accumulate(e0 + kBBatch, myB, avB, dvB);
+        }
+      }
+      __syncthreads();
+    }
+  }
+  if (cok) {
+#pragma unroll
+    for (int i = 0; i < kBTH; i++)
+#pragma unroll
+      for (int j = 0; j < kBTW; j++)
+        if (i < th && j < tw) *(float2*)(bottom + (((size_t)b * H + h0 + i) * W + w0 + j) * C + c) = acc[i * kBTW + j];
   }
 }
 
@@ -463,12 +486,14 @@ extern "C" int pcnn_roi_pool_bwd(const float* top_diff, const int32_t* argmax, i
   int32_t* geo = cv.take<int32_t>((size_t)(R_cap > 0 ? R_cap : 1) * 8);
   hipLaunchKernelGGL(k_roi_prep, dim3(1), dim3(1024), 0, st, rois, R_cap, roi_stride, num_rois_dev, B,
                      spatial_scale, pooled_h, pooled_w, geo, lo, hi);
-  const bool vec = layout == 0 && !pool_channel && C % 4 == 0 && C <= 4096 &&
-                   (((uintptr_t)top_diff | (uintptr_t)argmax | (uintptr_t)bottom_diff) & 15) == 0;
+  const bool vec = layout == 0 && !pool_channel && C % 2 == 0 && pooled_h * kBTH <= 32 && pooled_w * kBTW <= 32 &&
+                   (long)H * W * C < (1l << 30) && (long)R_cap * pooled_h * pooled_w * C < (1l << 29) &&
+                   (((uintptr_t)top_diff | (uintptr_t)argmax | (uintptr_t)bottom_diff) & 7) == 0;
   if (vec) {
-    const int tiles = ((H + kTileH - 1) / kTileH) * ((W + kTileW - 1) / kTileW);
-    hipLaunchKernelGGL(k_roi_bwd_tile, dim3(B * tiles), dim3(256), 0, st, top_diff, argmax, B, H, W, C, geo, lo, hi,
-                       pooled_h, pooled_w, bottom_diff);
+    const int tiles = ((H + kBTH - 1) / kBTH) * ((W + kBTW - 1) / kBTW);
+    const int nchunk = (C + kBChunk - 1) / kBChunk;
+    hipLaunchKernelGGL(k_roi_bwd_ent, dim3(B * tiles * nchunk), dim3(64 * kBWaves), 0, st, top_diff, argmax, B, H, W, C,
+                       geo, lo, hi, pooled_h, pooled_w, bottom_diff);
   } else {
     if (hipMemsetAsync(bottom_diff, 0, (size_t)B * H * W * C * sizeof(float), st) != hipSuccess) return PCNN_EHIP;
     const long npix = (long)B * H * W;

@@ -1,9 +1,9 @@
-"""Summarise a rocprofv3 kernel_stats.csv: name, calls, avg us, share."""
+"""Print the rocprofv3 kernel_stats.csv under a directory: name, calls, avg us, % of total."""
 import csv
+import glob
 import sys
 
-r = list(csv.DictReader(open(sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/prof/run_kernel_stats.csv")))
-tot = sum(float(x["TotalDurationNs"]) for x in r)
-for x in r[:int(sys.argv[2]) if len(sys.argv) > 2 else 26]:
-    print(x["Name"][:70].ljust(72), x["Calls"].rjust(5), f"{float(x['AverageNs']) / 1e3:9.1f}",
-          f"{float(x['TotalDurationNs']) / tot * 100:6.1f}")
+d = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/prof"
+f = glob.glob(f"{d}/**/*kernel_stats.csv", recursive=True)[0]
+for r in csv.DictReader(open(f)):
+    print(f"{r['Name'][:70]:70s} {int(r['Calls']):6d} {float(r['AverageNs']) / 1e3:9.1f} {float(r['Percentage']):6.1f}")

@@ -45,6 +45,43 @@ def test_roi_pool_fwd_bwd(hip, orc, pool_channel):
     np.testing.assert_array_equal(dd.cpu().numpy(), od)
 
 
+@pytest.mark.parametrize("C,B,H,W,scale", [(512, 2, 60, 80, 1 / 8), (68, 3, 30, 40, 1 / 16), (260, 2, 13, 21, 1 / 4),
+                                            (96, 2, 7, 9, 1 / 2), (66, 2, 30, 40, 1 / 16), (3, 2, 30, 40, 1 / 16)])
+def test_roi_pool_bwd_overlap(hip, orc, C, B, H, W, scale):
+    """Heavily overlapping RoIs (jittered copies, as the train-mode Hough op
+    emits), tiny and huge bins, RoIs past the map edges, ragged tiles and
+    channel chunks; then arbitrary (malformed) argmax values — the backward
+    must follow the reference's own membership tests, not the forward's."""
+    rng = np.random.default_rng(int(C) * 7 + H)
+    data = rng.normal(size=(B, H, W, C)).astype(np.float32)
+    data[:, 2:6, 3:9] = 0.5  # plateaus -> first-max ties
+    s = 1.0 / scale
+    base = _rois(rng, 12, B, H, W, s)
+    rows = []
+    for r in base:
+        for dx in (-0.05, 0.0, 0.05):
+            for dy in (-0.05, 0.0):
+                q = r.copy()
+                w, h = q[4] - q[2], q[5] - q[3]
+                q[2] += dx * w; q[4] += dx * w; q[3] += dy * h; q[5] += dy * h
+                rows.append(q)
+    rois = np.array(rows, np.float32)
+    rois = rois[np.argsort(rois[:, 0], kind="stable")]
+    top, arg = rp.roi_pool(T(data), T(rois), 7, 7, scale, 0)
+    ot, oa = orc.roi_pool_fwd(data, rois, 7, 7, scale, 0)
+    np.testing.assert_array_equal(arg.cpu().numpy(), oa)
+    g = rng.normal(size=ot.shape).astype(np.float32)
+    dd = rp.roi_pool_grad(T(data), T(rois), arg, T(g), 7, 7, scale, 0)
+    od = orc.roi_pool_bwd(g, oa, data.shape, rois, 7, 7, scale, 0)
+    np.testing.assert_array_equal(dd.cpu().numpy(), od)
+    bad = oa.copy()
+    sel = rng.random(bad.shape) < 0.3
+    bad[sel] = rng.integers(-1, H * W * C, int(sel.sum()))
+    dd = rp.roi_pool_grad(T(data), T(rois), T(bad), T(g), 7, 7, scale, 0)
+    od = orc.roi_pool_bwd(g, bad, data.shape, rois, 7, 7, scale, 0)
+    np.testing.assert_array_equal(dd.cpu().numpy(), od)
+
+
 def test_roi_pool_device_count(hip, orc):
     rng = np.random.default_rng(1)
     B, H, W, C = 2, 60, 80, 512
