@@ -115,9 +115,10 @@ _ws = {}
 
 
 def workspace(nbytes, device, tag="default"):
-    """Per-(device, tag) grow-only byte workspace (no allocation on the hot path
-    once sized)."""
-    key = (str(device), tag)
+    """Per-(device, tag, current stream) grow-only byte workspace (no
+    allocation on the hot path once sized; ops on different streams never
+    share scratch)."""
+    key = (str(device), tag, torch.cuda.current_stream(device).cuda_stream)
     buf = _ws.get(key)
     if buf is None or buf.numel() < nbytes:
         buf = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)

@@ -31,7 +31,8 @@ CAP = hv.CAPACITY
 class PoseStep:
     def __init__(self, B, H, W, num_classes, device, conv4_hw=None, conv5_hw=None, channels=512, units=4096,
                  is_train=1, skip_pixels=10, vote_threshold=-1.0, vote_percentage=0.02, margin=0.01,
-                 global_batch=None, batch_base=0, weights=None, dist=None, backward=True, precision=1):
+                 global_batch=None, batch_base=0, weights=None, dist=None, backward=True, precision=1,
+                 overlap_weight_grads=True):
         self.B, self.H, self.W, self.C = B, H, W, num_classes
         self.dev = device
         self.is_train, self.skip, self.vthr, self.vper, self.margin = is_train, skip_pixels, vote_threshold, \
@@ -75,6 +76,8 @@ class PoseStep:
         self.norm_rows = torch.zeros((1,), **i32)
         self.timer = None  # optional {name: [(start_event, end_event), ...]} (bench.py)
         self.xchg = RoiExchange(dist, CAP, device) if dist is not None else None
+        # weight-gradient branch of the backward (None: everything on the caller's stream)
+        self.side_stream = torch.cuda.Stream(device=device) if overlap_weight_grads else None
 
     # ------------------------------------------------------------------
     def _t(self, name):
@@ -137,31 +140,52 @@ class PoseStep:
         return self.loss
 
     def backward_pass(self, conv4, conv5):
+        """Backward through the ADD loss, the pose head and both RoI pools.
+
+        The data-gradient chain (fc8 dX -> fc7 dX -> fc6 dX -> RoI-pool
+        backward) stays on the step's stream; the weight / bias gradients are
+        leaves of the graph and run on a side stream that joins at the end, so
+        their launches fill the gaps and tails of the chain (HIP-graph branches
+        when captured)."""
         h = self.hough
         nr = h["num_rois"][1:2]
         w, g = self.weights, self.grads
         K6 = 49 * self.Ch
+        main = torch.cuda.current_stream()
+        side = self.side_stream if self.timer is None else None  # per-op timing runs the ops one by one
         with self._t("add_loss_head_bwd"):
             adl.average_distance_loss_grad(self.diff, self.one, num_rois=nr, out=self.dpred)
             ph.head_bwd(self.dpred, self.t8, h["weight"], self.pred, self.dy8, num_rois=nr)
-        with self._t("gemm_fc8_fc7_bwd"):
+        if side is not None:
+            side.wait_stream(main)
+        with torch.cuda.stream(side or main), self._t("gemm_fc8_fc7_dw_bias"):  # fc8 weight / bias gradients
             ph.gemm(self.y7, self.dy8, g["w8"], a_trans=1, K_dev=nr, M=w.units, N=self.D, K=CAP, precision=self.prec)
-            ph.gemm(self.dy8, w.w8, self.dy7, b_trans=1, mask=self.y7, M_dev=nr, precision=self.prec)
-            ph.gemm(self.y6, self.dy7, g["w7"], a_trans=1, K_dev=nr, M=w.units, N=w.units, K=CAP, precision=self.prec)
-            ph.gemm(self.dy7, w.w7, self.dy6, b_trans=1, mask=self.y6, M_dev=nr, precision=self.prec)
-        with self._t("bias_grads"):
             ph.colsum(self.dy8, g["b8"], M_dev=nr)
+        with self._t("gemm_fc8_fc7_dx"):
+            ph.gemm(self.dy8, w.w8, self.dy7, b_trans=1, mask=self.y7, M_dev=nr, precision=self.prec)
+        if side is not None:
+            side.wait_stream(main)
+        with torch.cuda.stream(side or main), self._t("gemm_fc8_fc7_dw_bias"):  # fc7 weight / bias gradients
+            ph.gemm(self.y6, self.dy7, g["w7"], a_trans=1, K_dev=nr, M=w.units, N=w.units, K=CAP, precision=self.prec)
             ph.colsum(self.dy7, g["b7"], M_dev=nr)
-            ph.colsum(self.dy6, g["b6"], M_dev=nr)
+        with self._t("gemm_fc8_fc7_dx"):
+            ph.gemm(self.dy7, w.w7, self.dy6, b_trans=1, mask=self.y6, M_dev=nr, precision=self.prec)
+        if side is not None:
+            side.wait_stream(main)
         x = self.pool.view(CAP, K6)
-        with self._t("gemm_fc6_dw"):  # A = pool5 + pool4
-            ph.gemm(x, self.dy6, g["w6"], a_trans=1, K_dev=nr, M=K6, N=w.units, K=CAP, precision=self.prec)
+        with torch.cuda.stream(side or main):  # fc6 weight / bias gradients (A = pool5 + pool4)
+            with self._t("gemm_fc6_dw"):
+                ph.gemm(x, self.dy6, g["w6"], a_trans=1, K_dev=nr, M=K6, N=w.units, K=CAP, precision=self.prec)
+            with self._t("gemm_fc8_fc7_dw_bias"):
+                ph.colsum(self.dy6, g["b6"], M_dev=nr)
         with self._t("gemm_fc6_dx"):
             ph.gemm(self.dy6, w.w6, self.dx, b_trans=1, M_dev=nr, precision=self.prec)
         dxp = self.dx.view(CAP, 7, 7, self.Ch)
         with self._t("roi_pool_bwd"):  # both pools receive d(pool5 + pool4) = dx
             rp.roi_pool_grad(conv5, h["box"], self.arg5, dxp, 7, 7, 1.0 / 16.0, 0, num_rois=nr, out=self.dconv5)
             rp.roi_pool_grad(conv4, h["box"], self.arg4, dxp, 7, 7, 1.0 / 8.0, 0, num_rois=nr, out=self.dconv4)
+        if side is not None:
+            main.wait_stream(side)
 
     def step(self, inputs):
         self.vote(inputs["label"], inputs["vertex"], inputs["extents"], inputs["meta"], inputs["gt"])
