@@ -13,9 +13,16 @@ namespace pcnn_hough {
 constexpr int kMaxClasses = 256;
 constexpr int kPixPerBlk = 4096;   // label pixels per compaction block
 constexpr int kCompactThreads = 256;
-constexpr int kBand = 8;           // Hough rows per vote workgroup
-constexpr int kVoteThreads = 256;
-constexpr int kPeakThreads = 256;
+#ifndef PCNN_VBAND
+#define PCNN_VBAND 4
+#define PCNN_VTHREADS 512
+#endif
+#ifndef PCNN_PTHREADS
+#define PCNN_PTHREADS 1024
+#endif
+constexpr int kBand = PCNN_VBAND;           // Hough rows per vote workgroup
+constexpr int kVoteThreads = PCNN_VTHREADS;
+constexpr int kPeakThreads = PCNN_PTHREADS;
 constexpr int kPeakChunk = 4096;   // voters per ordered-sum chunk (LDS floats)
 constexpr int kCandCap = 4096;     // NMS candidates per image
 constexpr int kEmitThreads = 256;

@@ -151,7 +151,7 @@ __global__ void __launch_bounds__(kPeakThreads) k_hough_peak(int B, int H, int W
                                                               int32_t* __restrict__ top_domain,
                                                               int32_t* __restrict__ num_rois, int cap) {
   __shared__ __attribute__((aligned(16))) float sh_d[kPeakChunk + 4];
-  __shared__ float sh_red[16];
+  __shared__ float sh_red[2 * (kPeakThreads / 64)];
   __shared__ int s_off[2];
   __shared__ EmitShared esh;
   const int b = blockIdx.y, slot = blockIdx.x;
@@ -225,7 +225,7 @@ __global__ void __launch_bounds__(kPeakThreads) k_hough_cand_data(int H, int W, 
                                                                    const float* __restrict__ meta, int num_meta,
                                                                    HoughWs ws) {
   __shared__ __attribute__((aligned(16))) float sh_d[kPeakChunk + 4];
-  __shared__ float sh_red[16];
+  __shared__ float sh_red[2 * (kPeakThreads / 64)];
   const int b = blockIdx.y;
   const int ncand = min(ws.ncand[b], kCandCap);
   const int HW = H * W;

@@ -103,9 +103,26 @@ __global__ void __launch_bounds__(kVoteThreads) k_hough_vote(int H, int W, int C
   __syncthreads();
 
   const size_t v0 = (size_t)b * ws.vcap + vb;
-  for (int i = ibeg + (int)threadIdx.x; i < iend; i += blockDim.x) {
-    const float4 q = ws.vdat[v0 + i];
-    const int p = ws.vpos[v0 + i];
+  // the next voter's record is loaded while the current one is processed
+  int i = ibeg + (int)threadIdx.x;
+  float4 qn = make_float4(0.f, 0.f, 0.f, 0.f), sn = qn;
+  int pn = 0, cn = 0;
+  if (i < iend) {
+    qn = ws.vdat[v0 + i];
+    pn = ws.vpos[v0 + i];
+    cn = ws.vcode[v0 + i];
+    sn = ws.vcone[v0 + i];
+  }
+  for (; i < iend; i += blockDim.x) {
+    const float4 q = qn, s = sn;
+    const int p = pn, code = cn;
+    if (i + (int)blockDim.x < iend) {
+      const size_t jn = v0 + i + blockDim.x;
+      qn = ws.vdat[jn];
+      pn = ws.vpos[jn];
+      cn = ws.vcode[jn];
+      sn = ws.vcone[jn];
+    }
     const int x = p % W, y = p / W;
     const int k = box_radius(q.w);
     if (k < 0) continue;
@@ -116,13 +133,11 @@ __global__ void __launch_bounds__(kVoteThreads) k_hough_vote(int H, int W, int C
     continue;
 #endif
     const int bx0 = max(x - k, 0), bx1 = min(x + k, W - 1);
-    const int code = ws.vcode[v0 + i];
     const float u = q.x, v = q.y;
     if (code & kSlowVoter) {  // pathological direction / threshold: exact predicate everywhere
       for (int r = ry0; r <= ry1; r++) exact_cells(diff + (r - y0) * Wp, bx0, bx1, r, x, y, u, v, inlier);
       continue;
     }
-    const float4 s = ws.vcone[v0 + i];
     const int co1 = code & 3, co2 = (code >> 2) & 3, ci1 = (code >> 4) & 3, ci2 = (code >> 6) & 3;
     for (int r = ry0; r <= ry1; r++) {
       int* row = diff + (r - y0) * Wp;
