@@ -26,7 +26,13 @@ namespace {
 constexpr int kAddThreads = 256;
 constexpr int kPtsPlain = kAddThreads;         // points per partial slot (plain rows: strided)
 constexpr int kSymLanes = 128;                 // symmetric rows: lanes per candidate group
-constexpr int kPPL = 4;                        // query points per lane (independent min chains)
+#ifndef ADD_GRID
+#define ADD_GRID 512
+#endif
+#ifndef ADD_PPL
+#define ADD_PPL 4
+#endif
+constexpr int kPPL = ADD_PPL;                  // query points per lane (independent min chains)
 constexpr int kPts = kSymLanes * kPPL;         // query points per (row, chunk) item
 constexpr int kMaxPointsLds = 8192;            // float4 candidates in LDS (128 KB)
 
@@ -77,17 +83,27 @@ __global__ void __launch_bounds__(kSymThreads) k_add_rows(const float* __restric
                                                            const int32_t* __restrict__ rcls,
                                                            const int32_t* __restrict__ sym_rows,
                                                            const int32_t* __restrict__ nsym,
+                                                           int32_t* __restrict__ queue,
                                                            float* __restrict__ partial) {
   extern __shared__ __attribute__((aligned(16))) float4 gpts[];  // [P] GT-rotated points
   __shared__ float mdist[kSymGroups - 1][kPts];                   // quarter minima of groups 1..3
   __shared__ int midx[kSymGroups - 1][kPts];
-  __shared__ float red[kSymLanes / 64][5];
+  __shared__ float red[kSymThreads / 64][5];
+  __shared__ int s_imin[kPts];
   const int R = rows_of(num_rois_dev, R_cap);
   const int items = *nsym * nchunk;
   const int grp = threadIdx.x / kSymLanes, lt = threadIdx.x % kSymLanes;
   const int quarter = ((P + kSymGroups - 1) / kSymGroups + 3) / 4 * 4;
   const int c0 = grp * quarter, c1 = min(P, c0 + quarter);
-  for (int item = blockIdx.x; item < items; item += gridDim.x) {
+  // items are handed out by an atomic counter (zeroed by k_add_prep), so a
+  // workgroup that finishes early takes the next (row, chunk)
+  __shared__ int s_item;
+  for (;;) {
+  __syncthreads();
+  if (threadIdx.x == 0) s_item = atomicAdd(queue, 1);
+  __syncthreads();
+  const int item = s_item;
+  if (item >= items) break;
   const int n = sym_rows[item / nchunk], chunk = item % nchunk;
   const int PC = 4 * C;
   const int cls = rcls[n];
@@ -184,7 +200,6 @@ __global__ void __launch_bounds__(kSymThreads) k_add_rows(const float* __restric
   }
   __syncthreads();
   if (grp == 0) {
-    int imin[kPPL];
 #pragma unroll
     for (int k = 0; k < kPPL; k++) {
 #pragma unroll
@@ -192,57 +207,63 @@ __global__ void __launch_bounds__(kSymThreads) k_add_rows(const float* __restric
         const float d = mdist[g][k * kSymLanes + lt];
         if (d < dmin[k]) { dmin[k] = d; iblk[k] = midx[g][k * kSymLanes + lt]; }
       }
-      imin[k] = -1;
+      int im = -1;
       if (iblk[k] >= 0) {
         const int e = min(iblk[k] + 4, P);
         for (int j = iblk[k]; j < e; j++)
-          if (dist_to(k, gpts[j]) == dmin[k]) { imin[k] = j; break; }
+          if (dist_to(k, gpts[j]) == dmin[k]) { im = j; break; }
       }
+      s_imin[k * kSymLanes + lt] = im;
     }
-    float acc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int k = 0; k < kPPL; k++) {
-      if (pq_[k] >= P) continue;
-      const int im = imin[k] < 0 ? pq_[k] : imin[k];  // no finite distance (index_min unset in the reference)
-      const float4 cm = gpts[im];
-      const float x1 = qx[k], y1 = qy[k], z1 = qz[k], x2 = cm.x, y2 = cm.y, z2 = cm.z;
-      const float X0 = Xq[k][0], X1 = Xq[k][1], X2 = Xq[k][2];
-      const int Rn = norm_rows_dev ? *norm_rows_dev : (norm_rows > 0 ? norm_rows : R);
-      const float bn = (float)(Rn * P);
-      const double ln = 2.0 * (double)Rn * (double)P;
-      const float dist = (x1 - x2) * (x1 - x2) + (y1 - y2) * (y1 - y2) + (z1 - z2) * (z1 - z2);
-      if (!(dist < margin)) {  // cu.cc:178-179
-        acc[0] += (float)((double)(dist - margin) / ln);  // cu.cc:181
-        // derivative matrices of Rp w.r.t. (s, u, v, w) (cu.cc:97-139)
-        const float d0[9] = {2 * s, -2 * w, 2 * v, 2 * w, 2 * s, -2 * u, -2 * v, 2 * u, 2 * s};
-        const float d1[9] = {2 * u, 2 * v, 2 * w, 2 * v, -2 * u, -2 * s, 2 * w, 2 * s, -2 * u};
-        const float d2[9] = {-2 * v, 2 * u, 2 * s, 2 * u, 2 * v, 2 * w, -2 * s, 2 * w, -2 * v};
-        const float d3[9] = {-2 * w, -2 * s, 2 * u, 2 * s, -2 * w, 2 * v, 2 * u, 2 * v, 2 * w};
-        const float X[3] = {X0, X1, X2};
-        const float df[3] = {x1 - x2, y1 - y2, z1 - z2};
-        float e0 = 0.f, e1 = 0.f, e2 = 0.f, e3 = 0.f;  // this point's terms, reference order
-#pragma unroll
-        for (int a = 0; a < 3; a++)
-#pragma unroll
-          for (int b = 0; b < 3; b++) {  // cu.cc:183-203, same operation order
-            e0 += df[a] * X[b] * d0[a * 3 + b] / bn;
-            e1 += df[a] * X[b] * d1[a * 3 + b] / bn;
-            e2 += df[a] * X[b] * d2[a * 3 + b] / bn;
-            e3 += df[a] * X[b] * d3[a * 3 + b] / bn;
-          }
-        acc[1] += e0; acc[2] += e1; acc[3] += e2; acc[4] += e3;
-      }
-    }
-#pragma unroll
-    for (int q = 0; q < 5; q++) acc[q] = pcnn::wave_sum(acc[q]);
-    const int wv = threadIdx.x >> 6;
-    if (pcnn::lane_id() == 0)
-      for (int q = 0; q < 5; q++) red[wv][q] = acc[q];
   }
   __syncthreads();
-  if (threadIdx.x < 5) {
+  // per-point loss and gradient terms (cu.cc:174-203), one point per thread
+  // over the whole workgroup
+  float acc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int jj = threadIdx.x; jj < kPts; jj += blockDim.x) {
+    const int p = chunk * kPts + jj;
+    if (p >= P) continue;
+    const int im = s_imin[jj] < 0 ? p : s_imin[jj];  // no finite distance (index_min unset in the reference)
+    const float X0 = pts[p * 3 + 0], X1 = pts[p * 3 + 1], X2 = pts[p * 3 + 2];
+    const float x1 = Rp[0] * X0 + Rp[1] * X1 + Rp[2] * X2;  // = the scan's query point, same expression
+    const float y1 = Rp[3] * X0 + Rp[4] * X1 + Rp[5] * X2;
+    const float z1 = Rp[6] * X0 + Rp[7] * X1 + Rp[8] * X2;
+    const float4 cm = gpts[im];
+    const float x2 = cm.x, y2 = cm.y, z2 = cm.z;
+    const int Rn = norm_rows_dev ? *norm_rows_dev : (norm_rows > 0 ? norm_rows : R);
+    const float bn = (float)(Rn * P);
+    const double ln = 2.0 * (double)Rn * (double)P;
+    const float dist = (x1 - x2) * (x1 - x2) + (y1 - y2) * (y1 - y2) + (z1 - z2) * (z1 - z2);
+    if (!(dist < margin)) {  // cu.cc:178-179
+      acc[0] += (float)((double)(dist - margin) / ln);  // cu.cc:181
+      // derivative matrices of Rp w.r.t. (s, u, v, w) (cu.cc:97-139)
+      const float d0[9] = {2 * s, -2 * w, 2 * v, 2 * w, 2 * s, -2 * u, -2 * v, 2 * u, 2 * s};
+      const float d1[9] = {2 * u, 2 * v, 2 * w, 2 * v, -2 * u, -2 * s, 2 * w, 2 * s, -2 * u};
+      const float d2[9] = {-2 * v, 2 * u, 2 * s, 2 * u, 2 * v, 2 * w, -2 * s, 2 * w, -2 * v};
+      const float d3[9] = {-2 * w, -2 * s, 2 * u, 2 * s, -2 * w, 2 * v, 2 * u, 2 * v, 2 * w};
+      const float X[3] = {X0, X1, X2};
+      const float df[3] = {x1 - x2, y1 - y2, z1 - z2};
+      float e0 = 0.f, e1 = 0.f, e2 = 0.f, e3 = 0.f;  // this point's terms, reference order
+#pragma unroll
+      for (int a = 0; a < 3; a++)
+#pragma unroll
+        for (int b = 0; b < 3; b++) {  // cu.cc:183-203, same operation order
+          e0 += df[a] * X[b] * d0[a * 3 + b] / bn;
+          e1 += df[a] * X[b] * d1[a * 3 + b] / bn;
+          e2 += df[a] * X[b] * d2[a * 3 + b] / bn;
+          e3 += df[a] * X[b] * d3[a * 3 + b] / bn;
+        }
+      acc[1] += e0; acc[2] += e1; acc[3] += e2; acc[4] += e3;
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 5; q++) acc[q] = pcnn::wave_sum(acc[q]);
+  if (pcnn::lane_id() == 0)
+    for (int q = 0; q < 5; q++) red[threadIdx.x >> 6][q] = acc[q];
+  __syncthreads();
+  if (threadIdx.x < 5) {  // fixed order over the waves
     float t = 0.f;
-    for (int i = 0; i < kSymLanes / 64; i++) t += red[i][threadIdx.x];
+    for (int i = 0; i < kSymThreads / 64; i++) t += red[i][threadIdx.x];
     out[threadIdx.x] = t;
   }
   __syncthreads();  // red / gpts / mdist reused by the next item
@@ -254,7 +275,7 @@ __global__ void __launch_bounds__(kSymThreads) k_add_rows(const float* __restric
 __global__ void __launch_bounds__(1024) k_add_prep(const float* __restrict__ weight, const float* __restrict__ symmetry,
                                                     int R_cap, const int32_t* __restrict__ num_rois_dev, int C,
                                                     int32_t* __restrict__ rcls, int32_t* __restrict__ sym_rows,
-                                                    int32_t* __restrict__ nsym) {
+                                                    int32_t* __restrict__ nsym, int32_t* __restrict__ queue) {
   __shared__ int wcount[16];
   __shared__ int base;
   const int R = rows_of(num_rois_dev, R_cap);
@@ -283,7 +304,10 @@ __global__ void __launch_bounds__(1024) k_add_prep(const float* __restrict__ wei
     }
     __syncthreads();
   }
-  if (threadIdx.x == 0) *nsym = base;
+  if (threadIdx.x == 0) {
+    *nsym = base;
+    *queue = 0;
+  }
 }
 
 // Non-symmetric rows (and rows without weight): one workgroup per row, points
@@ -423,7 +447,7 @@ extern "C" size_t pcnn_add_loss_workspace_size(int R_cap, int C, int P) {
   const int nchunk = (P + kPts - 1) / kPts;
   const size_t R = (size_t)(R_cap > 0 ? R_cap : 1);
   return pcnn::align_up(R * nchunk * 5 * sizeof(float), 256) + 2 * pcnn::align_up(R * sizeof(int32_t), 256) +
-         pcnn::align_up(R * sizeof(float), 256) + 2 * 256;
+         pcnn::align_up(R * sizeof(float), 256) + 3 * 256;
 }
 
 extern "C" int pcnn_add_loss_fwd(const float* pred, const float* target, const float* weight, const float* points,
@@ -440,17 +464,18 @@ extern "C" int pcnn_add_loss_fwd(const float* pred, const float* target, const f
   int32_t* rcls = cv.take<int32_t>(R_cap);
   int32_t* sym_rows = cv.take<int32_t>(R_cap);
   int32_t* nsym = cv.take<int32_t>(1);
+  int32_t* queue = cv.take<int32_t>(1);
   float* row_loss = cv.take<float>(R_cap);
   hipLaunchKernelGGL(k_add_prep, dim3(1), dim3(1024), 0, st, weight, symmetry, R_cap, num_rois_dev, C, rcls,
-                     sym_rows, nsym);
+                     sym_rows, nsym, queue);
   hipLaunchKernelGGL(k_add_rows_plain, dim3(R_cap), dim3(kAddThreads), 0, st, pred, target, points, symmetry, R_cap,
                      num_rois_dev, C, P, margin, loss_norm_rows, loss_norm_rows_dev, nchunk, rcls, partial);
   // symmetric rows: persistent grid over (row, chunk) items of the device-side list
   const long sym_items = (long)R_cap * nchunk;
-  const int sym_grid = (int)(sym_items < 512 ? sym_items : 512);
+  const int sym_grid = (int)(sym_items < ADD_GRID ? sym_items : ADD_GRID);
   hipLaunchKernelGGL(k_add_rows, dim3(sym_grid), dim3(kSymThreads), (size_t)P * sizeof(float4), st, pred,
                      target, weight, points, symmetry, R_cap, num_rois_dev, C, P, margin, loss_norm_rows,
-                     loss_norm_rows_dev, nchunk, rcls, sym_rows, nsym, partial);
+                     loss_norm_rows_dev, nchunk, rcls, sym_rows, nsym, queue, partial);
   hipLaunchKernelGGL(k_add_finish_rows, dim3((R_cap + 3) / 4), dim3(256), 0, st, R_cap, num_rois_dev, C, nchunk,
                      rcls, partial, row_loss, bottom_diff);
   hipLaunchKernelGGL(k_add_total, dim3(1), dim3(1024), 0, st, R_cap, num_rois_dev, row_loss, loss);
