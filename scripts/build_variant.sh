@@ -5,8 +5,15 @@
 set -e
 cd "$(dirname "$0")/.."
 name=$1; shift
-mkdir -p scratch
+mkdir -p scratch/$name.obj
 C=posecnn_amd/csrc
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fPIC -shared -Wno-unused-result "$@" \
-  -o scratch/$name.so $C/capi.hip $C/hough_compact.hip $C/hough_vote.hip $C/hough_peak.hip $C/hough_emit.hip \
-  $C/roi_pooling.hip $C/average_distance.hip $C/backprojecting.hip $C/pose_head.hip
+pids=""
+for f in capi hough_compact hough_vote hough_peak hough_emit roi_pooling average_distance backprojecting pose_head; do
+  extra=""; [ $f = pose_head ] && extra="-fno-slp-vectorize"
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fPIC -Wno-unused-result $extra "$@" \
+    -c $C/$f.hip -o scratch/$name.obj/$f.o &
+  pids="$pids $!"
+done
+for p in $pids; do wait $p; done
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o scratch/$name.so scratch/$name.obj/*.o
+rm -rf scratch/$name.obj
