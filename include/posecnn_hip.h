@@ -177,6 +177,24 @@ int pcnn_pose_head_fwd(const float* y8, const float* poses_weight, int R_cap, co
 int pcnn_pose_head_bwd(const float* d_pred, const float* tanh_out, const float* poses_weight, const float* pred,
                        int R_cap, const int32_t* num_rois_dev, int D, float* d_y8, void* stream);
 
+/* ---------------------------------------------------------------------------
+ * Class-aware greedy box NMS + pose combination (inference consumer of the
+ * Hough rows).
+ * Replaces lib/utils/nms.py:3-32 (numpy, on the host after a D2H copy) and the
+ * pose combination of lib/fcn/test.py:197-211.
+ *  rois (R_cap, roi_stride >= 7) [b,cls,x1,y1,x2,y2,score], row count from
+ *  num_rois_dev (may be NULL: R_cap rows), R_cap <= 1152 (MAX_ROI * 9).
+ *  keep (R_cap) int32: kept row indices, score descending (ties: lower row
+ *  first — numpy argsort()[::-1] leaves tie order unspecified); num_keep (1).
+ *  Optional (NULL to skip): rois_out (R_cap,7) = rois[keep]; poses_out (R_cap,7)
+ *  = poses_init[keep] with [:4] = poses_pred[keep, 4*cls : 4*cls+4] for cls >= 0
+ *  (poses_pred rows of pred_dim floats). Overlap test and areas in float32 in
+ *  nms.py's operation order; suppression needs ovr > thresh and equal class.
+ * ------------------------------------------------------------------------- */
+int pcnn_box_nms(const float* rois, int R_cap, int roi_stride, const int32_t* num_rois_dev, float thresh,
+                 int32_t* keep, int32_t* num_keep, const float* poses_init, const float* poses_pred, int pred_dim,
+                 float* rois_out, float* poses_out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -202,3 +202,24 @@ def ransac_hough(label, vertex, extents, meta, is_train=0, num_threads=0):
     n = lib().orc_ransac_hough(lp, vp, ep, mp, meta2.shape[1], B, H, W, C, int(is_train), int(num_threads),
                                rows.ctypes.data_as(F32P), cap)
     return rows[:min(n, cap)]
+
+
+def box_nms(dets, thresh):
+    """lib/utils/nms.py:3-32 (canonical tie order): kept row indices, score descending."""
+    d, dp = _f(dets)
+    keep = np.zeros((max(d.shape[0], 1),), np.int32)
+    n = lib().orc_box_nms(dp, d.shape[0], d.shape[1], ctypes.c_float(thresh), keep.ctypes.data_as(I32P))
+    return keep[:n]
+
+
+def nms_combine(rois, poses_init, poses_pred, keep):
+    """lib/fcn/test.py:199-211: kept rows and combined poses."""
+    r, rp = _f(rois)
+    pi, pip = _f(poses_init)
+    pp, ppp = _f(poses_pred)
+    k, kp = _i(keep)
+    ro = np.zeros((len(k), 7), np.float32)
+    po = np.zeros((len(k), 7), np.float32)
+    lib().orc_nms_combine(rp, r.shape[1], pip, ppp, pp.shape[1], kp, len(k), ro.ctypes.data_as(F32P),
+                          po.ctypes.data_as(F32P))
+    return ro, po
