@@ -207,9 +207,7 @@ def main():
             pmc = json.load(open(pmc_path))
             wl = pmc.get("full" if full else "vote_roi", {})
             if roof is not None and full and args.precision == 1:
-                tmpl = {"gemm_fc6_fwd": "<false, false, false, false>", "gemm_fc6_dw": "<true, false, false, false>",
-                        "gemm_fc6_dx": "<false, true, false, false>"}[dom]
-                ent = wl.get(f"k_gemm_x3{tmpl}:{dom.replace('gemm_', '')}")
+                ent = wl.get(f"k_gemm_x3:{dom.replace('gemm_', '')}")
                 if ent:
                     roof["traffic"] = round(ent["traffic_bytes"])
                     roof["traffic_unit"] = "bytes/launch (rocprofv3 2*FETCH_SIZE + WRITE_SIZE)"

@@ -3,7 +3,7 @@
 # profile.  Every GPU step has its own time limit; steps are chained with &&.
 cd $GRAFT_REPO_ROOT
 R=$GRAFT_REPO_ROOT
-timeout -k 10 600 python -m pytest tests -m gpu -q -p no:cacheprovider > gpurun_out/t_gpu.log 2>&1 &&
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/t_gpu.log 2>&1 &&
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 &&
 cd /tmp && export TMPDIR=/tmp &&
 timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $R/gpurun_out/pmc_fetch -o run -- python3 $R/bench.py --steps 4 --warmup 2 --no-cpu-baseline --no-graph > $R/gpurun_out/pmc_fetch.log 2>&1 &&

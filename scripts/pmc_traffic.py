@@ -3,11 +3,8 @@
 
 FETCH_SIZE / WRITE_SIZE are in KiB per dispatch.  On gfx950 FETCH_SIZE
 counts half the bytes of wide coalesced reads (MI355X_MICROARCH.md, HBM
-section), so reads are doubled.  GEMM dispatches of one template are told
-apart by their fixed order inside a pose step (pipeline.py):
-  k_gemm_x3<false, false, ...>: fc6_fwd, fc7_fwd, fc8_fwd
-  k_gemm_x3<true, false, ...>:  fc8_dw, fc7_dw, fc6_dw
-  k_gemm_x3<false, true, ...>:  fc8_dx, fc7_dx, fc6_dx
+section), so reads are doubled.  GEMM dispatches are told apart by their
+fixed enqueue order inside a pose step (STEP_ORDER, pipeline.py).
 """
 import csv
 import json
@@ -16,9 +13,18 @@ import re
 import sys
 from collections import defaultdict
 
-ROLES = {"k_gemm_x3<false, false, false, false>": ["fc6_fwd", "fc7_fwd", "fc8_fwd"],
-         "k_gemm_x3<true, false, false, false>": ["fc8_dw", "fc7_dw", "fc6_dw"],
-         "k_gemm_x3<false, true, false, false>": ["fc8_dx", "fc7_dx", "fc6_dx"]}
+# k_gemm_x3 dispatches of one pose step in enqueue order (pipeline.py), over
+# every tile / layout instantiation
+STEP_ORDER = ["fc6_fwd", "fc7_fwd", "fc8_fwd", "fc8_dw", "fc8_dx", "fc7_dw", "fc7_dx", "fc6_dw", "fc6_dx"]
+
+
+def gemm_roles(per):
+    """{role: [values]} from {kernel: [(dispatch_id, value)]}; roles by position in the step order."""
+    seq = sorted(x for k, v in per.items() if k.startswith("k_gemm_x3") for x in v)
+    out = defaultdict(list)
+    for i, (_, val) in enumerate(seq):
+        out[STEP_ORDER[i % len(STEP_ORDER)]].append(val)
+    return out
 HOUGH = ("k_label_hist", "k_label_scan", "k_label_scatter", "k_voter_setup", "k_hough_vote", "k_hough_peak",
          "k_hough_emit", "k_hough_nms_cand", "k_hough_cand_data", "k_hough_nms_select")
 
@@ -42,17 +48,14 @@ def load(path, counter):
 def summarize(fetch_csv, write_csv):
     f, w = load(fetch_csv, "FETCH_SIZE"), load(write_csv, "WRITE_SIZE")
     out = {}
+    fr_all, wr_all = gemm_roles(f), gemm_roles(w)
+    for role, fr in fr_all.items():
+        wr = wr_all.get(role, [])
+        out[f"k_gemm_x3:{role}"] = {"read_bytes": 2 * sum(fr) / len(fr), "write_bytes": sum(wr) / max(len(wr), 1),
+                                    "dispatches": len(fr)}
     for k in f:
         fv = [v for _, v in f[k]]
         wv = [v for _, v in w.get(k, [])]
-        roles = ROLES.get(k)
-        if roles:
-            for i, role in enumerate(roles):
-                fr, wr = fv[i::len(roles)], wv[i::len(roles)]
-                if fr:
-                    out[f"{k}:{role}"] = {"read_bytes": 2 * sum(fr) / len(fr),
-                                          "write_bytes": sum(wr) / max(len(wr), 1),
-                                          "dispatches": len(fr)}
         out[k] = {"read_bytes": 2 * sum(fv) / len(fv), "write_bytes": sum(wv) / max(len(wv), 1),
                   "dispatches": len(fv)}
     for v in out.values():

@@ -7,16 +7,15 @@ import sys
 from collections import defaultdict
 
 sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.abspath(__file__)))
-from pmc_traffic import ROLES  # noqa: E402
+from pmc_traffic import STEP_ORDER, gemm_roles  # noqa: E402
 
 per = defaultdict(list)
 for row in csv.DictReader(open(sys.argv[1])):
     m = re.search(r"(k_\w+(?:<[^>]*>)?)", row["Kernel_Name"])
     if m:
         per[m.group(1)].append((int(row["Dispatch_Id"]), (int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) / 1e3))
-for k, roles in ROLES.items():
-    d = [v for _, v in sorted(per.get(k, []))]
-    for i, role in enumerate(roles):
-        x = d[i::len(roles)]
-        if x:
-            print(f"{k}:{role:8s} n={len(x):4d} avg={sum(x) / len(x):8.1f} us")
+roles = gemm_roles(per)
+for role in STEP_ORDER:
+    x = roles.get(role, [])
+    if x:
+        print(f"k_gemm_x3:{role:8s} n={len(x):4d} avg={sum(x) / len(x):8.1f} us")
