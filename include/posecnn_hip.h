@@ -63,6 +63,20 @@ int pcnn_hough_voting(const int32_t* label, const float* vertex, const float* ex
                       float* top_weight, int32_t* top_domain, int32_t* num_rois, int cap, int32_t* debug_counts,
                       void* workspace, size_t workspace_bytes, void* stream);
 
+/* pcnn_hough_voting with the label producer fused in:
+ * instead of label_2d the op takes prob_normalized (B,H,W,C) fp32 — the
+ * softmax whose argmax is label_2d (argmax_2d, lib/networks/network.py:433-434;
+ * graph vgg16_convs.py:144-146 -> :167-170) — labels every pixel inside the
+ * compaction pass (first maximum; a NaN wins at its first occurrence, as
+ * numpy / tf.argmax) and writes label_out (B,H,W) int32 as a by-product.
+ * Outputs are those of pcnn_hough_voting on label_out; same workspace size. */
+int pcnn_hough_voting_prob(const float* prob, int32_t* label_out, const float* vertex, const float* extents,
+                           const float* meta, int num_meta, const float* gt, int num_gt, int B, int H, int W, int C,
+                           int batch_base, int global_batch, int is_train, float inlier_thr, int label_thr,
+                           float vote_thr, float per_thr, int skip_pixels, float* top_box, float* top_pose,
+                           float* top_target, float* top_weight, int32_t* top_domain, int32_t* num_rois, int cap,
+                           int32_t* debug_counts, void* workspace, size_t workspace_bytes, void* stream);
+
 /* HoughvotinggpuGrad (hough_voting_gpu_op.cc:440-484; set_gradients cu.cc:608-612):
  * zero gradients for label (B,H,W) and vertex (B,H,W,3C). Either may be NULL. */
 int pcnn_hough_voting_grad(float* grad_label, float* grad_vertex, int B, int H, int W, int C, void* stream);
@@ -194,6 +208,23 @@ int pcnn_pose_head_bwd(const float* d_pred, const float* tanh_out, const float* 
 int pcnn_box_nms(const float* rois, int R_cap, int roi_stride, const int32_t* num_rois_dev, float thresh,
                  int32_t* keep, int32_t* num_keep, const float* poses_init, const float* poses_pred, int pred_dim,
                  float* rois_out, float* poses_out, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Label producers.
+ * argmax_2d: label (B,H,W) int32 = argmax over the last axis of prob (B,H,W,C)
+ *   (lib/networks/network.py:433-434 `tf.to_int32(tf.argmax(input, 3))`);
+ *   first maximum, a NaN wins at its first occurrence (numpy / tf.argmax).
+ * Hardlabel: replaces HardlabelForwardLaucher / HardlabelBackwardLaucher
+ *   (lib/hard_label_layer/hard_label_op_gpu.cu.cc:17-29,32-52,56-90; op
+ *   hard_label_op.cc:30-44). top (B,H,W,C) = one-hot of gt where gt != -1 and
+ *   (gt > 0 or prob[gt] < threshold), else 0; threshold > 0 (the op's attr
+ *   check). gt outside [-1, C) (out-of-row store in the reference) -> zero row.
+ *   Backward: zero gradients for prob (B,H,W,C) and gt (B,H,W) (either NULL).
+ * ------------------------------------------------------------------------- */
+int pcnn_argmax_2d(const float* prob, int B, int H, int W, int C, int32_t* label, void* stream);
+int pcnn_hard_label_fwd(const float* prob, const int32_t* gt, int B, int H, int W, int C, float threshold,
+                        float* top, void* stream);
+int pcnn_hard_label_bwd(float* grad_prob, float* grad_gt, int B, int H, int W, int C, void* stream);
 
 #ifdef __cplusplus
 }

@@ -223,3 +223,29 @@ def nms_combine(rois, poses_init, poses_pred, keep):
     lib().orc_nms_combine(rp, r.shape[1], pip, ppp, pp.shape[1], kp, len(k), ro.ctypes.data_as(F32P),
                           po.ctypes.data_as(F32P))
     return ro, po
+
+
+def argmax_2d(prob):
+    """lib/networks/network.py:433-434 `tf.to_int32(tf.argmax(input, 3))`:
+    numpy argmax over the class axis (first maximum; first NaN wins)."""
+    return np.argmax(np.asarray(prob, np.float32), axis=3).astype(np.int32)
+
+
+def hard_label(prob, gt, threshold):
+    """Hardlabel forward, restated from the CPU op (hard_label_op.cc:94-106) and
+    HardlabelForward (hard_label_op_gpu.cu.cc:17-29): per pixel a zero row, then
+    1 at gt if gt != -1 and (gt > 0 or prob[gt] < threshold).  gt outside
+    [-1, C) stores past the pixel row in the reference (undefined): zero row."""
+    prob = np.asarray(prob, np.float32)
+    gt = np.asarray(gt, np.int32)
+    B, H, W, C = prob.shape
+    top = np.zeros((B, H, W, C), np.float32)
+    for b in range(B):
+        for y in range(H):
+            for x in range(W):
+                g = int(gt[b, y, x])
+                if g == -1 or g < -1 or g >= C:
+                    continue
+                if g > 0 or prob[b, y, x, g] < np.float32(threshold):
+                    top[b, y, x, g] = 1.0
+    return top

@@ -11,7 +11,10 @@
 namespace pcnn_hough {
 
 constexpr int kMaxClasses = 256;
-constexpr int kPixPerBlk = 4096;   // label pixels per compaction block
+#ifndef PCNN_PIXBLK
+#define PCNN_PIXBLK 2048
+#endif
+constexpr int kPixPerBlk = PCNN_PIXBLK;   // label pixels per compaction block
 constexpr int kCompactThreads = 256;
 #ifndef PCNN_VBAND
 #define PCNN_VBAND 4
@@ -325,8 +328,56 @@ __device__ __forceinline__ void for_each_label_group(int lab, bool valid, F fn) 
 }
 
 // ---------------------------------------------------------------------------
+// Label producer: label_2d = argmax over the class axis
+// of prob_normalized (B,H,W,C) fp32 (`argmax_2d`, lib/networks/network.py:
+// 433-434, fed from vgg16_convs.py:144-146).  tf.argmax = numpy argmax: the
+// first maximum wins; a NaN wins at its first occurrence.
+constexpr int kArgmaxStagedMaxC = 96;  // classes staged through LDS per wave (64 px * C * 4 B)
+
+__device__ __forceinline__ int argmax_classes(const float* v, int C) {
+  float bv = v[0];
+  if (bv != bv) return 0;
+  int best = 0;
+  for (int c = 1; c < C; c++) {
+    const float x = v[c];
+    if (x != x) return c;
+    if (x > bv) { bv = x; best = c; }
+  }
+  return best;
+}
+
+// argmax of pixel p0 + lane of the wave's 64-pixel group [p0, p0 + 64) of one
+// image's prob rows (img = prob + b*HW*C).  C <= kArgmaxStagedMaxC: the
+// group's 64*C contiguous floats are read coalesced (float4 when the group is
+// whole) into the wave's LDS slice `stage` and each lane scans its own row
+// there; larger C reads the row from global memory directly.  Returns -1 for
+// lanes past HW.  Every thread of the workgroup calls it together (it
+// synchronises the workgroup around the staging).
+__device__ __forceinline__ int wave_argmax_rows(const float* __restrict__ img, int p0, int HW, int C,
+                                                float* stage) {
+  const int lane = pcnn::lane_id();
+  const int p = p0 + lane;
+  if (C > kArgmaxStagedMaxC) return p < HW ? argmax_classes(img + (size_t)p * C, C) : -1;  // uniform branch
+  const int npx = HW - p0 < 64 ? (HW - p0 > 0 ? HW - p0 : 0) : 64;
+  const int n = npx * C;
+  const float* src = img + (size_t)p0 * C;
+  if (npx == 64 && ((((uintptr_t)src) & 15) == 0)) {
+    const float4* s4 = (const float4*)src;
+    for (int i = lane; i < n / 4; i += 64) ((float4*)stage)[i] = s4[i];
+  } else {
+    for (int i = lane; i < n; i += 64) stage[i] = src[i];
+  }
+  __syncthreads();
+  const int l = p < HW ? argmax_classes(stage + lane * C, C) : -1;
+  __syncthreads();  // the slice is reused by the wave's next group
+  return l;
+}
+
+// ---------------------------------------------------------------------------
 // kernels (defined in the TUs listed above)
 __global__ void k_label_hist(const int32_t* __restrict__ label, int HW, int C, HoughWs ws);
+__global__ void k_label_hist_prob(const float* __restrict__ prob, int32_t* __restrict__ label_out, int HW, int C,
+                                  HoughWs ws);
 __global__ void k_label_scan(int C, int label_thr, int index_size, int nms, int skip, HoughWs ws);
 __global__ void k_label_scatter(const int32_t* __restrict__ label, const float* __restrict__ vertex,
                                 const float* __restrict__ extents, const float* __restrict__ meta, int num_meta,

@@ -35,6 +35,36 @@ __global__ void __launch_bounds__(kCompactThreads) k_label_hist(const int32_t* _
   for (int i = threadIdx.x; i < C; i += blockDim.x) ws.blk[((size_t)b * ws.nblk + blk) * C + i] = h[i];
 }
 
+// k_label_hist with the label producer fused in: the
+// block's pixels are labelled by argmax over prob_normalized (argmax_2d,
+// network.py:433-434) as they are counted, and label_2d is written once for
+// k_label_scatter (and the caller).  One pass over the (B,H,W,C) prob map
+// replaces the argmax pass + label write + label re-read of the unfused graph.
+// Dynamic LDS: kCompactThreads/64 waves x 64 px x C floats when C is staged.
+__global__ void __launch_bounds__(kCompactThreads) k_label_hist_prob(const float* __restrict__ prob,
+                                                                      int32_t* __restrict__ label_out, int HW,
+                                                                      int C, HoughWs ws) {
+  extern __shared__ __attribute__((aligned(16))) float stage_all[];
+  __shared__ int h[kMaxClasses];
+  const int b = blockIdx.y, blk = blockIdx.x;
+  for (int i = threadIdx.x; i < C; i += blockDim.x) h[i] = 0;
+  const float* img = prob + (size_t)b * HW * C;
+  float* stage = stage_all + (threadIdx.x >> 6) * 64 * (C <= kArgmaxStagedMaxC ? C : 0);
+  const int base = blk * kPixPerBlk;
+  for (int r = 0; r < kPixPerBlk / kCompactThreads; r++) {
+    const int p0 = base + r * kCompactThreads + (threadIdx.x & ~63);
+    const int p = p0 + pcnn::lane_id();
+    const int l = wave_argmax_rows(img, p0, HW, C, stage);  // syncs the workgroup (h[] init included)
+    if (p < HW) label_out[(size_t)b * HW + p] = l;
+    const bool valid = p < HW && l > 0;
+    for_each_label_group(l, valid, [&](int l0, uint64_t m) {
+      if (pcnn::lane_id() == __ffsll((long long)m) - 1) atomicAdd(&h[l0], __popcll(m));
+    });
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < C; i += blockDim.x) ws.blk[((size_t)b * ws.nblk + blk) * C + i] = h[i];
+}
+
 constexpr int kScanLds = 16384;
 
 // Exclusive scan of the block histograms per class, present-class selection

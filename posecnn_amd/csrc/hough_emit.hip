@@ -68,17 +68,19 @@ extern "C" size_t pcnn_hough_voting_workspace_size(int B, int H, int W, int C, i
   return bytes + 256;
 }
 
-extern "C" int pcnn_hough_voting(const int32_t* label, const float* vertex, const float* extents, const float* meta,
-                                 int num_meta, const float* gt, int num_gt, int B, int H, int W, int C,
-                                 int batch_base, int global_batch, int is_train, float inlier_thr, int label_thr,
-                                 float vote_thr, float per_thr, int skip_pixels, float* top_box, float* top_pose,
-                                 float* top_target, float* top_weight, int32_t* top_domain, int32_t* num_rois,
-                                 int cap, int32_t* debug_counts, void* workspace, size_t workspace_bytes,
-                                 void* stream) {
+// label given (pcnn_hough_voting) or produced from prob_normalized by the
+// fused argmax (pcnn_hough_voting_prob: label = label_out, written here).
+static int hough_voting_impl(const int32_t* label, const float* prob, int32_t* label_out, const float* vertex,
+                             const float* extents, const float* meta, int num_meta, const float* gt, int num_gt,
+                             int B, int H, int W, int C, int batch_base, int global_batch, int is_train,
+                             float inlier_thr, int label_thr, float vote_thr, float per_thr, int skip_pixels,
+                             float* top_box, float* top_pose, float* top_target, float* top_weight,
+                             int32_t* top_domain, int32_t* num_rois, int cap, int32_t* debug_counts,
+                             void* workspace, size_t workspace_bytes, void* stream) {
   PCNN_REQUIRE(B > 0 && H > 0 && W > 0 && C >= 2 && C <= kMaxClasses && skip_pixels > 0 && num_meta >= 6);
   PCNN_REQUIRE((long)H * W * (C - 1) < (1l << 31) && W < (1 << 16));
-  PCNN_REQUIRE(label && vertex && extents && meta && top_box && top_pose && top_target && top_weight &&
-               top_domain && num_rois && workspace && cap > 0);
+  PCNN_REQUIRE((label || (prob && label_out && (long)H * W * C < (1l << 31))) && vertex && extents && meta &&
+               top_box && top_pose && top_target && top_weight && top_domain && num_rois && workspace && cap > 0);
   PCNN_REQUIRE(num_gt == 0 || gt);
   if (global_batch <= 0) global_batch = B;
   PCNN_REQUIRE(global_batch >= B);
@@ -92,7 +94,14 @@ extern "C" int pcnn_hough_voting(const int32_t* label, const float* vertex, cons
   const int HW = H * W;
 
   if (hipMemsetAsync(ws.diag, 0, 4 * sizeof(int32_t), st) != hipSuccess) return PCNN_EHIP;
-  hipLaunchKernelGGL(k_label_hist, dim3(ws.nblk, B), dim3(kCompactThreads), 0, st, label, HW, C, ws);
+  if (label) {
+    hipLaunchKernelGGL(k_label_hist, dim3(ws.nblk, B), dim3(kCompactThreads), 0, st, label, HW, C, ws);
+  } else {
+    const size_t lds = C <= kArgmaxStagedMaxC ? (size_t)kCompactThreads * C * sizeof(float) : 0;
+    hipLaunchKernelGGL(k_label_hist_prob, dim3(ws.nblk, B), dim3(kCompactThreads), lds, st, prob, label_out, HW, C,
+                       ws);
+    label = label_out;
+  }
   hipLaunchKernelGGL(k_label_scan, dim3(B), dim3(1024), 0, st, C, label_thr, index_size, nms ? 1 : 0, skip_pixels,
                      ws);
   hipLaunchKernelGGL(k_label_scatter, dim3(ws.nblk, B), dim3(kCompactThreads), 0, st, label, vertex, extents, meta,
@@ -137,6 +146,35 @@ extern "C" int pcnn_hough_voting(const int32_t* label, const float* vertex, cons
                        top_weight, top_domain, num_rois, cap);
   PCNN_CHECK_LAUNCH();
   return PCNN_OK;
+}
+
+extern "C" int pcnn_hough_voting(const int32_t* label, const float* vertex, const float* extents, const float* meta,
+                                 int num_meta, const float* gt, int num_gt, int B, int H, int W, int C,
+                                 int batch_base, int global_batch, int is_train, float inlier_thr, int label_thr,
+                                 float vote_thr, float per_thr, int skip_pixels, float* top_box, float* top_pose,
+                                 float* top_target, float* top_weight, int32_t* top_domain, int32_t* num_rois,
+                                 int cap, int32_t* debug_counts, void* workspace, size_t workspace_bytes,
+                                 void* stream) {
+  if (!label) return PCNN_EINVAL;
+  return hough_voting_impl(label, nullptr, nullptr, vertex, extents, meta, num_meta, gt, num_gt, B, H, W, C,
+                           batch_base, global_batch, is_train, inlier_thr, label_thr, vote_thr, per_thr, skip_pixels,
+                           top_box, top_pose, top_target, top_weight, top_domain, num_rois, cap, debug_counts,
+                           workspace, workspace_bytes, stream);
+}
+
+extern "C" int pcnn_hough_voting_prob(const float* prob, int32_t* label_out, const float* vertex,
+                                      const float* extents, const float* meta, int num_meta, const float* gt,
+                                      int num_gt, int B, int H, int W, int C, int batch_base, int global_batch,
+                                      int is_train, float inlier_thr, int label_thr, float vote_thr, float per_thr,
+                                      int skip_pixels, float* top_box, float* top_pose, float* top_target,
+                                      float* top_weight, int32_t* top_domain, int32_t* num_rois, int cap,
+                                      int32_t* debug_counts, void* workspace, size_t workspace_bytes,
+                                      void* stream) {
+  if (!prob || !label_out) return PCNN_EINVAL;
+  return hough_voting_impl(nullptr, prob, label_out, vertex, extents, meta, num_meta, gt, num_gt, B, H, W, C,
+                           batch_base, global_batch, is_train, inlier_thr, label_thr, vote_thr, per_thr, skip_pixels,
+                           top_box, top_pose, top_target, top_weight, top_domain, num_rois, cap, debug_counts,
+                           workspace, workspace_bytes, stream);
 }
 
 extern "C" int pcnn_hough_voting_grad(float* grad_label, float* grad_vertex, int B, int H, int W, int C,

@@ -28,19 +28,33 @@ def _as_meta2d(meta, B):
 
 def hough_voting_gpu_capacity(label, vertex, extents, meta_data, gt, is_train, threshold_vote,
                               threshold_percentage, skip_pixels, inlier_threshold=0.9, label_threshold=500,
-                              batch_base=0, global_batch=None, out=None, debug_counts=None, stream=None):
+                              batch_base=0, global_batch=None, out=None, debug_counts=None, stream=None, prob=None):
     """Launch without host sync.  Returns dict of capacity-sized tensors and
-    `num_rois` (int32[2] on device: rows, max(rows, 1))."""
-    _lib.require_gpu(label, vertex, extents, meta_data, gt)
+    `num_rois` (int32[2] on device: rows, max(rows, 1)).
+
+    With `prob` (B,H,W,C) given instead of `label` (pass label=None), the
+    label producer runs fused into the op (pcnn_hough_voting_prob): label_2d =
+    argmax over the class axis (network.py:433-434) is computed inside the
+    compaction pass and returned as out["label"]."""
+    _lib.require_gpu(label, prob, vertex, extents, meta_data, gt)
     lib = _lib.load()
-    if label.dim() != 3:
+    if (label is None) == (prob is None):
+        raise ValueError("pass exactly one of label / prob")
+    if label is not None and label.dim() != 3:
         raise ValueError("label must be 3-dimensional")  # hough_voting_gpu_op.cc:328-329
+    if prob is not None and prob.dim() != 4:
+        raise ValueError("prob must be 4-dimensional")
     if vertex.dim() != 4:
         raise ValueError("vertex must be 4-dimensional")  # :331-332
-    B, H, W = label.shape
+    B, H, W = (label.shape if label is not None else prob.shape[:3])
     C = vertex.shape[3] // 3
-    dev = label.device
-    label = label.contiguous().to(torch.int32)
+    if prob is not None and prob.shape[3] != C:
+        raise ValueError(f"prob has {prob.shape[3]} classes, vertex has {C}")
+    dev = vertex.device
+    if label is not None:
+        label = label.contiguous().to(torch.int32)
+    else:
+        prob = prob.contiguous().float()
     vertex = vertex.contiguous().float()
     extents = extents.contiguous().float()
     meta = _as_meta2d(meta_data.float(), B)
@@ -54,10 +68,14 @@ def hough_voting_gpu_capacity(label, vertex, extents, meta_data, gt, is_train, t
             domain=torch.empty((CAPACITY,), dtype=torch.int32, device=dev),
             num_rois=torch.empty((2,), dtype=torch.int32, device=dev),
         )
+    if prob is not None and out.get("label") is None:
+        out["label"] = torch.empty((B, H, W), dtype=torch.int32, device=dev)
     nbytes = lib.pcnn_hough_voting_workspace_size(B, H, W, C, int(skip_pixels), float(threshold_vote))
     ws = _lib.workspace(nbytes, dev, "hough")
-    rc = lib.pcnn_hough_voting(
-        _lib.ptr(label), _lib.ptr(vertex), _lib.ptr(extents), _lib.ptr(meta), meta.shape[1],
+    head = ((lib.pcnn_hough_voting, _lib.ptr(label)) if prob is None else
+            (lib.pcnn_hough_voting_prob, _lib.ptr(prob), _lib.ptr(out["label"])))
+    rc = head[0](
+        *head[1:], _lib.ptr(vertex), _lib.ptr(extents), _lib.ptr(meta), meta.shape[1],
         _lib.ptr(gt) if gt.numel() else None, gt.shape[0], B, H, W, C, int(batch_base),
         int(global_batch or B), int(is_train), float(inlier_threshold), int(label_threshold),
         float(threshold_vote), float(threshold_percentage), int(skip_pixels),
@@ -92,6 +110,21 @@ def hough_voting_gpu(bottom_label, bottom_vertex, bottom_extents, bottom_meta_da
     n = int(o["num_rois"][1].item())
     return (o["box"][:n].clone(), o["pose"][:n].clone(), o["target"][:n].clone(), o["weight"][:n].clone(),
             o["domain"][:n].clone())
+
+
+def hough_voting_gpu_from_prob(bottom_prob, bottom_vertex, bottom_extents, bottom_meta_data, bottom_gt, is_train,
+                               threshold_vote, threshold_percentage, skip_pixels, name=None, inlier_threshold=0.9,
+                               label_threshold=500, batch_base=0, global_batch=None):
+    """argmax_2d(prob) -> hough_voting_gpu fused (vgg16_convs.py:144-146 feeding
+    :167-170): returns (label_2d, top_box, top_pose, top_target, top_weight,
+    top_domain), the outputs equal to argmax_2d + hough_voting_gpu."""
+    o = hough_voting_gpu_capacity(None, bottom_vertex, bottom_extents, bottom_meta_data, bottom_gt, is_train,
+                                  threshold_vote, threshold_percentage, skip_pixels,
+                                  inlier_threshold=inlier_threshold, label_threshold=label_threshold,
+                                  batch_base=batch_base, global_batch=global_batch, prob=bottom_prob)
+    n = int(o["num_rois"][1].item())
+    return (o["label"], o["box"][:n].clone(), o["pose"][:n].clone(), o["target"][:n].clone(),
+            o["weight"][:n].clone(), o["domain"][:n].clone())
 
 
 def hough_voting_gpu_grad(bottom_label, bottom_vertex, grad, name=None):

@@ -8,7 +8,7 @@ name=$1; shift
 mkdir -p scratch/$name.obj
 C=posecnn_amd/csrc
 pids=""
-for f in capi hough_compact hough_vote hough_peak hough_emit roi_pooling average_distance backprojecting pose_head box_nms; do
+for f in capi hough_compact hough_vote hough_peak hough_emit roi_pooling average_distance backprojecting pose_head box_nms label_producer; do
   extra=""; [ $f = pose_head ] && extra="-fno-slp-vectorize"
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fPIC -Wno-unused-result $extra "$@" \
     -c $C/$f.hip -o scratch/$name.obj/$f.o &

@@ -38,7 +38,8 @@ def test_header_declares_the_reference_surface():
     # one entry per reference op launcher + the FC contraction
     for n in ("pcnn_hough_voting", "pcnn_hough_voting_grad", "pcnn_roi_pool_fwd", "pcnn_roi_pool_bwd",
               "pcnn_add_loss_fwd", "pcnn_add_loss_bwd", "pcnn_backproject_fwd", "pcnn_backproject_bwd",
-              "pcnn_gemm", "pcnn_abi_version", "pcnn_strerror"):
+              "pcnn_gemm", "pcnn_abi_version", "pcnn_strerror", "pcnn_box_nms", "pcnn_argmax_2d",
+              "pcnn_hard_label_fwd", "pcnn_hard_label_bwd", "pcnn_hough_voting_prob"):
         assert n in names
 
 
