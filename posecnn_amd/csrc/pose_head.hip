@@ -26,6 +26,7 @@ constexpr int kMaxSplit = 8;   // fp32 kernel
 constexpr int kMaxSplitX = 16; // split-bf16 kernel (small-tile shapes such as fc8)
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 struct GemmArgs {
   int M, N, K;
@@ -348,105 +349,117 @@ __device__ __forceinline__ xf4 x_ld4(const XOp& o, unsigned voff, int soff) {
 // the K edge (KC) or the row edge (NC) -> element-wise fallback; the common
 // instantiation has no divergent branch, so a K step is one basic block.
 template <int T, bool KC, bool RAGGED, bool A2>
-__device__ __forceinline__ void x_load(const XOp& P, const XOp& P2, int r0, int rlim, int k0, int ke,
-                                       float (&v)[16]) {
+__device__ __forceinline__ void x_load_part(const XOp& P, const XOp& P2, int r0, int rlim, int k0, int ke,
+                                            float (&v)[16], int q) {
   // Every mask is applied to the load ADDRESS (out-of-range voffset -> the
   // hardware returns 0), never to the loaded data: nothing consumes a loaded
   // register before the staging store of the next step, so all loads of a
   // step stay in flight together.  (A2: the summed operand of the generic
-  // A + A2 form adds right after its loads.)
+  // A + A2 form adds right after its loads.)  Part q = one float4 load.
   const int t = threadIdx.x;
+#ifdef PCNN_ABL_L2
+  k0 &= 127;  // timing ablation: operands stay L2-resident (wrong results)
+#endif
+  xf4 x;
   if (KC) {
     const int kq = t & 7;
-    const int row0 = r0 + (t >> 3);
+    const int row = r0 + (t >> 3) + (T / 4) * q;
     const int kl = k0 + 4 * kq;
+    const bool ok = row < rlim && kl < ke;
+    const unsigned vo = ok ? (unsigned)(row * P.ld + kl) * 4u : kXOob;
+    if (!RAGGED || kl + 4 <= ke || !ok) {
+      x = x_ld4(P, vo, 0);
+      if (A2) x += x_ld4(P2, vo, 0);
+    } else {
 #pragma unroll
-    for (int i = 0; i < 4; i++) {
-      const int row = row0 + (T / 4) * i;
-      const bool ok = row < rlim && kl < ke;
-      const unsigned vo = ok ? (unsigned)(row * P.ld + kl) * 4u : kXOob;
-      xf4 x;
-      if (!RAGGED || kl + 4 <= ke || !ok) {
-        x = x_ld4(P, vo, 0);
-        if (A2) x += x_ld4(P2, vo, 0);
-      } else {
-#pragma unroll
-        for (int e = 0; e < 4; e++) {
-          const unsigned ve = kl + e < ke ? vo + 4u * e : kXOob;
-          x[e] = x_ld1(P, ve, 0);
-          if (A2) x[e] += x_ld1(P2, ve, 0);
-        }
+      for (int e = 0; e < 4; e++) {
+        const unsigned ve = kl + e < ke ? vo + 4u * e : kXOob;
+        x[e] = x_ld1(P, ve, 0);
+        if (A2) x[e] += x_ld1(P2, ve, 0);
       }
-      v[4 * i + 0] = x[0]; v[4 * i + 1] = x[1]; v[4 * i + 2] = x[2]; v[4 * i + 3] = x[3];
     }
   } else {
     const int w = t >> 6, l = t & 63;
     const int rq = r0 + 64 * (w >> 1) + 4 * (l >> 2);
-    const int kg = k0 + 16 * (w & 1) + 4 * (l & 3);
+    const int k = k0 + 16 * (w & 1) + 4 * (l & 3) + q;
+    const bool ok = rq < rlim && k < ke;
+    const unsigned vo = ok ? (unsigned)(k * P.ld + rq) * 4u : kXOob;
+    if (!RAGGED || rq + 4 <= rlim || !ok) {
+      x = x_ld4(P, vo, 0);
+      if (A2) x += x_ld4(P2, vo, 0);
+    } else {
 #pragma unroll
-    for (int j = 0; j < 4; j++) {
-      const int k = kg + j;
-      const bool ok = rq < rlim && k < ke;
-      const unsigned vo = ok ? (unsigned)(k * P.ld + rq) * 4u : kXOob;
-      xf4 x;
-      if (!RAGGED || rq + 4 <= rlim || !ok) {
-        x = x_ld4(P, vo, 0);
-        if (A2) x += x_ld4(P2, vo, 0);
-      } else {
-#pragma unroll
-        for (int e = 0; e < 4; e++) {
-          const unsigned ve = rq + e < rlim ? vo + 4u * e : kXOob;
-          x[e] = x_ld1(P, ve, 0);
-          if (A2) x[e] += x_ld1(P2, ve, 0);
-        }
+      for (int e = 0; e < 4; e++) {
+        const unsigned ve = rq + e < rlim ? vo + 4u * e : kXOob;
+        x[e] = x_ld1(P, ve, 0);
+        if (A2) x[e] += x_ld1(P2, ve, 0);
       }
-      v[4 * j + 0] = x[0]; v[4 * j + 1] = x[1]; v[4 * j + 2] = x[2]; v[4 * j + 3] = x[3];
     }
   }
+  v[4 * q + 0] = x[0]; v[4 * q + 1] = x[1]; v[4 * q + 2] = x[2]; v[4 * q + 3] = x[3];
+}
+
+template <int T, bool KC, bool RAGGED, bool A2>
+__device__ __forceinline__ void x_load(const XOp& P, const XOp& P2, int r0, int rlim, int k0, int ke,
+                                       float (&v)[16]) {
+#pragma unroll
+  for (int q = 0; q < 4; q++) x_load_part<T, KC, RAGGED, A2>(P, P2, r0, rlim, k0, ke, v, q);
+}
+
+// Part q of the split-and-store of a staged operand: KC rows (t >> 3) + T/4 q
+// (register quad q); NC row rb + q, i.e. element q of every register quad —
+// so an NC part needs all four loads of the operand, a KC part only its own.
+template <int T, bool KC>
+__device__ __forceinline__ void x_store_part(const float (&v)[16], char* hi, char* lo, int q) {
+  const int t = threadIdx.x;
+  bf16x4 h, l4;
+  int o;
+  if (KC) {
+    const int kq = t & 7;
+    const int row = (t >> 3) + (T / 4) * q;
+#pragma unroll
+    for (int e = 0; e < 4; e++) {
+      const __bf16 b = (__bf16)v[4 * q + e];
+      h[e] = b;
+      l4[e] = (__bf16)(v[4 * q + e] - (float)b);
+    }
+    o = x_off(row, kq >> 1) + (kq & 1) * 8;
+  } else {  // v[4 j + e] = (k = k-quad base + j, row = row-quad base + e): transpose into k-contiguous rows
+    const int w = t >> 6, l = t & 63;
+    const int row = 64 * (w >> 1) + 4 * (l >> 2) + q;
+    const int kq = 4 * (w & 1) + (l & 3);  // k quad index 0..7 within the 32-k step
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const __bf16 b = (__bf16)v[4 * j + q];
+      h[j] = b;
+      l4[j] = (__bf16)(v[4 * j + q] - (float)b);
+    }
+    o = x_off(row, kq >> 1) + (kq & 1) * 8;
+  }
+  *(bf16x4*)(hi + o) = h;
+  *(bf16x4*)(lo + o) = l4;
 }
 
 template <int T, bool KC>
 __device__ __forceinline__ void x_store(const float (&v)[16], char* hi, char* lo) {
-  const int t = threadIdx.x;
-  if (KC) {
-    const int kq = t & 7;
 #pragma unroll
-    for (int i = 0; i < 4; i++) {
-      const int row = (t >> 3) + (T / 4) * i;
-      bf16x4 h, l;
-#pragma unroll
-      for (int e = 0; e < 4; e++) {
-        const __bf16 b = (__bf16)v[4 * i + e];
-        h[e] = b;
-        l[e] = (__bf16)(v[4 * i + e] - (float)b);
-      }
-      const int o = x_off(row, kq >> 1) + (kq & 1) * 8;
-      *(bf16x4*)(hi + o) = h;
-      *(bf16x4*)(lo + o) = l;
-    }
-  } else {  // v[4 j + e] = (k = k-quad base + j, row = row-quad base + e): transpose into k-contiguous rows
-    const int w = t >> 6, l = t & 63;
-    const int rb = 64 * (w >> 1) + 4 * (l >> 2);
-    const int kq = 4 * (w & 1) + (l & 3);  // k quad index 0..7 within the 32-k step
-#pragma unroll
-    for (int e = 0; e < 4; e++) {
-      const int row = rb + e;
-      bf16x4 h, lo4;
-#pragma unroll
-      for (int j = 0; j < 4; j++) {
-        const __bf16 b = (__bf16)v[4 * j + e];
-        h[j] = b;
-        lo4[j] = (__bf16)(v[4 * j + e] - (float)b);
-      }
-      const int o = x_off(row, kq >> 1) + (kq & 1) * 8;
-      *(bf16x4*)(hi + o) = h;
-      *(bf16x4*)(lo + o) = lo4;
-    }
-  }
+  for (int q = 0; q < 4; q++) x_store_part<T, KC>(v, hi, lo, q);
 }
 
 #ifndef PCNN_APF
 #define PCNN_APF 1
+#endif
+// PCNN_MFMA16: v_mfma_f32_16x16x32_bf16 instead of 32x32x16 (same cycles per
+// flop; the chip may hold a different clock on it, MI355X_MICROARCH.md DVFS
+// give-back item 7).  PCNN_PRIO: s_setprio(1) around each MFMA cluster.
+#ifndef PCNN_MFMA16
+#define PCNN_MFMA16 0
+#endif
+#ifndef PCNN_PRIO
+#define PCNN_PRIO 0
+#endif
+#if PCNN_MFMA16 && defined(PCNN_FUSED_STAGE) && !PCNN_FUSED_STAGE
+#error "PCNN_MFMA16 needs the fused staging loop"
 #endif
 template <int T, bool A_T, bool B_T, bool RAGGED, bool A2>
 __global__ void __launch_bounds__(XTile<T>::threads, T == 256 ? 1 : 2) k_gemm_x3(GemmArgs g) {
@@ -484,6 +497,16 @@ __global__ void __launch_bounds__(XTile<T>::threads, T == 256 ? 1 : 2) k_gemm_x3
 #pragma unroll
     for (int j = 0; j < 2; j++) b_off[ks][j] = x_off(wn * 64 + j * 32 + r, 2 * ks + hsel);
   }
+#if PCNN_MFMA16
+  // v_mfma_f32_16x16x32_bf16: lane -> row lane & 15 of a 16-row block, k chunk
+  // lane >> 4 (8 bf16 each: the whole 32-k step in one MFMA)
+  constexpr int AM16 = 2 * AM;  // 16-row accumulator blocks per wave along M
+  int a16[AM16], b16[4];
+#pragma unroll
+  for (int i = 0; i < AM16; i++) a16[i] = x_off(wm * (T / 2) + i * 16 + (lane & 15), lane >> 4);
+#pragma unroll
+  for (int j = 0; j < 4; j++) b16[j] = x_off(wn * 64 + j * 16 + (lane & 15), lane >> 4);
+#endif
   for (int item = wg; item < items; item += G) {
     const int tile = item % (mt * nt), z = item / (mt * nt);
     const int mi = m_fast ? tile % mt : tile / nt;
@@ -491,11 +514,19 @@ __global__ void __launch_bounds__(XTile<T>::threads, T == 256 ? 1 : 2) k_gemm_x3
     const int m0 = mi * T, n0 = ni * T;
     const int kb = z * kchunk, ke = min(Keff, kb + kchunk);
     const int nsteps = kb < ke ? (ke - kb + XBK - 1) / XBK : 0;
+#if PCNN_MFMA16
+    f32x4 acc[AM16][4];
+#pragma unroll
+    for (int i = 0; i < AM16; i++)
+#pragma unroll
+      for (int j = 0; j < 4; j++) acc[i][j] = (f32x4){};
+#else
     f32x16 acc[AM][2];
 #pragma unroll
     for (int i = 0; i < AM; i++)
 #pragma unroll
       for (int j = 0; j < 2; j++) acc[i][j] = (f32x16){};
+#endif
     if (nsteps > 0) {
       float va[16], vb[16];
       // prologue: stage 0 -> LDS buffer 0, stage 1 -> registers
@@ -515,6 +546,7 @@ __global__ void __launch_bounds__(XTile<T>::threads, T == 256 ? 1 : 2) k_gemm_x3
 #endif
       // PCNN_STAGGER: the SIMD partners (waves w, w + 4) run a step in
       // opposite order (MFMAs then staging / staging then MFMAs).
+#if !PCNN_MFMA16
       const bool late = PCNN_STAGGER && (threadIdx.x >> 6) >= 4;
       auto compute = [&](const char* cur) {
 #pragma unroll
@@ -566,6 +598,113 @@ __global__ void __launch_bounds__(XTile<T>::threads, T == 256 ? 1 : 2) k_gemm_x3
         x_load<T, A_KC, RAGGED, A2>(oa, oa2, m0, Meff, kb + s2 * XBK, ke, va);
         x_load<T, B_KC, RAGGED, false>(ob, onull, n0, g.N, kb + s2 * XBK, ke, vb);
       };
+#endif  // !PCNN_MFMA16
+#ifndef PCNN_FUSED_STAGE
+#define PCNN_FUSED_STAGE 1
+#endif
+#if PCNN_FUSED_STAGE
+      // Staging spread through the MFMA stream: after each accumulator row
+      // (six MFMAs) one part of step s+1's split-and-store and the matching
+      // loads of step s+2, so the conversion VALU and LDS writes fill MFMA
+      // gaps instead of running as a separate phase after them (both waves of
+      // a SIMD reach that phase together).  The `nxt` buffer was last read in
+      // step s-1, before the barrier, so it may be written at any point here.
+      auto stage_part = [&](int c, char* nxt, int kn) {
+        if (c < 4) {
+          x_store_part<T, A_KC>(va, nxt, nxt + kXPart, c);
+          if (A_KC) {
+            x_load_part<T, true, RAGGED, A2>(oa, oa2, m0, Meff, kn, ke, va, c);
+          } else if (c == 3) {
+#pragma unroll
+            for (int q = 0; q < 4; q++) x_load_part<T, false, RAGGED, A2>(oa, oa2, m0, Meff, kn, ke, va, q);
+          }
+        } else {
+          x_store_part<T, B_KC>(vb, nxt + 2 * kXPart, nxt + 3 * kXPart, c - 4);
+          if (B_KC) {
+            x_load_part<T, true, RAGGED, false>(ob, onull, n0, g.N, kn, ke, vb, c - 4);
+          } else if (c == 7) {
+#pragma unroll
+            for (int q = 0; q < 4; q++) x_load_part<T, false, RAGGED, false>(ob, onull, n0, g.N, kn, ke, vb, q);
+          }
+        }
+      };
+      constexpr int kCPG = 8 / (2 * AM);  // staging parts per accumulator row
+      for (int s = 0; s < nsteps; s++) {
+        const char* cur = xl + (s & 1) * kXStage;
+        char* nxt = xl + ((s + 1) & 1) * kXStage;
+        const int kn = kb + (s + 2 < nsteps ? s + 2 : nsteps - 1) * XBK;
+#if PCNN_MFMA16
+        {
+          constexpr int kCPG16 = 8 / AM16;  // staging parts per 16-row block
+          bf16x8 bh[4], bl[4];
+#pragma unroll
+          for (int j = 0; j < 4; j++) {
+            bh[j] = *(const bf16x8*)(cur + 2 * kXPart + b16[j]);
+            bl[j] = *(const bf16x8*)(cur + 3 * kXPart + b16[j]);
+          }
+          bf16x8 ah[2], al[2];
+          ah[0] = *(const bf16x8*)(cur + a16[0]);
+          al[0] = *(const bf16x8*)(cur + kXPart + a16[0]);
+#pragma unroll
+          for (int i = 0; i < AM16; i++) {
+            if (i + 1 < AM16) {
+              ah[(i + 1) & 1] = *(const bf16x8*)(cur + a16[i + 1]);
+              al[(i + 1) & 1] = *(const bf16x8*)(cur + kXPart + a16[i + 1]);
+            }
+#if PCNN_PRIO
+            __builtin_amdgcn_s_setprio(1);
+#endif
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[i & 1], bh[j], acc[i][j], 0, 0, 0);
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i & 1], bl[j], acc[i][j], 0, 0, 0);
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i & 1], bh[j], acc[i][j], 0, 0, 0);
+            }
+#if PCNN_PRIO
+            __builtin_amdgcn_s_setprio(0);
+#endif
+#ifndef PCNN_ABL_NOSTAGE
+#pragma unroll
+            for (int q = 0; q < kCPG16; q++) stage_part(i * kCPG16 + q, nxt, kn);
+#endif
+          }
+        }
+#else
+#pragma unroll
+        for (int ks = 0; ks < 2; ks++) {
+          bf16x8 bh[2], bl[2];
+#pragma unroll
+          for (int j = 0; j < 2; j++) {
+            bh[j] = *(const bf16x8*)(cur + 2 * kXPart + b_off[ks][j]);
+            bl[j] = *(const bf16x8*)(cur + 3 * kXPart + b_off[ks][j]);
+          }
+          bf16x8 ah[2], al[2];
+          ah[0] = *(const bf16x8*)(cur + a_off[ks][0]);
+          al[0] = *(const bf16x8*)(cur + kXPart + a_off[ks][0]);
+#pragma unroll
+          for (int i = 0; i < AM; i++) {
+            if (i + 1 < AM) {
+              ah[(i + 1) & 1] = *(const bf16x8*)(cur + a_off[ks][i + 1]);
+              al[(i + 1) & 1] = *(const bf16x8*)(cur + kXPart + a_off[ks][i + 1]);
+            }
+#pragma unroll
+            for (int j = 0; j < 2; j++) {
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i & 1], bh[j], acc[i][j], 0, 0, 0);
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i & 1], bl[j], acc[i][j], 0, 0, 0);
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i & 1], bh[j], acc[i][j], 0, 0, 0);
+            }
+#ifndef PCNN_ABL_NOSTAGE
+#pragma unroll
+            for (int q = 0; q < kCPG; q++) stage_part((ks * AM + i) * kCPG + q, nxt, kn);
+#endif
+          }
+        }
+#endif  // PCNN_MFMA16
+#ifndef PCNN_ABL_NOBAR
+        __syncthreads();
+#endif
+      }
+#else
       for (int s = 0; s < nsteps; s++) {
         const char* cur = xl + (s & 1) * kXStage;
         char* nxt = xl + ((s + 1) & 1) * kXStage;
@@ -578,6 +717,7 @@ __global__ void __launch_bounds__(XTile<T>::threads, T == 256 ? 1 : 2) k_gemm_x3
         }
         __syncthreads();
       }
+#endif
     }
     // epilogue, branch-free: bias / mask come in through buffer loads and
     // results leave through buffer stores, out-of-range lanes masked by an
@@ -589,28 +729,39 @@ __global__ void __launch_bounds__(XTile<T>::threads, T == 256 ? 1 : 2) k_gemm_x3
     // Masked epilogue (S == 1): the 16 mask values of group (j, i) are issued
     // one group ahead of their use, so the tile pays one mask latency, not 8.
     const bool msk = S == 1 && g.mask;
-    float mv[2][16];
-    auto load_mask = [&](int gi, float (&d)[16]) {
-      const int n = n0 + wn * 64 + (gi / AM) * 32 + r;
+    // accumulator blocks: EJ (N) x EI (M) blocks of EB x EB, EQ values per lane;
+    // e_col / e_row: output coordinates of a lane's value q of block (i, j)
+#if PCNN_MFMA16
+    constexpr int EJ = 4, EI = AM16, EQ = 4, EB = 16;
+    auto e_col = [&](int j) { return n0 + wn * 64 + j * EB + (lane & 15); };
+    auto e_row = [&](int i, int q) { return m0 + wm * (T / 2) + i * EB + 4 * (lane >> 4) + q; };
+#else
+    constexpr int EJ = 2, EI = AM, EQ = 16, EB = 32;
+    auto e_col = [&](int j) { return n0 + wn * 64 + j * EB + r; };
+    auto e_row = [&](int i, int q) { return m0 + wm * (T / 2) + i * EB + (q & 3) + 8 * (q >> 2) + 4 * hsel; };
+#endif
+    float mv[2][EQ];
+    auto load_mask = [&](int gi, float (&d)[EQ]) {
+      const int n = e_col(gi / EI);
 #pragma unroll
-      for (int q = 0; q < 16; q++) {
-        const int m = m0 + wm * (T / 2) + (gi % AM) * 32 + (q & 3) + 8 * (q >> 2) + 4 * hsel;
+      for (int q = 0; q < EQ; q++) {
+        const int m = e_row(gi % EI, q);
         d[q] = x_ld1(omask, (n < g.N && m < Meff) ? (unsigned)(m * g.ldm + n) * 4u : kXOob, 0);
       }
     };
     if (msk) load_mask(0, mv[0]);
 #pragma unroll
-    for (int j = 0; j < 2; j++) {
-      const int n = n0 + wn * 64 + j * 32 + r;
+    for (int j = 0; j < EJ; j++) {
+      const int n = e_col(j);
       const bool nok = n < g.N;
       const float bv = (S == 1 && g.bias) ? x_ld1(obias, nok ? (unsigned)n * 4u : kXOob, 0) : 0.f;
 #pragma unroll
-      for (int i = 0; i < AM; i++) {
-        const int gi = AM * j + i;
-        if (msk && gi + 1 < 2 * AM) load_mask(gi + 1, mv[(gi + 1) & 1]);
+      for (int i = 0; i < EI; i++) {
+        const int gi = EI * j + i;
+        if (msk && gi + 1 < EJ * EI) load_mask(gi + 1, mv[(gi + 1) & 1]);
 #pragma unroll
-        for (int q = 0; q < 16; q++) {
-          const int m = m0 + wm * (T / 2) + i * 32 + (q & 3) + 8 * (q >> 2) + 4 * hsel;
+        for (int q = 0; q < EQ; q++) {
+          const int m = e_row(i, q);
           const bool ok = nok && m < Meff;
           float v = acc[i][j][q];
           if (S == 1) {

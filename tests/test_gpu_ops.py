@@ -164,6 +164,34 @@ def test_add_loss_symmetric_ties(hip, orc):
     np.testing.assert_allclose(diff.cpu().numpy(), od, rtol=1e-4, atol=1e-6 * np.abs(od).max())
 
 
+@pytest.mark.parametrize("P,near", [(4096, True), (4096, False), (2620, True), (4200, False), (700, True)])
+def test_add_loss_symmetric_large(hip, orc, P, near):
+    """ADD-S at up to 4200 model points: predictions near the target and
+    arbitrary ones, duplicated model points and lattice coordinates (exact
+    distance ties), against the oracle's sequential first-minimum scan."""
+    rng = np.random.default_rng(P + int(near))
+    C, R = 3, 7
+    pts = rng.normal(size=(C, P, 3)).astype(np.float32)
+    pts[1, P // 2:P // 2 + 40] = pts[1, 10:50]          # duplicate points -> tied candidates
+    pts[2] = np.round(pts[2] * 4) / 4                    # lattice-like coordinates -> equal x values
+    sym = np.array([0, 1, 1], np.float32)
+    pred = np.zeros((R, 4 * C), np.float32)
+    target = np.zeros((R, 4 * C), np.float32)
+    weight = np.zeros((R, 4 * C), np.float32)
+    for r in range(R):
+        c = 1 + r % 2
+        q = rng.normal(size=4)
+        q /= np.linalg.norm(q)
+        dq = q + (rng.normal(size=4) * 0.02 if near else rng.normal(size=4))
+        target[r, 4 * c:4 * c + 4] = q
+        pred[r, 4 * c:4 * c + 4] = dq / np.linalg.norm(dq)
+        weight[r, 4 * c:4 * c + 4] = 1
+    loss, diff = adl.average_distance_loss(T(pred), T(target), T(weight), T(pts), T(sym), 0.01)
+    ol, od, _ = orc.average_distance_loss(pred, target, weight, pts, sym, 0.01)
+    np.testing.assert_allclose(loss.cpu().numpy(), ol, rtol=1e-5)
+    np.testing.assert_allclose(diff.cpu().numpy(), od, rtol=1e-4, atol=1e-6 * np.abs(od).max())
+
+
 def test_backproject(hip, orc):
     rng = np.random.default_rng(4)
     B, H, W, Ch, NC, G = 2, 48, 64, 16, 5, 12
