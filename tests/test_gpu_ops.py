@@ -212,6 +212,31 @@ def test_backproject(hip, orc):
     np.testing.assert_array_equal(gd.cpu().numpy(), orc.backproject_bwd(g, depth, meta, H, W, G))
 
 
+def test_backproject_linemod_config(hip, orc):
+    """configs[4] sizes for one image: 640x480 LINEMOD frame (15 objects' extents,
+    4 objects, rendered depth), G = 64, Ch = 64, NC = 16, kernel_size 1,
+    threshold 0.02, forward and backward bit-exact."""
+    rng = np.random.default_rng(45)
+    mdl = synth.models()
+    G, Ch, NC = 64, 64, 16
+    voxel = ([2.0 / G, 1.5 / G, 1.7 / G], [-1.0, -0.75, 0.4])
+    fr = synth.make_frames(1, 480, 640, num_classes=16, objects_per_image=4, seed=5,
+                           extents=mdl["linemod_extents"], with_depth=True, voxel=voxel)
+    depth = fr["depth"]
+    data = rng.normal(size=(1, 480, 640, Ch)).astype(np.float32)
+    label = rng.uniform(size=(1, 480, 640, NC)).astype(np.float32)
+    l3 = rng.uniform(size=(1, G, G, G, NC)).astype(np.float32)
+    td, tl, tf = bp.backproject(T(data), T(label), T(depth), T(fr["meta"]), T(l3), G, 1, 0.02)
+    od, ol, of = orc.backproject_fwd(data, label, depth, fr["meta"], l3, G, 1, 0.02)
+    np.testing.assert_array_equal(td.cpu().numpy(), od)
+    np.testing.assert_array_equal(tl.cpu().numpy(), ol)
+    np.testing.assert_array_equal(tf.cpu().numpy(), of)
+    assert of.any() and not of.all()
+    g = rng.normal(size=od.shape).astype(np.float32)
+    gd = bp.backproject_grad(T(data), T(depth), T(fr["meta"]), T(g), G, 1, 0.02)
+    np.testing.assert_array_equal(gd.cpu().numpy(), orc.backproject_bwd(g, depth, fr["meta"], 480, 640, G))
+
+
 # Tolerances: precision 0 is fp32 MFMA (fp32 products, fp32 accumulation);
 # precision 1 is the split-bf16 x3 MFMA (hi*hi + hi*lo + lo*hi, fp32
 # accumulation): per-product relative error <= ~2^-16, so the error of a
