@@ -119,6 +119,8 @@ __global__ void __launch_bounds__(1024) k_label_scan(int C, int label_thr, int i
   }
   __syncthreads();
   if (threadIdx.x == 0) {
+    if (b == 0)
+      for (int i = 0; i < 4; i++) ws.diag[i] = 0;  // self-check counters of this call (pcnn_hough_voting_diag)
     int count = 0;
     for (int c = 1; c < C; c++)
       if (tot[c] > label_thr) ws.slot_cls[(size_t)b * C + count++] = c;

@@ -93,7 +93,6 @@ static int hough_voting_impl(const int32_t* label, const float* prob, int32_t* l
   const int index_size = PCNN_MAX_ROI / global_batch;  // cu.cc:734
   const int HW = H * W;
 
-  if (hipMemsetAsync(ws.diag, 0, 4 * sizeof(int32_t), st) != hipSuccess) return PCNN_EHIP;
   if (label) {
     hipLaunchKernelGGL(k_label_hist, dim3(ws.nblk, B), dim3(kCompactThreads), 0, st, label, HW, C, ws);
   } else {

@@ -788,6 +788,27 @@ __global__ void __launch_bounds__(256) k_gemm_reduce(GemmArgs g) {
   const int Keff = eff_dim(g.K, g.K_dev);
   const int S = g.prec ? split_x3(Meff, g.N, Keff, g.tile) : split_for(Meff, g.N, Keff);
   if (S == 1) return;
+  // slab sums in slice order z = 0, 1, ... (0 + s0 == s0, so starting from
+  // s0 is the same fp32 sum); float4 along N when rows stay 16-B aligned
+  const size_t slab_stride = (size_t)g.M * g.N;
+  const bool vec = (long)g.M * g.N < (1l << 31) && (g.N & 3) == 0 && (g.ldc & 3) == 0 && (!g.mask || (g.ldm & 3) == 0) &&
+                   ((((uintptr_t)g.slab) | ((uintptr_t)g.C) | ((uintptr_t)g.mask) | ((uintptr_t)g.bias)) & 15) == 0;
+  if (vec) {
+    const int n4 = g.N >> 2;
+    const int total4 = Meff * n4;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total4; i += gridDim.x * blockDim.x) {
+      const int m = i / n4, n = (i - m * n4) << 2;
+      const float4* sp = (const float4*)(g.slab + (size_t)m * g.N + n);
+      float4 v = sp[0];
+      for (int z = 1; z < S; z++) {
+        const float4 t = sp[z * (slab_stride >> 2)];
+        v.x += t.x; v.y += t.y; v.z += t.z; v.w += t.w;
+      }
+      *(float4*)(g.C + (size_t)m * g.ldc + n) = make_float4(epilogue(v.x, g, m, n), epilogue(v.y, g, m, n + 1),
+                                                            epilogue(v.z, g, m, n + 2), epilogue(v.w, g, m, n + 3));
+    }
+    return;
+  }
   const long total = (long)Meff * g.N;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
     const int m = (int)(i / g.N), n = (int)(i % g.N);

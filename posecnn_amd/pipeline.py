@@ -108,8 +108,8 @@ class PoseStep:
         single-device order, posecnn_amd/exchange.py); global loss normaliser
         = max(sum of per-rank rows, 1)."""
         h = self.hough
-        if self.xchg is None:
-            self.norm_rows.copy_(h["num_rois"][1:2])
+        if self.xchg is None:  # single device: the loss normaliser is the op's own row count
+            self.norm_rows = h["num_rois"][1:2]
             return
         with self._t("allgather_rois"):
             _, total = self.xchg(h["box"], h["pose"], h["num_rois"])
