@@ -25,12 +25,15 @@ namespace {
 
 constexpr int kAddThreads = 256;
 constexpr int kPtsPlain = kAddThreads;         // points per partial slot (plain rows: strided)
-constexpr int kSymLanes = 128;                 // symmetric rows: lanes per candidate group
+#ifndef ADD_LANES
+#define ADD_LANES 64
+#endif
+constexpr int kSymLanes = ADD_LANES;           // symmetric rows: lanes per candidate group
 #ifndef ADD_GRID
-#define ADD_GRID 512
+#define ADD_GRID 768
 #endif
 #ifndef ADD_PPL
-#define ADD_PPL 4
+#define ADD_PPL 2
 #endif
 constexpr int kPPL = ADD_PPL;                  // query points per lane (independent min chains)
 constexpr int kPts = kSymLanes * kPPL;         // query points per (row, chunk) item
@@ -62,14 +65,17 @@ __device__ __forceinline__ int row_class(const float* __restrict__ weight, int n
   return -1;
 }
 
-// Symmetric rows: a 1024-thread workgroup owns (row, chunk of kPts query
-// points); its eight 128-lane groups scan disjoint eighths of the candidate
+// Symmetric rows: a 512-thread workgroup owns (row, chunk of kPts = 128 query
+// points); its eight one-wave groups scan disjoint eighths of the candidate
 // list for the same query points (the first-minimum update is a dependent
-// chain, so latency, not issue, bounds a lone wave: 16 waves per item and
-// kPPL chains per lane), then merge in LDS in group order with a strict < —
+// chain, so latency, not issue, bounds a lone wave: 8 waves per item, kPPL = 2
+// chains per lane, three items per CU), then merge in LDS in group order with a strict < —
 // a later range wins only with a strictly smaller distance, which is exactly
 // the reference's sequential first minimum (cu.cc:150-172).
-constexpr int kSymGroups = 8;
+#ifndef ADD_GROUPS
+#define ADD_GROUPS 8
+#endif
+constexpr int kSymGroups = ADD_GROUPS;
 constexpr int kSymThreads = kSymLanes * kSymGroups;
 
 __global__ void __launch_bounds__(kSymThreads) k_add_rows(const float* __restrict__ pred,
@@ -86,7 +92,7 @@ __global__ void __launch_bounds__(kSymThreads) k_add_rows(const float* __restric
                                                            int32_t* __restrict__ queue,
                                                            float* __restrict__ partial) {
   extern __shared__ __attribute__((aligned(16))) float4 gpts[];  // [P] GT-rotated points
-  __shared__ float mdist[kSymGroups - 1][kPts];                   // quarter minima of groups 1..3
+  __shared__ float mdist[kSymGroups - 1][kPts];                   // range minima of groups 1..kSymGroups-1
   __shared__ int midx[kSymGroups - 1][kPts];
   __shared__ float red[kSymThreads / 64][5];
   __shared__ int s_imin[kPts];
