@@ -992,7 +992,21 @@ extern "C" int pcnn_gemm(int M, int N, int K, const float* A, const float* A2, i
     else if (a_trans && !b_trans) hipLaunchKernelGGL((k_gemm_f32<true, false>), dim3(grid), dim3(kGemmThreads), 0, st, g);
     else hipLaunchKernelGGL((k_gemm_f32<true, true>), dim3(grid), dim3(kGemmThreads), 0, st, g);
   }
-  hipLaunchKernelGGL(k_gemm_reduce, dim3(1024), dim3(256), 0, st, g);
+  // split-K slab reduction, unless no device-side M can make the shape split
+  // (a static M whose tile count already fills the grid: split 1 for every K).
+  // A no-op launch is not free: queued behind a persistent GEMM on another
+  // stream it holds back everything after it on its own stream.
+  bool may_split = true;
+  if (!M_dev) {
+    if (precision == 1) {
+      const int T = g.tile;
+      const int tiles = ((M + T - 1) / T) * ((N + T - 1) / T);
+      may_split = tiles < (T == 256 ? XTile<256>::grid : XTile<128>::grid) / 2;
+    } else {
+      may_split = ((M + BM - 1) / BM) * ((N + BN - 1) / BN) < 256;
+    }
+  }
+  if (may_split) hipLaunchKernelGGL(k_gemm_reduce, dim3(1024), dim3(256), 0, st, g);
   PCNN_CHECK_LAUNCH();
   return PCNN_OK;
 }
