@@ -23,8 +23,6 @@
 
 namespace {
 
-constexpr int kAddThreads = 256;
-constexpr int kPtsPlain = kAddThreads;         // points per partial slot (plain rows: strided)
 #ifndef ADD_LANES
 #define ADD_LANES 64
 #endif
@@ -65,6 +63,74 @@ __device__ __forceinline__ int row_class(const float* __restrict__ weight, int n
   return -1;
 }
 
+// Non-symmetric rows (and rows without weight): one workgroup per row, points
+// strided over the threads; the per-point arithmetic is k_add_rows' (cu.cc:140-203).
+// Run as the tail items of k_add_rows' queue, after the symmetric items, so
+// they fill the workgroups that finish the O(P^2) items early.
+__device__ __forceinline__ void add_plain_row(int n, const float* __restrict__ pred, const float* __restrict__ target,
+                                              const float* __restrict__ points, const float* __restrict__ symmetry,
+                                              int R, int C, int P, float margin, int norm_rows,
+                                              const int32_t* __restrict__ norm_rows_dev, int nchunk,
+                                              const int32_t* __restrict__ rcls, float* __restrict__ partial,
+                                              float (*red)[5]) {
+  const int cls = rcls[n];
+  if (cls >= 0 && symmetry[cls] > 0) return;  // the symmetric items own this row
+  float* out = partial + (size_t)n * nchunk * 5;
+  for (int i = threadIdx.x; i < nchunk * 5; i += blockDim.x) out[i] = 0.f;
+  if (cls < 0) return;
+  const int PC = 4 * C;
+  const float* tq = target + (size_t)n * PC + 4 * cls;
+  const float* pq = pred + (size_t)n * PC + 4 * cls;
+  float Rg[9], Rp[9];
+  quat2rot(tq[0], tq[1], tq[2], tq[3], Rg);
+  const float s = pq[0], u = pq[1], v = pq[2], w = pq[3];
+  quat2rot(s, u, v, w, Rp);
+  const float d0[9] = {2 * s, -2 * w, 2 * v, 2 * w, 2 * s, -2 * u, -2 * v, 2 * u, 2 * s};
+  const float d1[9] = {2 * u, 2 * v, 2 * w, 2 * v, -2 * u, -2 * s, 2 * w, 2 * s, -2 * u};
+  const float d2[9] = {-2 * v, 2 * u, 2 * s, 2 * u, 2 * v, 2 * w, -2 * s, 2 * w, -2 * v};
+  const float d3[9] = {-2 * w, -2 * s, 2 * u, 2 * s, -2 * w, 2 * v, 2 * u, 2 * v, 2 * w};
+  const int Rn = norm_rows_dev ? *norm_rows_dev : (norm_rows > 0 ? norm_rows : R);
+  const float bn = (float)(Rn * P);
+  const double ln = 2.0 * (double)Rn * (double)P;
+  const float* pts = points + (size_t)cls * P * 3;
+  float acc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int p = threadIdx.x; p < P; p += blockDim.x) {
+    const float X0 = pts[p * 3 + 0], X1 = pts[p * 3 + 1], X2 = pts[p * 3 + 2];
+    const float x1 = Rp[0] * X0 + Rp[1] * X1 + Rp[2] * X2;
+    const float y1 = Rp[3] * X0 + Rp[4] * X1 + Rp[5] * X2;
+    const float z1 = Rp[6] * X0 + Rp[7] * X1 + Rp[8] * X2;
+    const float x2 = Rg[0] * X0 + Rg[1] * X1 + Rg[2] * X2;
+    const float y2 = Rg[3] * X0 + Rg[4] * X1 + Rg[5] * X2;
+    const float z2 = Rg[6] * X0 + Rg[7] * X1 + Rg[8] * X2;
+    const float dist = (x1 - x2) * (x1 - x2) + (y1 - y2) * (y1 - y2) + (z1 - z2) * (z1 - z2);
+    if (dist < margin) continue;
+    acc[0] += (float)((double)(dist - margin) / ln);
+    const float X[3] = {X0, X1, X2};
+    const float df[3] = {x1 - x2, y1 - y2, z1 - z2};
+    float e0 = 0.f, e1 = 0.f, e2 = 0.f, e3 = 0.f;  // this point's terms, reference order
+#pragma unroll
+    for (int j = 0; j < 3; j++)
+#pragma unroll
+      for (int k = 0; k < 3; k++) {
+        e0 += df[j] * X[k] * d0[j * 3 + k] / bn;
+        e1 += df[j] * X[k] * d1[j * 3 + k] / bn;
+        e2 += df[j] * X[k] * d2[j * 3 + k] / bn;
+        e3 += df[j] * X[k] * d3[j * 3 + k] / bn;
+      }
+    acc[1] += e0; acc[2] += e1; acc[3] += e2; acc[4] += e3;
+  }
+#pragma unroll
+  for (int q = 0; q < 5; q++) acc[q] = pcnn::wave_sum(acc[q]);
+  if (pcnn::lane_id() == 0)
+    for (int q = 0; q < 5; q++) red[threadIdx.x >> 6][q] = acc[q];
+  __syncthreads();
+  if (threadIdx.x < 5) {
+    float t = 0.f;
+    for (int i = 0; i < (int)(blockDim.x >> 6); i++) t += red[i][threadIdx.x];
+    out[threadIdx.x] = t;
+  }
+}
+
 // Symmetric rows: a 512-thread workgroup owns (row, chunk of kPts = 128 query
 // points); its eight one-wave groups scan disjoint eighths of the candidate
 // list for the same query points (the first-minimum update is a dependent
@@ -97,7 +163,8 @@ __global__ void __launch_bounds__(kSymThreads) k_add_rows(const float* __restric
   __shared__ float red[kSymThreads / 64][5];
   __shared__ int s_imin[kPts];
   const int R = rows_of(num_rois_dev, R_cap);
-  const int items = *nsym * nchunk;
+  const int sym_items = *nsym * nchunk;
+  const int items = sym_items + R;  // then one plain item per row (add_plain_row)
   const int grp = threadIdx.x / kSymLanes, lt = threadIdx.x % kSymLanes;
   const int quarter = ((P + kSymGroups - 1) / kSymGroups + 3) / 4 * 4;
   const int c0 = grp * quarter, c1 = min(P, c0 + quarter);
@@ -110,6 +177,11 @@ __global__ void __launch_bounds__(kSymThreads) k_add_rows(const float* __restric
   __syncthreads();
   const int item = s_item;
   if (item >= items) break;
+  if (item >= sym_items) {  // workgroup-uniform
+    add_plain_row(item - sym_items, pred, target, points, symmetry, R, C, P, margin, norm_rows, norm_rows_dev,
+                  nchunk, rcls, partial, red);
+    continue;  // the loop head synchronises before red is reused
+  }
   const int n = sym_rows[item / nchunk], chunk = item % nchunk;
   const int PC = 4 * C;
   const int cls = rcls[n];
@@ -316,79 +388,6 @@ __global__ void __launch_bounds__(1024) k_add_prep(const float* __restrict__ wei
   }
 }
 
-// Non-symmetric rows (and rows without weight): one workgroup per row, points
-// strided over the threads; the per-point arithmetic is k_add_rows' (cu.cc:140-203).
-__global__ void __launch_bounds__(kAddThreads) k_add_rows_plain(const float* __restrict__ pred,
-                                                                 const float* __restrict__ target,
-                                                                 const float* __restrict__ points,
-                                                                 const float* __restrict__ symmetry, int R_cap,
-                                                                 const int32_t* __restrict__ num_rois_dev, int C,
-                                                                 int P, float margin, int norm_rows,
-                                                                 const int32_t* __restrict__ norm_rows_dev,
-                                                                 int nchunk, const int32_t* __restrict__ rcls,
-                                                                 float* __restrict__ partial) {
-  __shared__ float red[kAddThreads / 64][5];
-  const int n = blockIdx.x;
-  const int R = rows_of(num_rois_dev, R_cap);
-  if (n >= R) return;
-  const int cls = rcls[n];
-  if (cls >= 0 && symmetry[cls] > 0) return;  // k_add_rows handles symmetric rows
-  float* out = partial + (size_t)n * nchunk * 5;
-  for (int i = threadIdx.x; i < nchunk * 5; i += blockDim.x) out[i] = 0.f;
-  if (cls < 0) return;
-  const int PC = 4 * C;
-  const float* tq = target + (size_t)n * PC + 4 * cls;
-  const float* pq = pred + (size_t)n * PC + 4 * cls;
-  float Rg[9], Rp[9];
-  quat2rot(tq[0], tq[1], tq[2], tq[3], Rg);
-  const float s = pq[0], u = pq[1], v = pq[2], w = pq[3];
-  quat2rot(s, u, v, w, Rp);
-  const float d0[9] = {2 * s, -2 * w, 2 * v, 2 * w, 2 * s, -2 * u, -2 * v, 2 * u, 2 * s};
-  const float d1[9] = {2 * u, 2 * v, 2 * w, 2 * v, -2 * u, -2 * s, 2 * w, 2 * s, -2 * u};
-  const float d2[9] = {-2 * v, 2 * u, 2 * s, 2 * u, 2 * v, 2 * w, -2 * s, 2 * w, -2 * v};
-  const float d3[9] = {-2 * w, -2 * s, 2 * u, 2 * s, -2 * w, 2 * v, 2 * u, 2 * v, 2 * w};
-  const int Rn = norm_rows_dev ? *norm_rows_dev : (norm_rows > 0 ? norm_rows : R);
-  const float bn = (float)(Rn * P);
-  const double ln = 2.0 * (double)Rn * (double)P;
-  const float* pts = points + (size_t)cls * P * 3;
-  float acc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
-  for (int p = threadIdx.x; p < P; p += blockDim.x) {
-    const float X0 = pts[p * 3 + 0], X1 = pts[p * 3 + 1], X2 = pts[p * 3 + 2];
-    const float x1 = Rp[0] * X0 + Rp[1] * X1 + Rp[2] * X2;
-    const float y1 = Rp[3] * X0 + Rp[4] * X1 + Rp[5] * X2;
-    const float z1 = Rp[6] * X0 + Rp[7] * X1 + Rp[8] * X2;
-    const float x2 = Rg[0] * X0 + Rg[1] * X1 + Rg[2] * X2;
-    const float y2 = Rg[3] * X0 + Rg[4] * X1 + Rg[5] * X2;
-    const float z2 = Rg[6] * X0 + Rg[7] * X1 + Rg[8] * X2;
-    const float dist = (x1 - x2) * (x1 - x2) + (y1 - y2) * (y1 - y2) + (z1 - z2) * (z1 - z2);
-    if (dist < margin) continue;
-    acc[0] += (float)((double)(dist - margin) / ln);
-    const float X[3] = {X0, X1, X2};
-    const float df[3] = {x1 - x2, y1 - y2, z1 - z2};
-    float e0 = 0.f, e1 = 0.f, e2 = 0.f, e3 = 0.f;  // this point's terms, reference order
-#pragma unroll
-    for (int j = 0; j < 3; j++)
-#pragma unroll
-      for (int k = 0; k < 3; k++) {
-        e0 += df[j] * X[k] * d0[j * 3 + k] / bn;
-        e1 += df[j] * X[k] * d1[j * 3 + k] / bn;
-        e2 += df[j] * X[k] * d2[j * 3 + k] / bn;
-        e3 += df[j] * X[k] * d3[j * 3 + k] / bn;
-      }
-    acc[1] += e0; acc[2] += e1; acc[3] += e2; acc[4] += e3;
-  }
-#pragma unroll
-  for (int q = 0; q < 5; q++) acc[q] = pcnn::wave_sum(acc[q]);
-  if (pcnn::lane_id() == 0)
-    for (int q = 0; q < 5; q++) red[threadIdx.x >> 6][q] = acc[q];
-  __syncthreads();
-  if (threadIdx.x < 5) {
-    float t = 0.f;
-    for (int i = 0; i < (int)(blockDim.x >> 6); i++) t += red[i][threadIdx.x];
-    out[threadIdx.x] = t;
-  }
-}
-
 // One wave per row: fold the chunk partials (fixed tree), write the row of
 // bottom_diff (zeros except the class's 4 channels) and the row loss.
 __global__ void __launch_bounds__(256) k_add_finish_rows(int R_cap, const int32_t* __restrict__ num_rois_dev, int C,
@@ -474,10 +473,8 @@ extern "C" int pcnn_add_loss_fwd(const float* pred, const float* target, const f
   float* row_loss = cv.take<float>(R_cap);
   hipLaunchKernelGGL(k_add_prep, dim3(1), dim3(1024), 0, st, weight, symmetry, R_cap, num_rois_dev, C, rcls,
                      sym_rows, nsym, queue);
-  hipLaunchKernelGGL(k_add_rows_plain, dim3(R_cap), dim3(kAddThreads), 0, st, pred, target, points, symmetry, R_cap,
-                     num_rois_dev, C, P, margin, loss_norm_rows, loss_norm_rows_dev, nchunk, rcls, partial);
-  // symmetric rows: persistent grid over (row, chunk) items of the device-side list
-  const long sym_items = (long)R_cap * nchunk;
+  // one persistent grid: symmetric (row, chunk) items of the device-side list, then the plain rows
+  const long sym_items = (long)R_cap * nchunk + R_cap;  // symmetric (row, chunk) items, then plain rows
   const int sym_grid = (int)(sym_items < ADD_GRID ? sym_items : ADD_GRID);
   hipLaunchKernelGGL(k_add_rows, dim3(sym_grid), dim3(kSymThreads), (size_t)P * sizeof(float4), st, pred,
                      target, weight, points, symmetry, R_cap, num_rois_dev, C, P, margin, loss_norm_rows,

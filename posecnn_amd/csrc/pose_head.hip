@@ -611,6 +611,14 @@ __global__ void __launch_bounds__(XTile<T>::threads, T == 256 ? 1 : 2) k_gemm_x3
       // step s-1, before the barrier, so it may be written at any point here.
       auto stage_part = [&](int c, char* nxt, int kn) {
         if (c < 4) {
+#ifdef PCNN_ABL_ARAW
+          if (A_KC) {  // timing ablation: A stored as if already split (no conversion VALU; wrong results)
+            const int t = threadIdx.x, row = (t >> 3) + (T / 4) * c, kq = t & 7;
+            const int o = x_off(row, kq >> 1) + (kq & 1) * 8;
+            *(uint2*)(nxt + o) = make_uint2(__float_as_uint(va[4 * c]), __float_as_uint(va[4 * c + 1]));
+            *(uint2*)(nxt + kXPart + o) = make_uint2(__float_as_uint(va[4 * c + 2]), __float_as_uint(va[4 * c + 3]));
+          } else
+#endif
           x_store_part<T, A_KC>(va, nxt, nxt + kXPart, c);
           if (A_KC) {
             x_load_part<T, true, RAGGED, A2>(oa, oa2, m0, Meff, kn, ke, va, c);
