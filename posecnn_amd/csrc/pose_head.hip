@@ -958,6 +958,17 @@ extern "C" int pcnn_gemm(int M, int N, int K, const float* A, const float* A2, i
     const int max_grid = T == 256 ? XTile<256>::grid : XTile<128>::grid;
     const long cap_items = (long)mt * nt * kMaxSplitX;
     long grid = cap_items < max_grid ? cap_items : max_grid;
+    if (!M_dev) {
+      // static M: the item count is known up to a device-side K, which can
+      // only lower the split.  Use the fewest workgroups that keep the same
+      // number of rounds (fc6 dW: 1568 tiles -> 224 workgroups x 7): the
+      // makespan is unchanged and the spare CUs run the other stream's kernels.
+      const long items = (long)mt * nt * split_x3(M, N, K, T);
+      const long rounds = (items + max_grid - 1) / max_grid;
+      long g2 = (items + rounds - 1) / rounds;
+      g2 = (g2 + 7) / 8 * 8;
+      if (g2 < grid) grid = g2;
+    }
     if (grid >= 8) grid -= grid % 8;
 #define PCNN_X3_LAUNCH_T(TT, AT, BT, RG, S2)                                                                   \
   do {                                                                                                          \
