@@ -113,6 +113,16 @@ int pcnn_roi_pool_fwd_accumulate(const float* data, int B, int H, int W, int C, 
                                  int pooled_h, int pooled_w, int pool_channel, float* top, int32_t* argmax,
                                  void* stream);
 
+/* Both pose-head RoI pools in one pass (vgg16_convs.py:177-184): pool5 on
+ * data_a (e.g. conv5_3 at 1/16) and pool4 on data_b (conv4_3 at 1/8), NHWC,
+ * all channels, C % 4 == 0, 16-B aligned. Writes top_sum = pool_a + pool_b
+ * (one fp32 add per element, as pcnn_roi_pool_fwd then _accumulate) and both
+ * argmax tensors (R_cap, pooled_h, pooled_w, C). */
+int pcnn_roi_pool_fwd_pair(const float* data_a, int Ha, int Wa, float scale_a, const float* data_b, int Hb, int Wb,
+                           float scale_b, int B, int C, const float* rois, int R_cap, int roi_stride,
+                           const int32_t* num_rois_dev, int pooled_h, int pooled_w, float* top_sum,
+                           int32_t* argmax_a, int32_t* argmax_b, void* stream);
+
 size_t pcnn_roi_pool_bwd_workspace_size(int B, int R_cap);
 
 int pcnn_roi_pool_bwd(const float* top_diff, const int32_t* argmax, int B, int H, int W, int C, int layout,

@@ -85,6 +85,43 @@ __device__ __forceinline__ void upd(float v, int idx, float& m, int& a) {
 // NHWC, all channels, C % 4 == 0: block (roi, bin), lane -> 4 channels.
 // ACC: top += pooled (the pool5 + pool4 sum of vgg16_convs.py:184 produced in
 // place by the second pool; the argmax of each map is still written).
+// Max / argmax of one bin over lane channels c..c+3 (cu.cc:45-97): bin
+// bounds as bin_bounds, strict > first max in raster order, empty bin (or a
+// RoI batch index outside [0, B)) -> 0 / -1.
+__device__ __forceinline__ void bin_max4(const float* __restrict__ data, int B, int H, int W, int C,
+                                         const RoiGeo& g, int ph, int pw, int c, float4& m, int4& a) {
+  const bool bad = g.b < 0 || g.b >= B;
+  int hs, he, ws, we;
+  bin_bounds(g, ph, pw, H, W, hs, he, ws, we);
+  const bool empty = bad || (he <= hs) || (we <= ws);
+  const float* bd = data + (size_t)(bad ? 0 : g.b) * H * W * C;
+  float m0, m1, m2, m3;
+  m0 = m1 = m2 = m3 = empty ? 0.f : -FLT_MAX;
+  int a0 = -1, a1 = -1, a2 = -1, a3 = -1;
+  if (!empty) {
+    for (int h = hs; h < he; h++) {
+      int w = ws;
+      for (; w + 1 < we; w += 2) {  // two independent 16 B loads in flight
+        const int i0 = (h * W + w) * C + c, i1 = i0 + C;
+        const float4 v0 = *(const float4*)(bd + i0);
+        const float4 v1 = *(const float4*)(bd + i1);
+        upd(v0.x, i0 + 0, m0, a0); upd(v0.y, i0 + 1, m1, a1); upd(v0.z, i0 + 2, m2, a2); upd(v0.w, i0 + 3, m3, a3);
+        upd(v1.x, i1 + 0, m0, a0); upd(v1.y, i1 + 1, m1, a1); upd(v1.z, i1 + 2, m2, a2); upd(v1.w, i1 + 3, m3, a3);
+      }
+      if (w < we) {
+        const int i0 = (h * W + w) * C + c;
+        const float4 v0 = *(const float4*)(bd + i0);
+        upd(v0.x, i0 + 0, m0, a0); upd(v0.y, i0 + 1, m1, a1); upd(v0.z, i0 + 2, m2, a2); upd(v0.w, i0 + 3, m3, a3);
+      }
+    }
+  }
+  m = make_float4(m0, m1, m2, m3);
+  a = make_int4(a0, a1, a2, a3);
+}
+
+// NHWC, all channels, C % 4 == 0: block (roi, bin), lane -> 4 channels.
+// ACC: top += pooled (the pool5 + pool4 sum of vgg16_convs.py:184 produced in
+// place by the second pool; the argmax of each map is still written).
 template <bool ACC>
 __global__ void __launch_bounds__(128) k_roi_fwd_nhwc4(const float* __restrict__ data, int B, int H, int W, int C,
                                                         const float* __restrict__ rois, int R_cap, int stride,
@@ -94,41 +131,48 @@ __global__ void __launch_bounds__(128) k_roi_fwd_nhwc4(const float* __restrict__
   if (r >= rows_of(num_rois_dev, R_cap)) return;
   const int ph = bin / PW, pw = bin % PW;
   const RoiGeo g = roi_geo(rois, r, stride, scale, PH, PW);
-  const bool bad = g.b < 0 || g.b >= B;
-  int hs, he, ws, we;
-  bin_bounds(g, ph, pw, H, W, hs, he, ws, we);
-  const bool empty = bad || (he <= hs) || (we <= ws);
-  const float* bd = data + (size_t)(bad ? 0 : g.b) * H * W * C;
   float* to = top + (((size_t)r * PH + ph) * PW + pw) * C;
   int32_t* ao = argmax + (((size_t)r * PH + ph) * PW + pw) * C;
   for (int c = threadIdx.x * 4; c < C; c += blockDim.x * 4) {
-    float m0, m1, m2, m3;
-    m0 = m1 = m2 = m3 = empty ? 0.f : -FLT_MAX;
-    int a0 = -1, a1 = -1, a2 = -1, a3 = -1;
-    if (!empty) {
-      for (int h = hs; h < he; h++) {
-        int w = ws;
-        for (; w + 1 < we; w += 2) {  // two independent 16 B loads in flight
-          const int i0 = (h * W + w) * C + c, i1 = i0 + C;
-          const float4 v0 = *(const float4*)(bd + i0);
-          const float4 v1 = *(const float4*)(bd + i1);
-          upd(v0.x, i0 + 0, m0, a0); upd(v0.y, i0 + 1, m1, a1); upd(v0.z, i0 + 2, m2, a2); upd(v0.w, i0 + 3, m3, a3);
-          upd(v1.x, i1 + 0, m0, a0); upd(v1.y, i1 + 1, m1, a1); upd(v1.z, i1 + 2, m2, a2); upd(v1.w, i1 + 3, m3, a3);
-        }
-        if (w < we) {
-          const int i0 = (h * W + w) * C + c;
-          const float4 v0 = *(const float4*)(bd + i0);
-          upd(v0.x, i0 + 0, m0, a0); upd(v0.y, i0 + 1, m1, a1); upd(v0.z, i0 + 2, m2, a2); upd(v0.w, i0 + 3, m3, a3);
-        }
-      }
-    }
+    float4 m;
+    int4 a;
+    bin_max4(data, B, H, W, C, g, ph, pw, c, m, a);
     if (ACC) {
       const float4 p = *(const float4*)(to + c);
-      *(float4*)(to + c) = make_float4(p.x + m0, p.y + m1, p.z + m2, p.w + m3);
+      *(float4*)(to + c) = make_float4(p.x + m.x, p.y + m.y, p.z + m.z, p.w + m.w);
     } else {
-      *(float4*)(to + c) = make_float4(m0, m1, m2, m3);
+      *(float4*)(to + c) = m;
     }
-    *(int4*)(ao + c) = make_int4(a0, a1, a2, a3);
+    *(int4*)(ao + c) = a;
+  }
+}
+
+// Both RoI pools of the pose head in one pass (vgg16_convs.py:177-184:
+// pool5 on conv5_3 at 1/16, pool4 on conv4_3 at 1/8, then their sum): block
+// (roi, bin) takes the bin on both maps, so the two maps' loads are in flight
+// together, and writes pool5 + pool4 (the same single fp32 add as the
+// accumulate pass) and both argmax tensors — no pool5 round trip through HBM.
+__global__ void __launch_bounds__(128) k_roi_fwd_pair_nhwc4(const float* __restrict__ data_a, int Ha, int Wa,
+                                                             float scale_a, const float* __restrict__ data_b, int Hb,
+                                                             int Wb, float scale_b, int B, int C,
+                                                             const float* __restrict__ rois, int R_cap, int stride,
+                                                             const int32_t* __restrict__ num_rois_dev, int PH, int PW,
+                                                             float* __restrict__ top, int32_t* __restrict__ arg_a,
+                                                             int32_t* __restrict__ arg_b) {
+  const int r = blockIdx.x, bin = blockIdx.y;
+  if (r >= rows_of(num_rois_dev, R_cap)) return;
+  const int ph = bin / PW, pw = bin % PW;
+  const RoiGeo ga = roi_geo(rois, r, stride, scale_a, PH, PW);
+  const RoiGeo gb = roi_geo(rois, r, stride, scale_b, PH, PW);
+  const size_t o = (((size_t)r * PH + ph) * PW + pw) * C;
+  for (int c = threadIdx.x * 4; c < C; c += blockDim.x * 4) {
+    float4 ma, mb;
+    int4 aa, ab;
+    bin_max4(data_a, B, Ha, Wa, C, ga, ph, pw, c, ma, aa);
+    bin_max4(data_b, B, Hb, Wb, C, gb, ph, pw, c, mb, ab);
+    *(float4*)(top + o + c) = make_float4(ma.x + mb.x, ma.y + mb.y, ma.z + mb.z, ma.w + mb.w);
+    *(int4*)(arg_a + o + c) = aa;
+    *(int4*)(arg_b + o + c) = ab;
   }
 }
 
@@ -463,6 +507,25 @@ extern "C" int pcnn_roi_pool_fwd_accumulate(const float* data, int B, int H, int
                                             void* stream) {
   return roi_pool_fwd(data, B, H, W, C, layout, rois, R_cap, roi_stride, num_rois_dev, spatial_scale, pooled_h,
                       pooled_w, pool_channel, 1, top, argmax, stream);
+}
+
+extern "C" int pcnn_roi_pool_fwd_pair(const float* data_a, int Ha, int Wa, float scale_a, const float* data_b, int Hb,
+                                      int Wb, float scale_b, int B, int C, const float* rois, int R_cap, int roi_stride,
+                                      const int32_t* num_rois_dev, int pooled_h, int pooled_w, float* top_sum,
+                                      int32_t* argmax_a, int32_t* argmax_b, void* stream) {
+  PCNN_REQUIRE(data_a && data_b && rois && top_sum && argmax_a && argmax_b && B > 0 && C > 0 && C % 4 == 0);
+  PCNN_REQUIRE(Ha > 0 && Wa > 0 && Hb > 0 && Wb > 0 && pooled_h > 0 && pooled_w > 0 && R_cap >= 0);
+  PCNN_REQUIRE(roi_stride >= 5);
+  PCNN_REQUIRE((long)Ha * Wa * C < (1l << 31) && (long)Hb * Wb * C < (1l << 31));
+  PCNN_REQUIRE(((((uintptr_t)data_a) | ((uintptr_t)data_b) | ((uintptr_t)top_sum) | ((uintptr_t)argmax_a) |
+                 ((uintptr_t)argmax_b)) & 15) == 0);
+  if (R_cap == 0) return PCNN_OK;
+  const int threads = C / 4 >= 128 ? 128 : ((C / 4 + 63) / 64) * 64;
+  hipLaunchKernelGGL(k_roi_fwd_pair_nhwc4, dim3(R_cap, pooled_h * pooled_w), dim3(threads), 0, (hipStream_t)stream,
+                     data_a, Ha, Wa, scale_a, data_b, Hb, Wb, scale_b, B, C, rois, R_cap, roi_stride, num_rois_dev,
+                     pooled_h, pooled_w, top_sum, argmax_a, argmax_b);
+  PCNN_CHECK_LAUNCH();
+  return PCNN_OK;
 }
 
 extern "C" size_t pcnn_roi_pool_bwd_workspace_size(int B, int R_cap) {

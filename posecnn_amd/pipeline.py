@@ -120,10 +120,9 @@ class PoseStep:
         nr = h["num_rois"][1:2]  # output row count (incl. dummy row)
         w = self.weights
         K6 = 49 * self.Ch
-        with self._t("roi_pool_fwd"):
-            rp.roi_pool(conv5, h["box"], 7, 7, 1.0 / 16.0, 0, num_rois=nr, out=(self.pool, self.arg5))
-            rp.roi_pool(conv4, h["box"], 7, 7, 1.0 / 8.0, 0, num_rois=nr, out=(self.pool, self.arg4),
-                        accumulate=True)  # pool = pool5 + pool4
+        with self._t("roi_pool_fwd"):  # pool = pool5 + pool4 (vgg16_convs.py:177-184), one pass
+            rp.roi_pool_pair(conv5, 1.0 / 16.0, conv4, 1.0 / 8.0, h["box"], 7, 7, num_rois=nr,
+                             out=(self.pool, self.arg5, self.arg4))
         x = self.pool.view(CAP, K6)
         with self._t("gemm_fc6_fwd"):
             ph.gemm(x, w.w6, self.y6, bias=w.b6, act=1, M_dev=nr, precision=self.prec)

@@ -47,6 +47,34 @@ def roi_pool(bottom_data, bottom_rois, pooled_height, pooled_width, spatial_scal
     return top, arg
 
 
+def roi_pool_pair(data_a, scale_a, data_b, scale_b, rois, pooled_height, pooled_width, num_rois=None, out=None):
+    """pool_a + pool_b and both argmax tensors in one pass (vgg16_convs.py:177-184:
+    roi_pool(conv5_3, 1/16) + roi_pool(conv4_3, 1/8)); NHWC, all channels.
+    Equal to roi_pool(data_a) then roi_pool(data_b, accumulate=True)."""
+    _lib.require_gpu(data_a, data_b, rois)
+    if data_a.dim() != 4 or data_b.dim() != 4 or rois.dim() != 2:
+        raise ValueError("data must be 4-dimensional and rois 2-dimensional")
+    da, db = data_a.contiguous().float(), data_b.contiguous().float()
+    B, Ha, Wa, C = da.shape
+    Bb, Hb, Wb, Cb = db.shape
+    if (Bb, Cb) != (B, C):
+        raise ValueError("both maps need the same batch and channel count")
+    rois = rois.contiguous().float()
+    R, stride = rois.shape
+    shape = (R, pooled_height, pooled_width, C)
+    if out is None:
+        out = (torch.empty(shape, dtype=torch.float32, device=da.device),
+               torch.empty(shape, dtype=torch.int32, device=da.device),
+               torch.empty(shape, dtype=torch.int32, device=da.device))
+    top, arg_a, arg_b = out
+    rc = _lib.load().pcnn_roi_pool_fwd_pair(_lib.ptr(da), Ha, Wa, float(scale_a), _lib.ptr(db), Hb, Wb,
+                                            float(scale_b), B, C, _lib.ptr(rois), R, stride, _lib.ptr(num_rois),
+                                            int(pooled_height), int(pooled_width), _lib.ptr(top), _lib.ptr(arg_a),
+                                            _lib.ptr(arg_b), _lib.stream_ptr())
+    _lib.check(rc, "roi_pool_pair")
+    return top, arg_a, arg_b
+
+
 def roi_pool_grad(bottom_data, bottom_rois, argmax, grad, pooled_height, pooled_width, spatial_scale,
                   pool_channel=0, name=None, num_rois=None, layout=0, out=None):
     _lib.require_gpu(bottom_data, bottom_rois, argmax, grad)

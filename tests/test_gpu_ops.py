@@ -97,6 +97,28 @@ def test_roi_pool_device_count(hip, orc):
     np.testing.assert_array_equal(dd.cpu().numpy(), od)
 
 
+def test_roi_pool_pair(hip, orc):
+    """pool5 + pool4 in one pass == the two oracle pools added in fp32, argmax of
+    both maps bit-exact, device row count honoured (rows past it untouched)."""
+    rng = np.random.default_rng(9)
+    B, C = 2, 64
+    d5 = rng.normal(size=(B, 30, 40, C)).astype(np.float32)
+    d4 = rng.normal(size=(B, 60, 80, C)).astype(np.float32)
+    d4[0, 10:20, 10:30] = 0.25  # plateaus -> first-max ties
+    rois = _rois(rng, 29, B, 480, 640, 1)
+    nr = torch.tensor([23], dtype=torch.int32, device=D)
+    top = torch.full((29, 7, 7, C), 7.0, device=D)
+    a5 = torch.full((29, 7, 7, C), -7, dtype=torch.int32, device=D)
+    a4 = torch.full((29, 7, 7, C), -7, dtype=torch.int32, device=D)
+    rp.roi_pool_pair(T(d5), 1.0 / 16, T(d4), 1.0 / 8, T(rois), 7, 7, num_rois=nr, out=(top, a5, a4))
+    o5, oa5 = orc.roi_pool_fwd(d5, rois, 7, 7, 1.0 / 16, 0)
+    o4, oa4 = orc.roi_pool_fwd(d4, rois, 7, 7, 1.0 / 8, 0)
+    np.testing.assert_array_equal(top[:23].cpu().numpy(), (o5 + o4)[:23])
+    np.testing.assert_array_equal(a5[:23].cpu().numpy(), oa5[:23])
+    np.testing.assert_array_equal(a4[:23].cpu().numpy(), oa4[:23])
+    assert (top[23:] == 7.0).all() and (a5[23:] == -7).all()
+
+
 def _add_inputs(rng, R, C=22, sym_rows=True):
     pts, sym = synth.rescaled_points(C)
     pred = rng.normal(size=(R, 4 * C)).astype(np.float32) * 0.5
