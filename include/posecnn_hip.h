@@ -77,6 +77,18 @@ int pcnn_hough_voting_prob(const float* prob, int32_t* label_out, const float* v
                            float* top_target, float* top_weight, int32_t* top_domain, int32_t* num_rois, int cap,
                            int32_t* debug_counts, void* workspace, size_t workspace_bytes, void* stream);
 
+/* pcnn_hough_voting on a class-compact vertex map:
+ * vertex3 (B,H,W,3) holds, per pixel, the 3 vertex channels of that pixel's
+ * own label class (pcnn_vertex_pred_compact) instead of all 3C. Voters read
+ * only their own class's channels (cu.cc:276-280), so the outputs equal
+ * pcnn_hough_voting on any full map with those channels. C = num classes. */
+int pcnn_hough_voting_compact(const int32_t* label, const float* vertex3, const float* extents, const float* meta,
+                              int num_meta, const float* gt, int num_gt, int B, int H, int W, int C, int batch_base,
+                              int global_batch, int is_train, float inlier_thr, int label_thr, float vote_thr,
+                              float per_thr, int skip_pixels, float* top_box, float* top_pose, float* top_target,
+                              float* top_weight, int32_t* top_domain, int32_t* num_rois, int cap,
+                              int32_t* debug_counts, void* workspace, size_t workspace_bytes, void* stream);
+
 /* HoughvotinggpuGrad (hough_voting_gpu_op.cc:440-484; set_gradients cu.cc:608-612):
  * zero gradients for label (B,H,W) and vertex (B,H,W,3C). Either may be NULL. */
 int pcnn_hough_voting_grad(float* grad_label, float* grad_vertex, int B, int H, int W, int C, void* stream);
@@ -235,6 +247,15 @@ int pcnn_argmax_2d(const float* prob, int B, int H, int W, int C, int32_t* label
 int pcnn_hard_label_fwd(const float* prob, const int32_t* gt, int B, int H, int W, int C, float threshold,
                         float* top, void* stream);
 int pcnn_hard_label_bwd(float* grad_prob, float* grad_gt, int B, int H, int W, int C, void* stream);
+
+/* vertex_pred (vgg16_convs.py:152-163: 1x1 conv K -> 3C + bias_add,
+ * network.py:168-185) evaluated only at each pixel's label class (SURVEY
+ * §8(f) row 3): feat (B,H,W,K) NHWC, K % 4 == 0, weights (K,3C) as the
+ * reference's [1,1,K,3C] kernel, bias (3C), label (B,H,W) -> vertex3 (B,H,W,3)
+ * = (sum_k feat[k] * w[k][3l+j] in k order) + bias[3l+j]; zeros for labels
+ * outside [0, C). K * 3C * 4 B <= 64 KiB. */
+int pcnn_vertex_pred_compact(const float* feat, const float* weights, const float* bias, const int32_t* label, int B,
+                             int H, int W, int K, int C, float* vertex3, void* stream);
 
 #ifdef __cplusplus
 }

@@ -249,3 +249,25 @@ def hard_label(prob, gt, threshold):
                 if g > 0 or prob[b, y, x, g] < np.float32(threshold):
                     top[b, y, x, g] = 1.0
     return top
+
+
+def vertex_pred_compact(feat, weights, biases, label):
+    """vertex_pred (vgg16_convs.py:152-163: conv2d 1x1 K -> 3C, then bias_add,
+    network.py:168-185) at each pixel's own class channels 3l..3l+2: the dot
+    product summed in k order in float32 (each product and sum rounded), then
+    the bias; labels outside [0, C) give zeros."""
+    feat = np.asarray(feat, np.float32)
+    B, H, W, K = feat.shape
+    w = np.asarray(weights, np.float32).reshape(K, -1)
+    b = np.asarray(biases, np.float32).reshape(-1)
+    C = w.shape[1] // 3
+    lab = np.asarray(label).reshape(-1).astype(np.int64)
+    x = feat.reshape(-1, K)
+    ok = (lab >= 0) & (lab < C)
+    cols = 3 * np.where(ok, lab, 0)[:, None] + np.arange(3)[None, :]
+    acc = np.zeros((x.shape[0], 3), np.float32)
+    for k in range(K):
+        acc = acc + x[:, k:k + 1] * w[k][cols]
+    acc = acc + b[cols]
+    acc[~ok] = 0.0
+    return acc.reshape(B, H, W, 3)

@@ -35,6 +35,10 @@ _SIGS = {
                                        c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_int, c_float,
                                        c_float, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                        c_int, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "pcnn_hough_voting_compact": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int, c_int,
+                                          c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_int, c_float, c_float,
+                                          c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
+                                          c_void_p, c_void_p, c_size_t, c_void_p]),
     "pcnn_hough_voting_grad": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p]),
     "pcnn_hough_voting_diag": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_float, c_void_p, c_void_p]),
     "pcnn_roi_pool_fwd": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p,
@@ -65,6 +69,8 @@ _SIGS = {
     "pcnn_argmax_2d": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
     "pcnn_hard_label_fwd": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float, c_void_p, c_void_p]),
     "pcnn_hard_label_bwd": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p]),
+    "pcnn_vertex_pred_compact": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int,
+                                         c_void_p, c_void_p]),
     "pcnn_pose_head_fwd": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p]),
     "pcnn_pose_head_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p,
                                    c_void_p]),

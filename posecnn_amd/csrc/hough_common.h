@@ -379,7 +379,7 @@ __global__ void k_label_hist(const int32_t* __restrict__ label, int HW, int C, H
 __global__ void k_label_hist_prob(const float* __restrict__ prob, int32_t* __restrict__ label_out, int HW, int C,
                                   HoughWs ws);
 __global__ void k_label_scan(int C, int label_thr, int index_size, int nms, int skip, HoughWs ws);
-__global__ void k_label_scatter(const int32_t* __restrict__ label, const float* __restrict__ vertex,
+__global__ void k_label_scatter(const int32_t* __restrict__ label, const float* __restrict__ vertex, int vch,
                                 const float* __restrict__ extents, const float* __restrict__ meta, int num_meta,
                                 int H, int W, int C, int skip, HoughWs ws);
 __global__ void k_voter_setup(int H, int W, int C, float inlier, double so, double si, HoughWs ws);

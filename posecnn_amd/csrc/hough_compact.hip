@@ -161,8 +161,11 @@ __device__ __forceinline__ void bound_setup(double ex, double ey, double cc, dou
   else c2 = qx > 0.0 ? kNeedNegDy : kNeedPosDy;
 }
 
+// vch = channels per vertex pixel: 3C (the reference's (B,H,W,3C) map, a
+// voter reads its class's channels 3l..3l+2) or 3 (the class-compact map of
+// the pixel's own class only).
 __global__ void __launch_bounds__(kCompactThreads) k_label_scatter(const int32_t* __restrict__ label,
-                                                                    const float* __restrict__ vertex,
+                                                                    const float* __restrict__ vertex, int vch,
                                                                     const float* __restrict__ extents,
                                                                     const float* __restrict__ meta, int num_meta,
                                                                     int H, int W, int C, int skip, HoughWs ws) {
@@ -196,7 +199,7 @@ __global__ void __launch_bounds__(kCompactThreads) k_label_scatter(const int32_t
       for (int w = 0; w < wave; w++) rank += wcnt[w][l];
       if (rank % skip == 0) {  // list positions 0, skip, 2 skip, ... (cu.cc:269)
         const size_t vi = (size_t)b * ws.vcap + ws.vbase[(size_t)b * C + l] + rank / skip;
-        const size_t off = ((size_t)b * HW + p) * (size_t)(3 * C) + 3 * l;
+        const size_t off = ((size_t)b * HW + p) * (size_t)vch + (vch == 3 ? 0 : 3 * l);
         const float u = vertex[off], v = vertex[off + 1];
         const float d = (float)exp((double)vertex[off + 2]);  // cu.cc:280
         const float T = project_box(l, extents, mb, d, 0.6f);  // cu.cc:285

@@ -71,7 +71,7 @@ extern "C" size_t pcnn_hough_voting_workspace_size(int B, int H, int W, int C, i
 // label given (pcnn_hough_voting) or produced from prob_normalized by the
 // fused argmax (pcnn_hough_voting_prob: label = label_out, written here).
 static int hough_voting_impl(const int32_t* label, const float* prob, int32_t* label_out, const float* vertex,
-                             const float* extents, const float* meta, int num_meta, const float* gt, int num_gt,
+                             int vch, const float* extents, const float* meta, int num_meta, const float* gt, int num_gt,
                              int B, int H, int W, int C, int batch_base, int global_batch, int is_train,
                              float inlier_thr, int label_thr, float vote_thr, float per_thr, int skip_pixels,
                              float* top_box, float* top_pose, float* top_target, float* top_weight,
@@ -103,7 +103,7 @@ static int hough_voting_impl(const int32_t* label, const float* prob, int32_t* l
   }
   hipLaunchKernelGGL(k_label_scan, dim3(B), dim3(1024), 0, st, C, label_thr, index_size, nms ? 1 : 0, skip_pixels,
                      ws);
-  hipLaunchKernelGGL(k_label_scatter, dim3(ws.nblk, B), dim3(kCompactThreads), 0, st, label, vertex, extents, meta,
+  hipLaunchKernelGGL(k_label_scatter, dim3(ws.nblk, B), dim3(kCompactThreads), 0, st, label, vertex, vch, extents, meta,
                      num_meta, H, W, C, skip_pixels, ws);
   {
     const double c = (double)inlier_thr, co = c - kConeEps, ci = c + kConeEps;
@@ -155,7 +155,7 @@ extern "C" int pcnn_hough_voting(const int32_t* label, const float* vertex, cons
                                  int cap, int32_t* debug_counts, void* workspace, size_t workspace_bytes,
                                  void* stream) {
   if (!label) return PCNN_EINVAL;
-  return hough_voting_impl(label, nullptr, nullptr, vertex, extents, meta, num_meta, gt, num_gt, B, H, W, C,
+  return hough_voting_impl(label, nullptr, nullptr, vertex, 3 * C, extents, meta, num_meta, gt, num_gt, B, H, W, C,
                            batch_base, global_batch, is_train, inlier_thr, label_thr, vote_thr, per_thr, skip_pixels,
                            top_box, top_pose, top_target, top_weight, top_domain, num_rois, cap, debug_counts,
                            workspace, workspace_bytes, stream);
@@ -170,7 +170,22 @@ extern "C" int pcnn_hough_voting_prob(const float* prob, int32_t* label_out, con
                                       int32_t* debug_counts, void* workspace, size_t workspace_bytes,
                                       void* stream) {
   if (!prob || !label_out) return PCNN_EINVAL;
-  return hough_voting_impl(nullptr, prob, label_out, vertex, extents, meta, num_meta, gt, num_gt, B, H, W, C,
+  return hough_voting_impl(nullptr, prob, label_out, vertex, 3 * C, extents, meta, num_meta, gt, num_gt, B, H, W, C,
+                           batch_base, global_batch, is_train, inlier_thr, label_thr, vote_thr, per_thr, skip_pixels,
+                           top_box, top_pose, top_target, top_weight, top_domain, num_rois, cap, debug_counts,
+                           workspace, workspace_bytes, stream);
+}
+
+extern "C" int pcnn_hough_voting_compact(const int32_t* label, const float* vertex3, const float* extents,
+                                         const float* meta, int num_meta, const float* gt, int num_gt, int B, int H,
+                                         int W, int C, int batch_base, int global_batch, int is_train,
+                                         float inlier_thr, int label_thr, float vote_thr, float per_thr,
+                                         int skip_pixels, float* top_box, float* top_pose, float* top_target,
+                                         float* top_weight, int32_t* top_domain, int32_t* num_rois, int cap,
+                                         int32_t* debug_counts, void* workspace, size_t workspace_bytes,
+                                         void* stream) {
+  if (!label) return PCNN_EINVAL;
+  return hough_voting_impl(label, nullptr, nullptr, vertex3, 3, extents, meta, num_meta, gt, num_gt, B, H, W, C,
                            batch_base, global_batch, is_train, inlier_thr, label_thr, vote_thr, per_thr, skip_pixels,
                            top_box, top_pose, top_target, top_weight, top_domain, num_rois, cap, debug_counts,
                            workspace, workspace_bytes, stream);

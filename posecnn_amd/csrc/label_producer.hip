@@ -9,6 +9,11 @@
 //  Hardlabel  one-hot GT label weights (lib/hard_label_layer/
 //             hard_label_op_gpu.cu.cc:17-29, grad :56-64), written as a single
 //             coalesced stream of the (B,H,W,C) output.
+//  vertex_pred, class-compact: the 1x1 conv 128 -> 3C
+//             + bias of vgg16_convs.py:152-163 evaluated only at the 3
+//             channels of each pixel's label class, written as (B,H,W,3):
+//             12 B/px instead of the 264 B/px (C = 22) map the Hough op
+//             reads ~2 % of.
 #include "hough_common.h"
 
 namespace {
@@ -61,6 +66,47 @@ __global__ void __launch_bounds__(256) k_hard_label(const float* __restrict__ pr
   }
 }
 
+// One thread per pixel over a persistent grid; the (K, 3C) weights sit in
+// LDS.  out[j] = (sum over k in order of feat[k] * w[k][3l + j]) + bias[3l + j]
+// (conv2d then bias_add, network.py:168-185), every op rounded separately.
+// A label outside [0, C) writes zeros (the vote never reads such pixels).
+constexpr int kVpThreads = 256;
+__global__ void __launch_bounds__(kVpThreads) k_vertex_pred_compact(const float* __restrict__ feat,
+                                                                    const float* __restrict__ w,
+                                                                    const float* __restrict__ bias,
+                                                                    const int32_t* __restrict__ label, long n_pix,
+                                                                    int K, int C, float* __restrict__ out) {
+  extern __shared__ float wl[];  // [K][3C]
+  const int NC3 = 3 * C;
+  for (int i = threadIdx.x; i < K * NC3; i += blockDim.x) wl[i] = w[i];
+  __syncthreads();
+  for (long p = (long)blockIdx.x * blockDim.x + threadIdx.x; p < n_pix; p += (long)gridDim.x * blockDim.x) {
+    const int l = label[p];
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f;
+    if (l >= 0 && l < C) {
+      const float4* x4 = (const float4*)(feat + p * K);
+      const float* wc = wl + 3 * l;
+      for (int k4 = 0; k4 < K / 4; k4++) {
+        const float4 x = x4[k4];
+        const float xv[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+          const float* wr = wc + (4 * k4 + e) * NC3;
+          a0 = a0 + xv[e] * wr[0];
+          a1 = a1 + xv[e] * wr[1];
+          a2 = a2 + xv[e] * wr[2];
+        }
+      }
+      a0 = a0 + bias[3 * l + 0];
+      a1 = a1 + bias[3 * l + 1];
+      a2 = a2 + bias[3 * l + 2];
+    }
+    out[p * 3 + 0] = a0;
+    out[p * 3 + 1] = a1;
+    out[p * 3 + 2] = a2;
+  }
+}
+
 inline size_t argmax_lds(int C) { return C <= kArgmaxStagedMaxC ? (size_t)(kArgThreads / 64) * 64 * C * 4 : 0; }
 
 }  // namespace
@@ -98,6 +144,22 @@ extern "C" int pcnn_hard_label_bwd(float* grad_prob, float* grad_gt, int B, int 
   const size_t n_pix = (size_t)B * H * W;
   if (grad_prob && hipMemsetAsync(grad_prob, 0, n_pix * C * sizeof(float), st) != hipSuccess) return PCNN_EHIP;
   if (grad_gt && hipMemsetAsync(grad_gt, 0, n_pix * sizeof(float), st) != hipSuccess) return PCNN_EHIP;
+  PCNN_CHECK_LAUNCH();
+  return PCNN_OK;
+}
+
+extern "C" int pcnn_vertex_pred_compact(const float* feat, const float* weights, const float* bias,
+                                        const int32_t* label, int B, int H, int W, int K, int C, float* vertex3,
+                                        void* stream) {
+  PCNN_REQUIRE(feat && weights && bias && label && vertex3 && B > 0 && H > 0 && W > 0 && C > 0);
+  PCNN_REQUIRE(K > 0 && K % 4 == 0 && (((uintptr_t)feat) & 15) == 0);
+  const size_t lds = (size_t)K * 3 * C * sizeof(float);
+  PCNN_REQUIRE(lds <= 64 * 1024);
+  const long n_pix = (long)B * H * W;
+  long blocks = (n_pix + kVpThreads - 1) / kVpThreads;
+  if (blocks > 256 * 4) blocks = 256 * 4;  // persistent: the weights are staged once per workgroup
+  hipLaunchKernelGGL(k_vertex_pred_compact, dim3((unsigned)blocks), dim3(kVpThreads), lds, (hipStream_t)stream, feat,
+                     weights, bias, label, n_pix, K, C, vertex3);
   PCNN_CHECK_LAUNCH();
   return PCNN_OK;
 }

@@ -28,14 +28,19 @@ def _as_meta2d(meta, B):
 
 def hough_voting_gpu_capacity(label, vertex, extents, meta_data, gt, is_train, threshold_vote,
                               threshold_percentage, skip_pixels, inlier_threshold=0.9, label_threshold=500,
-                              batch_base=0, global_batch=None, out=None, debug_counts=None, stream=None, prob=None):
+                              batch_base=0, global_batch=None, out=None, debug_counts=None, stream=None, prob=None,
+                              vertex_compact=False):
     """Launch without host sync.  Returns dict of capacity-sized tensors and
     `num_rois` (int32[2] on device: rows, max(rows, 1)).
 
     With `prob` (B,H,W,C) given instead of `label` (pass label=None), the
     label producer runs fused into the op (pcnn_hough_voting_prob): label_2d =
     argmax over the class axis (network.py:433-434) is computed inside the
-    compaction pass and returned as out["label"]."""
+    compaction pass and returned as out["label"].
+
+    vertex_compact=True: `vertex` is the class-compact (B,H,W,3) map of
+    vertex_pred.vertex_pred_compact (each pixel's own class channels; SURVEY
+    8(f) row 3); the class count then comes from `extents` (C,3)."""
     _lib.require_gpu(label, prob, vertex, extents, meta_data, gt)
     lib = _lib.load()
     if (label is None) == (prob is None):
@@ -47,7 +52,12 @@ def hough_voting_gpu_capacity(label, vertex, extents, meta_data, gt, is_train, t
     if vertex.dim() != 4:
         raise ValueError("vertex must be 4-dimensional")  # :331-332
     B, H, W = (label.shape if label is not None else prob.shape[:3])
-    C = vertex.shape[3] // 3
+    if vertex_compact:
+        if label is None or vertex.shape[3] != 3:
+            raise ValueError("vertex_compact takes label and a (B,H,W,3) vertex map")
+        C = extents.shape[0]
+    else:
+        C = vertex.shape[3] // 3
     if prob is not None and prob.shape[3] != C:
         raise ValueError(f"prob has {prob.shape[3]} classes, vertex has {C}")
     dev = vertex.device
@@ -72,8 +82,12 @@ def hough_voting_gpu_capacity(label, vertex, extents, meta_data, gt, is_train, t
         out["label"] = torch.empty((B, H, W), dtype=torch.int32, device=dev)
     nbytes = lib.pcnn_hough_voting_workspace_size(B, H, W, C, int(skip_pixels), float(threshold_vote))
     ws = _lib.workspace(nbytes, dev, "hough")
-    head = ((lib.pcnn_hough_voting, _lib.ptr(label)) if prob is None else
-            (lib.pcnn_hough_voting_prob, _lib.ptr(prob), _lib.ptr(out["label"])))
+    if prob is not None:
+        head = (lib.pcnn_hough_voting_prob, _lib.ptr(prob), _lib.ptr(out["label"]))
+    elif vertex_compact:
+        head = (lib.pcnn_hough_voting_compact, _lib.ptr(label))
+    else:
+        head = (lib.pcnn_hough_voting, _lib.ptr(label))
     rc = head[0](
         *head[1:], _lib.ptr(vertex), _lib.ptr(extents), _lib.ptr(meta), meta.shape[1],
         _lib.ptr(gt) if gt.numel() else None, gt.shape[0], B, H, W, C, int(batch_base),

@@ -55,6 +55,25 @@ res = {
     "hough_prob_fused_us": timeit(lambda: hv.hough_voting_gpu_capacity(None, *args, out=o2, prob=prob)),
     "hard_label_us": timeit(lambda: hl.hard_label(prob, gt_label, 0.9)),
 }
+# class-compact vertex map: producer + vote on it vs the vote on the full map
+from posecnn_amd.vertex_pred import vertex_pred_compact  # noqa: E402
+K = 128
+feat = torch.randn((B, H, W, K), generator=g, device=D)
+vw = torch.randn((K, 3 * C), generator=g, device=D) * 0.05
+vb = torch.randn((3 * C,), generator=g, device=D)
+v3 = torch.empty((B, H, W, 3), device=D)
+res["vertex_pred_compact_us"] = timeit(lambda: vertex_pred_compact(feat, vw, vb, lab, out=v3))
+# the vote on the compact form of the frames' own vertex map (same field as hough_label_us)
+vfull = args[0]
+idx = (3 * lab.long()).unsqueeze(3) + torch.arange(3, device=D)
+v3f = torch.gather(vfull, 3, idx).contiguous()
+oc = hv.hough_voting_gpu_capacity(lab, v3f, *args[1:], vertex_compact=True)
+res["hough_compact_us"] = timeit(lambda: hv.hough_voting_gpu_capacity(lab, v3f, *args[1:], out=oc, vertex_compact=True))
+nr = int(o1["num_rois"][1].item())
+assert torch.equal(oc["num_rois"], o1["num_rois"])
+for k in ("box", "pose", "target", "weight", "domain"):
+    assert torch.equal(oc[k][:nr], o1[k][:nr]), k
+res["vertex_pred_compact_GBps"] = (B * H * W * (K * 4 + 4 + 12)) / (res["vertex_pred_compact_us"] * 1e-6) / 1e9
 res["argmax_then_hough_us"] = res["argmax_2d_us"] + res["hough_label_us"]
 prob_bytes = B * H * W * C * 4
 res["argmax_2d_GBps"] = (prob_bytes + B * H * W * 4) / (res["argmax_2d_us"] * 1e-6) / 1e9

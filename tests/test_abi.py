@@ -39,7 +39,8 @@ def test_header_declares_the_reference_surface():
     for n in ("pcnn_hough_voting", "pcnn_hough_voting_grad", "pcnn_roi_pool_fwd", "pcnn_roi_pool_bwd",
               "pcnn_add_loss_fwd", "pcnn_add_loss_bwd", "pcnn_backproject_fwd", "pcnn_backproject_bwd",
               "pcnn_gemm", "pcnn_abi_version", "pcnn_strerror", "pcnn_box_nms", "pcnn_argmax_2d",
-              "pcnn_hard_label_fwd", "pcnn_hard_label_bwd", "pcnn_hough_voting_prob", "pcnn_roi_pool_fwd_pair"):
+              "pcnn_hard_label_fwd", "pcnn_hard_label_bwd", "pcnn_hough_voting_prob", "pcnn_roi_pool_fwd_pair",
+              "pcnn_hough_voting_compact", "pcnn_vertex_pred_compact"):
         assert n in names
 
 

@@ -96,3 +96,35 @@ def test_hough_from_prob_full_frame_matches_label_path(hip):
     assert n == int(b["num_rois"][1].item()) and n > 1
     for k in ("box", "pose", "target", "weight", "domain"):
         assert torch.equal(a[k][:n], b[k][:n]), k
+
+
+@pytest.mark.parametrize("B,H,W,K,C", [(2, 24, 32, 128, 22), (1, 9, 13, 16, 4)])
+def test_vertex_pred_compact(hip, orc, B, H, W, K, C):
+    """Class-compact vertex_pred bit-exact vs the oracle's
+    k-ordered fp32 restatement; labels outside [0, C) -> zeros."""
+    from posecnn_amd.vertex_pred import vertex_pred_compact
+    rng = np.random.default_rng(K + C)
+    feat = rng.normal(size=(B, H, W, K)).astype(np.float32)
+    w = (rng.normal(size=(1, 1, K, 3 * C)) * 0.05).astype(np.float32)
+    b = rng.normal(size=3 * C).astype(np.float32)
+    lab = rng.integers(0, C, size=(B, H, W)).astype(np.int32)
+    lab[0, 0, :2] = [-1, C]
+    out = vertex_pred_compact(T(feat), T(w), T(b), T(lab))
+    np.testing.assert_array_equal(out.cpu().numpy(), orc.vertex_pred_compact(feat, w, b, lab))
+
+
+@pytest.mark.parametrize("is_train,thr_vote", [(1, -1.0), (0, 0.5)])
+def test_hough_from_compact_vertex_matches_full(hip, is_train, thr_vote):
+    """The vote on the class-compact (B,H,W,3) map equals the vote on the full
+    (B,H,W,3C) map, bit for bit, at the bench size (640x480, 22 classes)."""
+    fr = synth.make_frames(2, 480, 640, num_classes=22, objects_per_image=6, seed=3)
+    lab = fr["label"]
+    b, y, x = np.indices(lab.shape)
+    v3 = np.stack([fr["vertex"][b, y, x, 3 * lab + j] for j in range(3)], axis=-1).astype(np.float32)
+    args = (T(fr["extents"]), T(fr["meta"]), T(fr["gt"]), is_train, thr_vote, 0.02, 10)
+    a = hv.hough_voting_gpu_capacity(T(lab), T(fr["vertex"]), *args)
+    c = hv.hough_voting_gpu_capacity(T(lab), T(v3), *args, vertex_compact=True)
+    n = int(a["num_rois"][1].item())
+    assert n == int(c["num_rois"][1].item()) and n > 1
+    for k in ("box", "pose", "target", "weight", "domain"):
+        assert torch.equal(a[k][:n], c[k][:n]), k

@@ -28,3 +28,17 @@ def test_hard_label_known_answers():
     want[0, 0, 2, 2] = 1      # foreground always labelled
     want[0, 0, 4, 1] = 1
     np.testing.assert_array_equal(top, want)  # gt -1 and out-of-range 3 -> zero rows
+
+
+def test_vertex_pred_compact_known_answer():
+    # 1 pixel per class, K = 4: out = (((0 + x0 w0) + x1 w1) + x2 w2) + x3 w3 + b at the class columns
+    K, C = 4, 3
+    x = np.arange(1, 1 + 3 * K, dtype=np.float32).reshape(1, 1, 3, K)
+    w = np.arange(K * 3 * C, dtype=np.float32).reshape(K, 3 * C) / 8
+    b = np.arange(3 * C, dtype=np.float32) / 2
+    lab = np.array([[[0, 2, 5]]], np.int32)  # 5: out of range -> zeros
+    out = oracle.vertex_pred_compact(x, w, b, lab)
+    for px, l in enumerate([0, 2]):
+        want = (x[0, 0, px] @ w[:, 3 * l:3 * l + 3]) + b[3 * l:3 * l + 3]  # small integers / 8: exact
+        np.testing.assert_array_equal(out[0, 0, px], want)
+    assert not out[0, 0, 2].any()
