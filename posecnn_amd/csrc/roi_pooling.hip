@@ -265,19 +265,23 @@ __global__ void __launch_bounds__(1024) k_roi_prep(const float* __restrict__ roi
 // for every masked tile pixel, add the top gradient of each channel whose
 // argmax names that pixel to a register accumulator (cu.cc:219-224) — in
 // list order, so the fp32 sums are bit-equal to the reference's.
-constexpr int kBTH = 2, kBTW = 4, kBPix = kBTH * kBTW;
+#ifndef PCNN_RBW_NARROW
+#define PCNN_RBW_NARROW 8192
+#endif
 constexpr int kBWaves = 1;  // one wave per workgroup: a tile's channel chunks land on different CUs
 constexpr int kBChunk = 128 * kBWaves;  // channels per workgroup
 constexpr int kBGroup = 16;             // RoIs expanded per list round (<= 16 * 49 entries)
 constexpr int kBCap = kBGroup * 49;
 constexpr int kBBatch = 8;              // entries per fetch (two fetches in flight per wave)
 
+template <int kBTH, int kBTW>
 __global__ void __launch_bounds__(64 * kBWaves) k_roi_bwd_ent(const float* __restrict__ top_diff,
                                                                const int32_t* __restrict__ argmax, int B, int H, int W,
                                                                int C, const int32_t* __restrict__ geo,
                                                                const int32_t* __restrict__ lo,
                                                                const int32_t* __restrict__ hi, int PH, int PW,
                                                                float* __restrict__ bottom) {
+  constexpr int kBPix = kBTH * kBTW;
   __shared__ int2 ent[kBCap];  // element offset ((r*PH+ph)*PW+pw)*C, pixel mask
   __shared__ int sh_total;
   const int tiles_w = (W + kBTW - 1) / kBTW, tiles_h = (H + kBTH - 1) / kBTH;
@@ -549,14 +553,24 @@ extern "C" int pcnn_roi_pool_bwd(const float* top_diff, const int32_t* argmax, i
   int32_t* geo = cv.take<int32_t>((size_t)(R_cap > 0 ? R_cap : 1) * 8);
   hipLaunchKernelGGL(k_roi_prep, dim3(1), dim3(1024), 0, st, rois, R_cap, roi_stride, num_rois_dev, B,
                      spatial_scale, pooled_h, pooled_w, geo, lo, hi);
-  const bool vec = layout == 0 && !pool_channel && C % 2 == 0 && pooled_h * kBTH <= 32 && pooled_w * kBTW <= 32 &&
+  // tile shape: 2x4 pixels, or 1x4 when 2x4 tiles would leave the chip short
+  // of workgroups (conv5_3 at 30x40: 4800 -> 9600 workgroups, measured
+  // 64 -> 50 us; conv4_3 at 60x80 keeps 2x4: 77 vs 88 us for 1x4)
+  const int nchunk = (C + kBChunk - 1) / kBChunk;
+  const long wg24 = (long)B * ((H + 1) / 2) * ((W + 3) / 4) * nchunk;
+  const bool narrow = wg24 < PCNN_RBW_NARROW;
+  const int tbh = narrow ? 1 : 2, tbw = 4;
+  const bool vec = layout == 0 && !pool_channel && C % 2 == 0 && pooled_h * tbh <= 32 && pooled_w * tbw <= 32 &&
                    (long)H * W * C < (1l << 30) && (long)R_cap * pooled_h * pooled_w * C < (1l << 29) &&
                    (((uintptr_t)top_diff | (uintptr_t)argmax | (uintptr_t)bottom_diff) & 7) == 0;
   if (vec) {
-    const int tiles = ((H + kBTH - 1) / kBTH) * ((W + kBTW - 1) / kBTW);
-    const int nchunk = (C + kBChunk - 1) / kBChunk;
-    hipLaunchKernelGGL(k_roi_bwd_ent, dim3(B * tiles * nchunk), dim3(64 * kBWaves), 0, st, top_diff, argmax, B, H, W, C,
-                       geo, lo, hi, pooled_h, pooled_w, bottom_diff);
+    const int tiles = ((H + tbh - 1) / tbh) * ((W + tbw - 1) / tbw);
+    if (narrow)
+      hipLaunchKernelGGL((k_roi_bwd_ent<1, 4>), dim3(B * tiles * nchunk), dim3(64 * kBWaves), 0, st, top_diff, argmax,
+                         B, H, W, C, geo, lo, hi, pooled_h, pooled_w, bottom_diff);
+    else
+      hipLaunchKernelGGL((k_roi_bwd_ent<2, 4>), dim3(B * tiles * nchunk), dim3(64 * kBWaves), 0, st, top_diff, argmax,
+                         B, H, W, C, geo, lo, hi, pooled_h, pooled_w, bottom_diff);
   } else {
     if (hipMemsetAsync(bottom_diff, 0, (size_t)B * H * W * C * sizeof(float), st) != hipSuccess) return PCNN_EHIP;
     const long npix = (long)B * H * W;
