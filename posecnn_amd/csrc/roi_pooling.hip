@@ -82,9 +82,37 @@ __device__ __forceinline__ void upd(float v, int idx, float& m, int& a) {
   if (v > m) { m = v; a = idx; }
 }
 
-// NHWC, all channels, C % 4 == 0: block (roi, bin), lane -> 4 channels.
-// ACC: top += pooled (the pool5 + pool4 sum of vgg16_convs.py:184 produced in
-// place by the second pool; the argmax of each map is still written).
+// XCD-aware (row, bin) of a forward workgroup.  Workgroups are dealt
+// round-robin to the 8 XCDs, each with its own L2.  Rows go to the XCDs in
+// runs of kRun = 9 (one object's box and its 8 jitters in train mode,
+// cu.cc:469-554), with a run's bins consecutive, so a RoI's feature window is
+// fetched into one L2 and re-read there by its jittered neighbours instead of
+// by all eight XCDs.  Same box, B = 8 bench RoIs: the pool pair 94.6 -> 60 us
+// (PCNN_ROI_XCD=0 is the plain row-fastest order, kept for A/B).
+#ifndef PCNN_ROI_XCD
+#define PCNN_ROI_XCD 1
+#endif
+constexpr int kXcds = 8;
+constexpr int kRun = 9;
+__device__ __forceinline__ bool fwd_item(int R, int nbins, int& r, int& bin) {
+  const int id = blockIdx.x;
+#if PCNN_ROI_XCD
+  const int x = id % kXcds, local = id / kXcds;
+  const int lr = local / nbins;
+  bin = local % nbins;
+  r = ((lr / kRun) * kXcds + x) * kRun + lr % kRun;
+#else
+  const int rows = gridDim.x / nbins;
+  r = id % rows;
+  bin = id / rows;
+#endif
+  return r < R;
+}
+// 1-D grid: whole runs on every XCD
+static inline unsigned fwd_grid(int R_cap, int nbins) {
+  return (unsigned)(kXcds * ((R_cap + kXcds * kRun - 1) / (kXcds * kRun)) * kRun * nbins);
+}
+
 // Max / argmax of one bin over lane channels c..c+3 (cu.cc:45-97): bin
 // bounds as bin_bounds, strict > first max in raster order, empty bin (or a
 // RoI batch index outside [0, B)) -> 0 / -1.
@@ -127,8 +155,8 @@ __global__ void __launch_bounds__(128) k_roi_fwd_nhwc4(const float* __restrict__
                                                         const float* __restrict__ rois, int R_cap, int stride,
                                                         const int32_t* __restrict__ num_rois_dev, float scale, int PH,
                                                         int PW, float* __restrict__ top, int32_t* __restrict__ argmax) {
-  const int r = blockIdx.x, bin = blockIdx.y;
-  if (r >= rows_of(num_rois_dev, R_cap)) return;
+  int r, bin;
+  if (!fwd_item(rows_of(num_rois_dev, R_cap), PH * PW, r, bin)) return;
   const int ph = bin / PW, pw = bin % PW;
   const RoiGeo g = roi_geo(rois, r, stride, scale, PH, PW);
   float* to = top + (((size_t)r * PH + ph) * PW + pw) * C;
@@ -159,8 +187,8 @@ __global__ void __launch_bounds__(128) k_roi_fwd_pair_nhwc4(const float* __restr
                                                              const int32_t* __restrict__ num_rois_dev, int PH, int PW,
                                                              float* __restrict__ top, int32_t* __restrict__ arg_a,
                                                              int32_t* __restrict__ arg_b) {
-  const int r = blockIdx.x, bin = blockIdx.y;
-  if (r >= rows_of(num_rois_dev, R_cap)) return;
+  int r, bin;
+  if (!fwd_item(rows_of(num_rois_dev, R_cap), PH * PW, r, bin)) return;
   const int ph = bin / PW, pw = bin % PW;
   const RoiGeo ga = roi_geo(rois, r, stride, scale_a, PH, PW);
   const RoiGeo gb = roi_geo(rois, r, stride, scale_b, PH, PW);
@@ -481,10 +509,10 @@ static int roi_pool_fwd(const float* data, int B, int H, int W, int C, int layou
   if (vec) {
     const int threads = C / 4 >= 128 ? 128 : ((C / 4 + 63) / 64) * 64;
     if (acc)
-      hipLaunchKernelGGL(k_roi_fwd_nhwc4<true>, dim3(R_cap, pooled_h * pooled_w), dim3(threads), 0, st, data, B, H,
+      hipLaunchKernelGGL(k_roi_fwd_nhwc4<true>, dim3(fwd_grid(R_cap, pooled_h * pooled_w)), dim3(threads), 0, st, data, B, H,
                          W, C, rois, R_cap, roi_stride, num_rois_dev, spatial_scale, pooled_h, pooled_w, top, argmax);
     else
-      hipLaunchKernelGGL(k_roi_fwd_nhwc4<false>, dim3(R_cap, pooled_h * pooled_w), dim3(threads), 0, st, data, B, H,
+      hipLaunchKernelGGL(k_roi_fwd_nhwc4<false>, dim3(fwd_grid(R_cap, pooled_h * pooled_w)), dim3(threads), 0, st, data, B, H,
                          W, C, rois, R_cap, roi_stride, num_rois_dev, spatial_scale, pooled_h, pooled_w, top, argmax);
   } else {
     const long n = (long)R_cap * pooled_h * pooled_w * (pool_channel ? 1 : C);
@@ -525,7 +553,7 @@ extern "C" int pcnn_roi_pool_fwd_pair(const float* data_a, int Ha, int Wa, float
                  ((uintptr_t)argmax_b)) & 15) == 0);
   if (R_cap == 0) return PCNN_OK;
   const int threads = C / 4 >= 128 ? 128 : ((C / 4 + 63) / 64) * 64;
-  hipLaunchKernelGGL(k_roi_fwd_pair_nhwc4, dim3(R_cap, pooled_h * pooled_w), dim3(threads), 0, (hipStream_t)stream,
+  hipLaunchKernelGGL(k_roi_fwd_pair_nhwc4, dim3(fwd_grid(R_cap, pooled_h * pooled_w)), dim3(threads), 0, (hipStream_t)stream,
                      data_a, Ha, Wa, scale_a, data_b, Hb, Wb, scale_b, B, C, rois, R_cap, roi_stride, num_rois_dev,
                      pooled_h, pooled_w, top_sum, argmax_a, argmax_b);
   PCNN_CHECK_LAUNCH();

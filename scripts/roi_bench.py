@@ -38,6 +38,7 @@ d4, d5 = torch.empty_like(c4), torch.empty_like(c5)
 cases = [
     ("fwd_conv5", lambda: rp.roi_pool(c5, box, 7, 7, 1 / 16, 0, num_rois=nr, out=(top, a5))),
     ("fwd_conv4_acc", lambda: rp.roi_pool(c4, box, 7, 7, 1 / 8, 0, num_rois=nr, out=(top, a4), accumulate=True)),
+    ("fwd_pair", lambda: rp.roi_pool_pair(c5, 1 / 16, c4, 1 / 8, box, 7, 7, num_rois=nr, out=(top, a5, a4))),
     ("bwd_conv5", lambda: rp.roi_pool_grad(c5, box, a5, gd, 7, 7, 1 / 16, 0, num_rois=nr, out=d5)),
     ("bwd_conv4", lambda: rp.roi_pool_grad(c4, box, a4, gd, 7, 7, 1 / 8, 0, num_rois=nr, out=d4)),
 ]
