@@ -307,10 +307,9 @@ def test_gemm_device_dims_split(hip, prec):
     np.testing.assert_allclose(C2.cpu().numpy(), ref2, **(dict(rtol=2e-5, atol=5e-4) if prec == 0 else _gemm_tol(1, 77)))
 
 
-def test_gemm_weight_grad_xcd_blocks(hip):
-    """Unsplit x3 grid with mt % 2 == 0 and nt % 4 == 0 (the fc6 / fc7 dW
-    form: C = A^T B over a device-side row count): tiles are taken as one 2-D
-    block per XCD (k_gemm_x3 xblk).  16 x 8 tiles of 256, K = 405 rows of 1152."""
+def test_gemm_weight_grad_unsplit(hip):
+    """Unsplit x3 persistent grid in the fc6 / fc7 dW form: C = A^T B over a
+    device-side row count, 16 x 8 tiles of 256, K = 405 rows of 1152."""
     rng = np.random.default_rng(9)
     R, M, N = 1152, 4096, 2048
     A = rng.normal(size=(R, M)).astype(np.float32)
