@@ -293,6 +293,9 @@ __global__ void __launch_bounds__(1024) k_roi_prep(const float* __restrict__ roi
 // for every masked tile pixel, add the top gradient of each channel whose
 // argmax names that pixel to a register accumulator (cu.cc:219-224) — in
 // list order, so the fp32 sums are bit-equal to the reference's.
+#ifndef PCNN_RBW_XCD
+#define PCNN_RBW_XCD 1
+#endif
 #ifndef PCNN_RBW_NARROW
 #define PCNN_RBW_NARROW 8192
 #endif
@@ -314,7 +317,15 @@ __global__ void __launch_bounds__(64 * kBWaves) k_roi_bwd_ent(const float* __res
   __shared__ int sh_total;
   const int tiles_w = (W + kBTW - 1) / kBTW, tiles_h = (H + kBTH - 1) / kBTH;
   const int nchunk = (C + kBChunk - 1) / kBChunk;
+#if PCNN_RBW_XCD
+  // XCD-aware: XCD x takes the contiguous item range [x*ipx, (x+1)*ipx), so
+  // neighbouring tiles, which list the same RoI bins, read them through one L2
+  const int ipx = (int)((gridDim.x + 7) / 8);
+  int id = (int)(blockIdx.x % 8) * ipx + (int)(blockIdx.x / 8);
+#else
   int id = blockIdx.x;
+#endif
+  if (id >= B * tiles_w * tiles_h * nchunk) return;  // grid padded to a multiple of 8
   const int chunk = id % nchunk;
   id /= nchunk;
   const int t = id % (tiles_w * tiles_h), b = id / (tiles_w * tiles_h);
@@ -593,11 +604,12 @@ extern "C" int pcnn_roi_pool_bwd(const float* top_diff, const int32_t* argmax, i
                    (((uintptr_t)top_diff | (uintptr_t)argmax | (uintptr_t)bottom_diff) & 7) == 0;
   if (vec) {
     const int tiles = ((H + tbh - 1) / tbh) * ((W + tbw - 1) / tbw);
+    const unsigned nwg = (unsigned)((B * tiles * nchunk + 7) / 8 * 8);
     if (narrow)
-      hipLaunchKernelGGL((k_roi_bwd_ent<1, 4>), dim3(B * tiles * nchunk), dim3(64 * kBWaves), 0, st, top_diff, argmax,
+      hipLaunchKernelGGL((k_roi_bwd_ent<1, 4>), dim3(nwg), dim3(64 * kBWaves), 0, st, top_diff, argmax,
                          B, H, W, C, geo, lo, hi, pooled_h, pooled_w, bottom_diff);
     else
-      hipLaunchKernelGGL((k_roi_bwd_ent<2, 4>), dim3(B * tiles * nchunk), dim3(64 * kBWaves), 0, st, top_diff, argmax,
+      hipLaunchKernelGGL((k_roi_bwd_ent<2, 4>), dim3(nwg), dim3(64 * kBWaves), 0, st, top_diff, argmax,
                          B, H, W, C, geo, lo, hi, pooled_h, pooled_w, bottom_diff);
   } else {
     if (hipMemsetAsync(bottom_diff, 0, (size_t)B * H * W * C * sizeof(float), st) != hipSuccess) return PCNN_EHIP;
