@@ -7,8 +7,10 @@ hough_voting_gpu (skip 10, single instance, 9 jittered RoIs per max) ->
 roi_pool x2 (conv5_3 1/16, conv4_3 1/8) -> fc6/fc7/fc8 -> tanh * weight ->
 l2_normalize -> ADD loss (margin 0.01) -> backward through loss, FC and both
 RoI pools.  Weak scaling: every rank processes B images of the global batch
-B*N (index_size = 128 / (B*N) as the reference computes it), with an RCCL
-all-gather of the detected RoIs/poses and an all-reduce of the loss.
+B*N (index_size = 128 / (B*N) as the reference computes it).  N > 1 runs the
+step's RCCL collectives inside the timed region: the row-count and loss
+all-reduces and the row-block reduction of the fc6/fc7/fc8 weight gradients
+(all-to-all of the layer inputs + all-gather of dY, exchange.GradShard).
 
 A step = one pass over one batch; inputs are resident in HBM before timing.
 Prints ONE JSON line (rank 0).  --workload vote_roi times configs[1]
@@ -41,6 +43,8 @@ def parse():
     p.add_argument("--no-graph", action="store_true", help="time eager launches instead of a HIP graph")
     p.add_argument("--precision", type=int, choices=[0, 1], default=1,
                    help="FC GEMMs: 1 = split-bf16 x3 MFMA (fp32-class), 0 = fp32 MFMA")
+    p.add_argument("--no-fp32-leg", action="store_true",
+                   help="skip the extra fp32-MFMA (precision 0) timing reported beside the main line")
     return p.parse_args()
 
 
@@ -100,9 +104,9 @@ def main():
                                              out=hout.get("o"))
             hout["o"] = o
             nr = o["num_rois"][1:2]
-            pool["p5"] = rp.roi_pool(inputs["conv5"], o["box"], 7, 7, 1.0 / 16, 0, num_rois=nr,
+            pool["p5"] = rp.roi_pool(inputs["conv5"], o["box"], 7, 7, 1.0 / 16, 0, num_rois=nr, batch_base=rank * B,
                                      out=pool.get("p5"))
-            pool["p4"] = rp.roi_pool(inputs["conv4"], o["box"], 7, 7, 1.0 / 8, 0, num_rois=nr,
+            pool["p4"] = rp.roi_pool(inputs["conv4"], o["box"], 7, 7, 1.0 / 8, 0, num_rois=nr, batch_base=rank * B,
                                      out=pool.get("p4"))
         step = None
 
@@ -178,6 +182,20 @@ def main():
         modes["hipgraph"] = measure(graph_replay)
     modes["eager"] = measure(run)
     mode = min(modes, key=modes.get)
+    # the same step with the FC GEMMs on exact fp32 MFMA (precision 0), eager,
+    # reported beside the line (the split-bf16 x3 GEMMs are fp32-class, not
+    # fp32-rounded; the reference runs these layers as fp32 matmuls)
+    fp32_leg = None
+    if full and world == 1 and args.precision == 1 and not args.no_fp32_leg:
+        step0 = PoseStep(B, H, W, C, dev, is_train=1, skip_pixels=10, global_batch=gB, batch_base=rank * B,
+                         dist=dist, precision=0, weights=step.weights)
+        run0 = lambda: step0.step(inputs)
+        run0()
+        t0_ = measure(run0)
+        fp32_leg = {"value": round(gB * args.steps / t0_, 2), "unit": "frames/s",
+                    "ms_per_step": round(t0_ / args.steps * 1e3, 4), "fc_gemm": "fp32 MFMA (k_gemm_f32, 32x32x2f32)",
+                    "timing": "eager"}
+        del step0
     elapsed = modes[mode]
     frames = gB * args.steps
     value = frames / elapsed
@@ -213,7 +231,7 @@ def main():
     else:
         roof = roof_vote
     # HBM traffic of the same launches from the committed rocprofv3 FETCH_SIZE /
-    # WRITE_SIZE passes (scripts/gpu_pmc.sh -> scripts/pmc_traffic.py)
+    # WRITE_SIZE passes (scripts/gpu.sh pmc -> scripts/pmc_traffic.py)
     pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(pmc_path):
         try:
@@ -249,7 +267,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f32",
+            "dtype": "f32 (FC GEMMs split-bf16x3 MFMA, fp32 accumulate)" if args.precision == 1 else "f32",
             "data": "synthetic (seeded label/vertex maps per minibatch.py:517-575; random conv4_3/conv5_3; "
                     "random-init FC weights)",
             "config": {
@@ -259,7 +277,8 @@ def main():
                 "global_batch": gB, "per_rank_batch": B, "height": H, "width": W, "num_classes": C,
                 "skip_pixels": 10, "index_size": 128 // gB, "roi_rows_rank0": nrows,
                 "fc_gemm": "split-bf16x3 MFMA, fp32 accumulate" if args.precision == 1 else "fp32 MFMA",
-                "parallelism": f"image-shard x{world} (RCCL all-gather of RoIs/poses)" if world > 1 else "single",
+                "parallelism": (f"image-shard x{world} (RCCL: row-count/loss all-reduce, fc weight-gradient "
+                                f"row blocks via all-to-all + all-gather)") if world > 1 else "single",
             },
             "roofline": roof,
             "roofline_vote": roof_vote,
@@ -267,6 +286,7 @@ def main():
             "timing": mode,
             "timing_ms_per_step": {k: round(v / args.steps * 1e3, 4) for k, v in modes.items()},
             "cpu_baseline": cpu,
+            "fp32_mfma_step": fp32_leg,
         }
         print(json.dumps(out), flush=True)
     if dist is not None:

@@ -109,21 +109,24 @@ int pcnn_hough_voting_diag(const void* workspace, int B, int H, int W, int C, in
  *  layout 1 = NCHW data (B,C,H,W), output (R,Cout,PH,PW)  [my_tools _RoIPooling]
  *  rois (R_cap, roi_stride) rows [b, cls, x1, y1, x2, y2, ...] (roi_stride >= 6), or
  *       with roi_stride == 5 rows [b, x1, y1, x2, y2] (pth API, class column absent)
+ *  batch_base: subtracted from the rows' batch column to index `data` (an
+ *       image-sharded rank holds images [batch_base, batch_base + B) of the
+ *       global batch and the Hough rows carry the global index; 0 otherwise)
  *  num_rois_dev: optional device int; when non-NULL the row count is
  *       min(*num_rois_dev, R_cap) (rows beyond are not touched)
  *  argmax: flat index within the image, (h*W + w)*C + c (NHWC) or (c*H + h)*W + w (NCHW)
  * ------------------------------------------------------------------------- */
 int pcnn_roi_pool_fwd(const float* data, int B, int H, int W, int C, int layout, const float* rois, int R_cap,
-                      int roi_stride, const int32_t* num_rois_dev, float spatial_scale, int pooled_h, int pooled_w,
+                      int roi_stride, int batch_base, const int32_t* num_rois_dev, float spatial_scale, int pooled_h, int pooled_w,
                       int pool_channel, float* top, int32_t* argmax, void* stream);
 
 /* As pcnn_roi_pool_fwd but top += pooled (argmax is written as usual): the
  * second pool of vgg16_convs.py:178-184 produces pool5 + pool4 in place, so
  * the fc6 contraction reads one operand.  Same sum as tf.add(pool5, pool4). */
 int pcnn_roi_pool_fwd_accumulate(const float* data, int B, int H, int W, int C, int layout, const float* rois,
-                                 int R_cap, int roi_stride, const int32_t* num_rois_dev, float spatial_scale,
-                                 int pooled_h, int pooled_w, int pool_channel, float* top, int32_t* argmax,
-                                 void* stream);
+                                 int R_cap, int roi_stride, int batch_base, const int32_t* num_rois_dev,
+                                 float spatial_scale, int pooled_h, int pooled_w, int pool_channel, float* top,
+                                 int32_t* argmax, void* stream);
 
 /* Both pose-head RoI pools in one pass (vgg16_convs.py:177-184): pool5 on
  * data_a (e.g. conv5_3 at 1/16) and pool4 on data_b (conv4_3 at 1/8), NHWC,
@@ -132,13 +135,13 @@ int pcnn_roi_pool_fwd_accumulate(const float* data, int B, int H, int W, int C, 
  * argmax tensors (R_cap, pooled_h, pooled_w, C). */
 int pcnn_roi_pool_fwd_pair(const float* data_a, int Ha, int Wa, float scale_a, const float* data_b, int Hb, int Wb,
                            float scale_b, int B, int C, const float* rois, int R_cap, int roi_stride,
-                           const int32_t* num_rois_dev, int pooled_h, int pooled_w, float* top_sum,
+                           int batch_base, const int32_t* num_rois_dev, int pooled_h, int pooled_w, float* top_sum,
                            int32_t* argmax_a, int32_t* argmax_b, void* stream);
 
 size_t pcnn_roi_pool_bwd_workspace_size(int B, int R_cap);
 
 int pcnn_roi_pool_bwd(const float* top_diff, const int32_t* argmax, int B, int H, int W, int C, int layout,
-                      const float* rois, int R_cap, int roi_stride, const int32_t* num_rois_dev,
+                      const float* rois, int R_cap, int roi_stride, int batch_base, const int32_t* num_rois_dev,
                       float spatial_scale, int pooled_h, int pooled_w, int pool_channel, float* bottom_diff,
                       void* workspace, size_t workspace_bytes, void* stream);
 

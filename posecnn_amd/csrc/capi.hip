@@ -1,7 +1,7 @@
 // C-ABI housekeeping entry points of libposecnn_hip.so (see include/posecnn_hip.h).
 #include "pcnn_common.h"
 
-extern "C" int pcnn_abi_version(void) { return 1; }
+extern "C" int pcnn_abi_version(void) { return 2; }
 
 extern "C" const char* pcnn_strerror(int code) {
   switch (code) {

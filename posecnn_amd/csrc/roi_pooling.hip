@@ -28,11 +28,14 @@ struct RoiGeo {
   float bin_h, bin_w;
 };
 
-__device__ __forceinline__ RoiGeo roi_geo(const float* __restrict__ rois, int r, int stride, float scale, int PH,
-                                          int PW) {
+// batch_base: the rows' batch column holds the global image index in an
+// image-sharded run (hough emit adds it, hough_common.h); the feature maps
+// hold only this rank's images, so the map index is column - batch_base.
+__device__ __forceinline__ RoiGeo roi_geo(const float* __restrict__ rois, int r, int stride, int batch_base,
+                                          float scale, int PH, int PW) {
   const float* o = rois + (size_t)r * stride;
   RoiGeo g;
-  g.b = (int)o[0];
+  g.b = (int)o[0] - batch_base;
   const int c0 = stride == 5 ? 1 : 2;
   g.cls = stride == 5 ? 0 : (int)o[1];
   g.sw = (int)roundf(o[c0 + 0] * scale);
@@ -153,12 +156,13 @@ __device__ __forceinline__ void bin_max4(const float* __restrict__ data, int B, 
 template <bool ACC>
 __global__ void __launch_bounds__(128) k_roi_fwd_nhwc4(const float* __restrict__ data, int B, int H, int W, int C,
                                                         const float* __restrict__ rois, int R_cap, int stride,
-                                                        const int32_t* __restrict__ num_rois_dev, float scale, int PH,
-                                                        int PW, float* __restrict__ top, int32_t* __restrict__ argmax) {
+                                                        int batch_base, const int32_t* __restrict__ num_rois_dev,
+                                                        float scale, int PH, int PW, float* __restrict__ top,
+                                                        int32_t* __restrict__ argmax) {
   int r, bin;
   if (!fwd_item(rows_of(num_rois_dev, R_cap), PH * PW, r, bin)) return;
   const int ph = bin / PW, pw = bin % PW;
-  const RoiGeo g = roi_geo(rois, r, stride, scale, PH, PW);
+  const RoiGeo g = roi_geo(rois, r, stride, batch_base, scale, PH, PW);
   float* to = top + (((size_t)r * PH + ph) * PW + pw) * C;
   int32_t* ao = argmax + (((size_t)r * PH + ph) * PW + pw) * C;
   for (int c = threadIdx.x * 4; c < C; c += blockDim.x * 4) {
@@ -184,14 +188,14 @@ __global__ void __launch_bounds__(128) k_roi_fwd_pair_nhwc4(const float* __restr
                                                              float scale_a, const float* __restrict__ data_b, int Hb,
                                                              int Wb, float scale_b, int B, int C,
                                                              const float* __restrict__ rois, int R_cap, int stride,
-                                                             const int32_t* __restrict__ num_rois_dev, int PH, int PW,
-                                                             float* __restrict__ top, int32_t* __restrict__ arg_a,
-                                                             int32_t* __restrict__ arg_b) {
+                                                             int batch_base, const int32_t* __restrict__ num_rois_dev,
+                                                             int PH, int PW, float* __restrict__ top,
+                                                             int32_t* __restrict__ arg_a, int32_t* __restrict__ arg_b) {
   int r, bin;
   if (!fwd_item(rows_of(num_rois_dev, R_cap), PH * PW, r, bin)) return;
   const int ph = bin / PW, pw = bin % PW;
-  const RoiGeo ga = roi_geo(rois, r, stride, scale_a, PH, PW);
-  const RoiGeo gb = roi_geo(rois, r, stride, scale_b, PH, PW);
+  const RoiGeo ga = roi_geo(rois, r, stride, batch_base, scale_a, PH, PW);
+  const RoiGeo gb = roi_geo(rois, r, stride, batch_base, scale_b, PH, PW);
   const size_t o = (((size_t)r * PH + ph) * PW + pw) * C;
   for (int c = threadIdx.x * 4; c < C; c += blockDim.x * 4) {
     float4 ma, mb;
@@ -206,7 +210,7 @@ __global__ void __launch_bounds__(128) k_roi_fwd_pair_nhwc4(const float* __restr
 
 // generic: one thread per output element (NCHW layout, pool_channel, C % 4 != 0)
 __global__ void k_roi_fwd_generic(const float* __restrict__ data, int B, int H, int W, int C, int layout,
-                                  const float* __restrict__ rois, int R_cap, int stride,
+                                  const float* __restrict__ rois, int R_cap, int stride, int batch_base,
                                   const int32_t* __restrict__ num_rois_dev, float scale, int PH, int PW,
                                   int pool_channel, int acc, float* __restrict__ top, int32_t* __restrict__ argmax) {
   const int R = rows_of(num_rois_dev, R_cap);
@@ -225,7 +229,7 @@ __global__ void k_roi_fwd_generic(const float* __restrict__ data, int B, int H, 
       ph = (int)(t % PH); t /= PH;
       c = (int)(t % Co); r = (int)(t / Co);
     }
-    const RoiGeo g = roi_geo(rois, r, stride, scale, PH, PW);
+    const RoiGeo g = roi_geo(rois, r, stride, batch_base, scale, PH, PW);
     const bool bad = g.b < 0 || g.b >= B;
     const int ch = pool_channel ? g.cls : c;
     int hs, he, ws, we;
@@ -250,8 +254,8 @@ __global__ void k_roi_fwd_generic(const float* __restrict__ data, int B, int H, 
 // RoI geometry once per row + per-image RoI index ranges.
 // geo[r] = {b, cls, sw, sh, ew, eh, bits(bin_h), bits(bin_w)}
 __global__ void __launch_bounds__(1024) k_roi_prep(const float* __restrict__ rois, int R_cap, int stride,
-                                                    const int32_t* __restrict__ num_rois_dev, int B, float scale,
-                                                    int PH, int PW, int32_t* __restrict__ geo,
+                                                    int batch_base, const int32_t* __restrict__ num_rois_dev, int B,
+                                                    float scale, int PH, int PW, int32_t* __restrict__ geo,
                                                     int32_t* __restrict__ lo, int32_t* __restrict__ hi) {
   __shared__ int slo[1024], shi[1024];
   const int R = rows_of(num_rois_dev, R_cap);
@@ -262,7 +266,7 @@ __global__ void __launch_bounds__(1024) k_roi_prep(const float* __restrict__ roi
   }
   __syncthreads();
   for (int r = threadIdx.x; r < R; r += blockDim.x) {
-    const RoiGeo g = roi_geo(rois, r, stride, scale, PH, PW);
+    const RoiGeo g = roi_geo(rois, r, stride, batch_base, scale, PH, PW);
     int32_t* o = geo + (size_t)r * 8;
     o[0] = g.b; o[1] = g.cls; o[2] = g.sw; o[3] = g.sh; o[4] = g.ew; o[5] = g.eh;
     o[6] = __float_as_int(g.bin_h);
@@ -507,8 +511,9 @@ __global__ void k_roi_bwd_generic(const float* __restrict__ top_diff, const int3
 }  // namespace
 
 static int roi_pool_fwd(const float* data, int B, int H, int W, int C, int layout, const float* rois, int R_cap,
-                        int roi_stride, const int32_t* num_rois_dev, float spatial_scale, int pooled_h, int pooled_w,
-                        int pool_channel, int acc, float* top, int32_t* argmax, void* stream) {
+                        int roi_stride, int batch_base, const int32_t* num_rois_dev, float spatial_scale,
+                        int pooled_h, int pooled_w, int pool_channel, int acc, float* top, int32_t* argmax,
+                        void* stream) {
   PCNN_REQUIRE(data && rois && top && argmax && B > 0 && H > 0 && W > 0 && C > 0 && R_cap >= 0);
   PCNN_REQUIRE(pooled_h > 0 && pooled_w > 0 && (layout == 0 || layout == 1));
   PCNN_REQUIRE(roi_stride >= 6 || (roi_stride == 5 && !pool_channel));
@@ -521,40 +526,45 @@ static int roi_pool_fwd(const float* data, int B, int H, int W, int C, int layou
     const int threads = C / 4 >= 128 ? 128 : ((C / 4 + 63) / 64) * 64;
     if (acc)
       hipLaunchKernelGGL(k_roi_fwd_nhwc4<true>, dim3(fwd_grid(R_cap, pooled_h * pooled_w)), dim3(threads), 0, st, data, B, H,
-                         W, C, rois, R_cap, roi_stride, num_rois_dev, spatial_scale, pooled_h, pooled_w, top, argmax);
+                         W, C, rois, R_cap, roi_stride, batch_base, num_rois_dev, spatial_scale, pooled_h, pooled_w, top,
+                         argmax);
     else
       hipLaunchKernelGGL(k_roi_fwd_nhwc4<false>, dim3(fwd_grid(R_cap, pooled_h * pooled_w)), dim3(threads), 0, st, data, B, H,
-                         W, C, rois, R_cap, roi_stride, num_rois_dev, spatial_scale, pooled_h, pooled_w, top, argmax);
+                         W, C, rois, R_cap, roi_stride, batch_base, num_rois_dev, spatial_scale, pooled_h, pooled_w, top,
+                         argmax);
   } else {
     const long n = (long)R_cap * pooled_h * pooled_w * (pool_channel ? 1 : C);
     const int blocks = (int)((n + 255) / 256 < 8192 ? (n + 255) / 256 : 8192);
     hipLaunchKernelGGL(k_roi_fwd_generic, dim3(blocks), dim3(256), 0, st, data, B, H, W, C, layout, rois, R_cap,
-                       roi_stride, num_rois_dev, spatial_scale, pooled_h, pooled_w, pool_channel, acc, top, argmax);
+                       roi_stride, batch_base, num_rois_dev, spatial_scale, pooled_h, pooled_w, pool_channel, acc, top,
+                       argmax);
   }
   PCNN_CHECK_LAUNCH();
   return PCNN_OK;
 }
 
 extern "C" int pcnn_roi_pool_fwd(const float* data, int B, int H, int W, int C, int layout, const float* rois,
-                                 int R_cap, int roi_stride, const int32_t* num_rois_dev, float spatial_scale,
-                                 int pooled_h, int pooled_w, int pool_channel, float* top, int32_t* argmax,
-                                 void* stream) {
-  return roi_pool_fwd(data, B, H, W, C, layout, rois, R_cap, roi_stride, num_rois_dev, spatial_scale, pooled_h,
+                                 int R_cap, int roi_stride, int batch_base, const int32_t* num_rois_dev,
+                                 float spatial_scale, int pooled_h, int pooled_w, int pool_channel, float* top,
+                                 int32_t* argmax, void* stream) {
+  return roi_pool_fwd(data, B, H, W, C, layout, rois, R_cap, roi_stride, batch_base, num_rois_dev, spatial_scale,
+                      pooled_h,
                       pooled_w, pool_channel, 0, top, argmax, stream);
 }
 
 extern "C" int pcnn_roi_pool_fwd_accumulate(const float* data, int B, int H, int W, int C, int layout,
-                                            const float* rois, int R_cap, int roi_stride,
+                                            const float* rois, int R_cap, int roi_stride, int batch_base,
                                             const int32_t* num_rois_dev, float spatial_scale, int pooled_h,
                                             int pooled_w, int pool_channel, float* top, int32_t* argmax,
                                             void* stream) {
-  return roi_pool_fwd(data, B, H, W, C, layout, rois, R_cap, roi_stride, num_rois_dev, spatial_scale, pooled_h,
+  return roi_pool_fwd(data, B, H, W, C, layout, rois, R_cap, roi_stride, batch_base, num_rois_dev, spatial_scale,
+                      pooled_h,
                       pooled_w, pool_channel, 1, top, argmax, stream);
 }
 
 extern "C" int pcnn_roi_pool_fwd_pair(const float* data_a, int Ha, int Wa, float scale_a, const float* data_b, int Hb,
                                       int Wb, float scale_b, int B, int C, const float* rois, int R_cap, int roi_stride,
-                                      const int32_t* num_rois_dev, int pooled_h, int pooled_w, float* top_sum,
+                                      int batch_base, const int32_t* num_rois_dev, int pooled_h, int pooled_w, float* top_sum,
                                       int32_t* argmax_a, int32_t* argmax_b, void* stream) {
   PCNN_REQUIRE(data_a && data_b && rois && top_sum && argmax_a && argmax_b && B > 0 && C > 0 && C % 4 == 0);
   PCNN_REQUIRE(Ha > 0 && Wa > 0 && Hb > 0 && Wb > 0 && pooled_h > 0 && pooled_w > 0 && R_cap >= 0);
@@ -565,7 +575,7 @@ extern "C" int pcnn_roi_pool_fwd_pair(const float* data_a, int Ha, int Wa, float
   if (R_cap == 0) return PCNN_OK;
   const int threads = C / 4 >= 128 ? 128 : ((C / 4 + 63) / 64) * 64;
   hipLaunchKernelGGL(k_roi_fwd_pair_nhwc4, dim3(fwd_grid(R_cap, pooled_h * pooled_w)), dim3(threads), 0, (hipStream_t)stream,
-                     data_a, Ha, Wa, scale_a, data_b, Hb, Wb, scale_b, B, C, rois, R_cap, roi_stride, num_rois_dev,
+                     data_a, Ha, Wa, scale_a, data_b, Hb, Wb, scale_b, B, C, rois, R_cap, roi_stride, batch_base, num_rois_dev,
                      pooled_h, pooled_w, top_sum, argmax_a, argmax_b);
   PCNN_CHECK_LAUNCH();
   return PCNN_OK;
@@ -577,9 +587,9 @@ extern "C" size_t pcnn_roi_pool_bwd_workspace_size(int B, int R_cap) {
 }
 
 extern "C" int pcnn_roi_pool_bwd(const float* top_diff, const int32_t* argmax, int B, int H, int W, int C, int layout,
-                                 const float* rois, int R_cap, int roi_stride, const int32_t* num_rois_dev,
-                                 float spatial_scale, int pooled_h, int pooled_w, int pool_channel,
-                                 float* bottom_diff, void* workspace, size_t workspace_bytes, void* stream) {
+                                 const float* rois, int R_cap, int roi_stride, int batch_base,
+                                 const int32_t* num_rois_dev, float spatial_scale, int pooled_h, int pooled_w,
+                                 int pool_channel, float* bottom_diff, void* workspace, size_t workspace_bytes, void* stream) {
   PCNN_REQUIRE(top_diff && argmax && rois && bottom_diff && workspace && B > 0 && H > 0 && W > 0 && C > 0);
   PCNN_REQUIRE(pooled_h > 0 && pooled_w > 0 && (layout == 0 || layout == 1) && R_cap >= 0);
   PCNN_REQUIRE(roi_stride >= 6 || (roi_stride == 5 && !pool_channel));
@@ -590,8 +600,8 @@ extern "C" int pcnn_roi_pool_bwd(const float* top_diff, const int32_t* argmax, i
   int32_t* lo = cv.take<int32_t>(B);
   int32_t* hi = cv.take<int32_t>(B);
   int32_t* geo = cv.take<int32_t>((size_t)(R_cap > 0 ? R_cap : 1) * 8);
-  hipLaunchKernelGGL(k_roi_prep, dim3(1), dim3(1024), 0, st, rois, R_cap, roi_stride, num_rois_dev, B,
-                     spatial_scale, pooled_h, pooled_w, geo, lo, hi);
+  hipLaunchKernelGGL(k_roi_prep, dim3(1), dim3(1024), 0, st, rois, R_cap, roi_stride, batch_base, num_rois_dev,
+                     B, spatial_scale, pooled_h, pooled_w, geo, lo, hi);
   // tile shape: 2x4 pixels, or 1x4 when 2x4 tiles would leave the chip short
   // of workgroups (conv5_3 at 30x40: 4800 -> 9600 workgroups, measured
   // 64 -> 50 us; conv4_3 at 60x80 keeps 2x4: 77 vs 88 us for 1x4)

@@ -11,10 +11,15 @@ be captured in a HIP graph.
 
 Image sharding (one process per GPU): rank r votes on images
 [r*B, (r+1)*B) with index_size = MAX_ROI / global_batch and the batch column
-rebased to the global image index; the detected RoI boxes + initial poses
-and the row counts are all-gathered over RCCL (torch.distributed "nccl"),
-the ADD-loss normaliser is the global row count (so per-rank losses sum to
-the single-device loss) and the loss scalar is all-reduced.
+rebased to the global image index (the RoI pools subtract batch_base again to
+index the rank's own feature maps).  Collectives (RCCL, torch.distributed
+"nccl"): an all-reduce of the row count gives the ADD-loss normaliser (the
+global row count, so per-rank losses sum to the single-device loss); the
+pose-head weight gradients are reduced by row block through their factors
+(posecnn_amd/exchange.py GradShard: rank r ends with rows_r of the global
+dW6/dW7/dW8 and the full bias gradients); the loss scalar is all-reduced.
+`gather_detections()` all-gathers the detected RoIs + initial poses in
+single-device row order (exchange.RoiExchange).
 """
 import torch
 
@@ -23,7 +28,7 @@ from . import pose_head as ph
 from .hough_voting_gpu_layer import hough_voting_gpu_op as hv
 from .roi_pooling_layer import roi_pooling_op as rp
 from .average_distance_loss import average_distance_loss_op as adl
-from .exchange import RoiExchange
+from .exchange import GradShard, RoiExchange
 
 CAP = hv.CAPACITY
 
@@ -70,12 +75,23 @@ class PoseStep:
         self.dy7 = torch.zeros((CAP, units), **f32)
         self.dy6 = torch.zeros((CAP, units), **f32)
         self.dx = torch.zeros((CAP, K6), **f32)
+        self.gshard = None
+        if dist is not None:
+            # rows a rank can emit: B images x index_size maxima x (9 jitters | 1), or the dummy row
+            per_max = 9 if is_train else 1
+            slot = max(1, min(CAP, B * (hv.MAX_ROI // self.global_batch) * per_max))
+            self.gshard = GradShard(dist, slot, [("w6", (K6, units)), ("w7", (units, units)), ("w8", (units, D))],
+                                    device)
         self.grads = self.weights.grads_like()
+        if self.gshard is not None:  # this rank's row block of each weight gradient
+            for k in ("w6", "w7", "w8"):
+                self.grads[k] = self.grads[k][self.gshard.rows(k)].contiguous()
         self.dconv4 = torch.zeros((B, self.h4, self.w4, channels), **f32)
         self.dconv5 = torch.zeros((B, self.h5, self.w5, channels), **f32)
         self.norm_rows = torch.zeros((1,), **i32)
         self.timer = None  # optional {name: [(start_event, end_event), ...]} (bench.py)
-        self.xchg = RoiExchange(dist, CAP, device) if dist is not None else None
+        self.xchg = None  # RoiExchange, built on the first gather_detections()
+        self._pending = {}  # async collectives of the current step
         # weight-gradient branch of the backward (None: everything on the caller's stream)
         self.side_stream = torch.cuda.Stream(device=device) if overlap_weight_grads else None
 
@@ -104,16 +120,32 @@ class PoseStep:
                                                 batch_base=self.batch_base, out=self.hough)
 
     def exchange(self):
-        """RCCL all-gather of the detected RoIs + initial poses (global rows in
-        single-device order, posecnn_amd/exchange.py); global loss normaliser
-        = max(sum of per-rank rows, 1)."""
+        """Global ADD-loss normaliser = max(sum of per-rank rows, 1): an
+        all-reduce of one int (async; the loss kernel waits for it)."""
         h = self.hough
-        if self.xchg is None:  # single device: the loss normaliser is the op's own row count
+        if self.dist is None:  # single device: the loss normaliser is the op's own row count
             self.norm_rows = h["num_rois"][1:2]
             return
-        with self._t("allgather_rois"):
-            _, total = self.xchg(h["box"], h["pose"], h["num_rois"])
-            self.norm_rows.copy_(total.clamp(min=1))
+        with self._t("allreduce_rows"):
+            self.norm_rows.copy_(h["num_rois"][0:1])
+            self._pending["rows"] = self.dist.all_reduce(self.norm_rows, async_op=True)
+
+    def _wait(self, key):
+        w = self._pending.pop(key, None)
+        if w is not None:
+            w.wait()
+
+    def gather_detections(self):
+        """All-gather of the detected RoI boxes + initial poses (RCCL): returns
+        (rows (ws*CAP, 14) = [box(7) | pose(7)], total (1,) int32), the global
+        rows first in single-device order (image-major).  Single device: the
+        op's own rows."""
+        h = self.hough
+        if self.dist is None:
+            return torch.cat([h["box"], h["pose"]], 1), h["num_rois"][0:1]
+        if self.xchg is None:
+            self.xchg = RoiExchange(self.dist, CAP, self.dev)
+        return self.xchg(h["box"], h["pose"], h["num_rois"])
 
     def forward(self, conv4, conv5, points, symmetry):
         h = self.hough
@@ -122,20 +154,29 @@ class PoseStep:
         K6 = 49 * self.Ch
         with self._t("roi_pool_fwd"):  # pool = pool5 + pool4 (vgg16_convs.py:177-184), one pass
             rp.roi_pool_pair(conv5, 1.0 / 16.0, conv4, 1.0 / 8.0, h["box"], 7, 7, num_rois=nr,
-                             out=(self.pool, self.arg5, self.arg4))
+                             out=(self.pool, self.arg5, self.arg4), batch_base=self.batch_base)
         x = self.pool.view(CAP, K6)
+        gs = self.gshard if self.backward else None
+        if gs is not None:  # fc6 input column blocks to their owners (overlaps the forward)
+            gs.send_input("w6", x)
         with self._t("gemm_fc6_fwd"):
             ph.gemm(x, w.w6, self.y6, bias=w.b6, act=1, M_dev=nr, precision=self.prec)
+        if gs is not None:
+            gs.send_input("w7", self.y6)
         with self._t("gemm_fc7_fc8_fwd"):
             ph.gemm(self.y6, w.w7, self.y7, bias=w.b7, act=1, M_dev=nr, precision=self.prec)
+            if gs is not None:
+                gs.send_input("w8", self.y7)
             ph.gemm(self.y7, w.w8, self.y8, bias=w.b8, act=0, M_dev=nr, precision=self.prec)
+        if self.dist is not None:
+            self._wait("rows")
+            self.norm_rows.clamp_(min=1)
         with self._t("head_add_loss_fwd"):
             ph.head_fwd(self.y8, h["weight"], self.t8, self.pred, num_rois=nr)
             adl.average_distance_loss(self.pred, h["target"], h["weight"], points, symmetry, self.margin,
                                       num_rois=nr, loss_norm_rows_dev=self.norm_rows, out=(self.loss, self.diff))
-        if self.dist is not None:
-            with self._t("allreduce_loss"):
-                self.dist.all_reduce(self.loss)
+        if self.dist is not None:  # nothing downstream reads the global loss: joined at the end of the step
+            self._pending["loss"] = self.dist.all_reduce(self.loss, async_op=True)
         return self.loss
 
     def backward_pass(self, conv4, conv5):
@@ -145,46 +186,56 @@ class PoseStep:
         backward) stays on the step's stream; the weight / bias gradients are
         leaves of the graph and run on a side stream that joins at the end, so
         their launches fill the gaps and tails of the chain (HIP-graph branches
-        when captured)."""
+        when captured).  Image-sharded: each layer's dY goes to the all-gather
+        as soon as it exists and the side stream computes this rank's row
+        block of the global weight gradient (GradShard)."""
         h = self.hough
         nr = h["num_rois"][1:2]
         w, g = self.weights, self.grads
         K6 = 49 * self.Ch
         main = torch.cuda.current_stream()
         side = self.side_stream if self.timer is None else None  # per-op timing runs the ops one by one
+        gs = self.gshard
+        x = self.pool.view(CAP, K6)
+
+        def weight_grads(name, X, dY, K_loc, M, N):
+            if side is not None:
+                side.wait_stream(main)
+            if gs is not None:
+                gs.send_grad(name, dY, nr)
+            with torch.cuda.stream(side or main):
+                if gs is not None:
+                    gs.reduce(name, g[name], g["b" + name[1:]], self._gemm, ph.colsum)
+                else:
+                    ph.gemm(X, dY, g[name], a_trans=1, K_dev=nr, M=M, N=N, K=K_loc, precision=self.prec)
+                    ph.colsum(dY, g["b" + name[1:]], M_dev=nr)
+
         with self._t("add_loss_head_bwd"):
             adl.average_distance_loss_grad(self.diff, self.one, num_rois=nr, out=self.dpred)
             ph.head_bwd(self.dpred, self.t8, h["weight"], self.pred, self.dy8, num_rois=nr)
-        if side is not None:
-            side.wait_stream(main)
-        with torch.cuda.stream(side or main), self._t("gemm_fc8_fc7_dw_bias"):  # fc8 weight / bias gradients
-            ph.gemm(self.y7, self.dy8, g["w8"], a_trans=1, K_dev=nr, M=w.units, N=self.D, K=CAP, precision=self.prec)
-            ph.colsum(self.dy8, g["b8"], M_dev=nr)
+        with self._t("gemm_fc8_fc7_dw_bias"):  # fc8 weight / bias gradients
+            weight_grads("w8", self.y7, self.dy8, CAP, w.units, self.D)
         with self._t("gemm_fc8_fc7_dx"):
             ph.gemm(self.dy8, w.w8, self.dy7, b_trans=1, mask=self.y7, M_dev=nr, precision=self.prec)
-        if side is not None:
-            side.wait_stream(main)
-        with torch.cuda.stream(side or main), self._t("gemm_fc8_fc7_dw_bias"):  # fc7 weight / bias gradients
-            ph.gemm(self.y6, self.dy7, g["w7"], a_trans=1, K_dev=nr, M=w.units, N=w.units, K=CAP, precision=self.prec)
-            ph.colsum(self.dy7, g["b7"], M_dev=nr)
+        with self._t("gemm_fc8_fc7_dw_bias"):  # fc7 weight / bias gradients
+            weight_grads("w7", self.y6, self.dy7, CAP, w.units, w.units)
         with self._t("gemm_fc8_fc7_dx"):
             ph.gemm(self.dy7, w.w7, self.dy6, b_trans=1, mask=self.y6, M_dev=nr, precision=self.prec)
-        if side is not None:
-            side.wait_stream(main)
-        x = self.pool.view(CAP, K6)
-        with torch.cuda.stream(side or main):  # fc6 weight / bias gradients (A = pool5 + pool4)
-            with self._t("gemm_fc6_dw"):
-                ph.gemm(x, self.dy6, g["w6"], a_trans=1, K_dev=nr, M=K6, N=w.units, K=CAP, precision=self.prec)
-            with self._t("gemm_fc8_fc7_dw_bias"):
-                ph.colsum(self.dy6, g["b6"], M_dev=nr)
+        with self._t("gemm_fc6_dw"):  # fc6 weight / bias gradients (A = pool5 + pool4)
+            weight_grads("w6", x, self.dy6, CAP, K6, w.units)
         with self._t("gemm_fc6_dx"):
             ph.gemm(self.dy6, w.w6, self.dx, b_trans=1, M_dev=nr, precision=self.prec)
         dxp = self.dx.view(CAP, 7, 7, self.Ch)
         with self._t("roi_pool_bwd"):  # both pools receive d(pool5 + pool4) = dx
-            rp.roi_pool_grad(conv5, h["box"], self.arg5, dxp, 7, 7, 1.0 / 16.0, 0, num_rois=nr, out=self.dconv5)
-            rp.roi_pool_grad(conv4, h["box"], self.arg4, dxp, 7, 7, 1.0 / 8.0, 0, num_rois=nr, out=self.dconv4)
+            rp.roi_pool_grad(conv5, h["box"], self.arg5, dxp, 7, 7, 1.0 / 16.0, 0, num_rois=nr, out=self.dconv5,
+                             batch_base=self.batch_base)
+            rp.roi_pool_grad(conv4, h["box"], self.arg4, dxp, 7, 7, 1.0 / 8.0, 0, num_rois=nr, out=self.dconv4,
+                             batch_base=self.batch_base)
         if side is not None:
             main.wait_stream(side)
+
+    def _gemm(self, A, B, C, **kw):
+        return ph.gemm(A, B, C, precision=self.prec, **kw)
 
     def step(self, inputs):
         self.vote(inputs["label"], inputs["vertex"], inputs["extents"], inputs["meta"], inputs["gt"])
@@ -192,4 +243,5 @@ class PoseStep:
         loss = self.forward(inputs["conv4"], inputs["conv5"], inputs["points"], inputs["symmetry"])
         if self.backward:
             self.backward_pass(inputs["conv4"], inputs["conv5"])
+        self._wait("loss")
         return loss

@@ -6,7 +6,9 @@ roi_pool(data (B,H,W,C), rois (R, >=6), pooled_height, pooled_width,
          spatial_scale, pool_channel) -> (top (R,PH,PW,C or 1), argmax int32)
 roi_pool_grad(data, rois, argmax, grad, ...) -> d data  (roi_pooling_op_grad.py:33-50)
 `num_rois` (optional device int32 scalar tensor) bounds the rows used, for the
-capacity-sized RoI buffers of the fused pose step.
+capacity-sized RoI buffers of the fused pose step.  `batch_base` is subtracted
+from the rows' batch column: an image-sharded rank holds images
+[batch_base, batch_base + B) while the Hough rows carry the global index.
 """
 import torch
 
@@ -14,7 +16,7 @@ from .. import _lib
 
 
 def roi_pool(bottom_data, bottom_rois, pooled_height, pooled_width, spatial_scale, pool_channel=0, name=None,
-             num_rois=None, layout=0, out=None, accumulate=False):
+             num_rois=None, layout=0, out=None, accumulate=False, batch_base=0):
     """accumulate=True: out[0] += pooled (out required), argmax written to out[1]."""
     _lib.require_gpu(bottom_data, bottom_rois)
     if bottom_data.dim() != 4:
@@ -39,15 +41,15 @@ def roi_pool(bottom_data, bottom_rois, pooled_height, pooled_width, spatial_scal
         top, arg = out
     lib = _lib.load()
     fn = lib.pcnn_roi_pool_fwd_accumulate if accumulate else lib.pcnn_roi_pool_fwd
-    rc = fn(_lib.ptr(data), B, H, W, C, layout, _lib.ptr(rois), R, stride,
-                                       _lib.ptr(num_rois), float(spatial_scale), int(pooled_height),
-                                       int(pooled_width), int(pool_channel), _lib.ptr(top), _lib.ptr(arg),
-                                       _lib.stream_ptr())
+    rc = fn(_lib.ptr(data), B, H, W, C, layout, _lib.ptr(rois), R, stride, int(batch_base), _lib.ptr(num_rois),
+            float(spatial_scale), int(pooled_height), int(pooled_width), int(pool_channel), _lib.ptr(top),
+            _lib.ptr(arg), _lib.stream_ptr())
     _lib.check(rc, "roi_pool")
     return top, arg
 
 
-def roi_pool_pair(data_a, scale_a, data_b, scale_b, rois, pooled_height, pooled_width, num_rois=None, out=None):
+def roi_pool_pair(data_a, scale_a, data_b, scale_b, rois, pooled_height, pooled_width, num_rois=None, out=None,
+                  batch_base=0):
     """pool_a + pool_b and both argmax tensors in one pass (vgg16_convs.py:177-184:
     roi_pool(conv5_3, 1/16) + roi_pool(conv4_3, 1/8)); NHWC, all channels.
     Equal to roi_pool(data_a) then roi_pool(data_b, accumulate=True)."""
@@ -68,7 +70,8 @@ def roi_pool_pair(data_a, scale_a, data_b, scale_b, rois, pooled_height, pooled_
                torch.empty(shape, dtype=torch.int32, device=da.device))
     top, arg_a, arg_b = out
     rc = _lib.load().pcnn_roi_pool_fwd_pair(_lib.ptr(da), Ha, Wa, float(scale_a), _lib.ptr(db), Hb, Wb,
-                                            float(scale_b), B, C, _lib.ptr(rois), R, stride, _lib.ptr(num_rois),
+                                            float(scale_b), B, C, _lib.ptr(rois), R, stride, int(batch_base),
+                                            _lib.ptr(num_rois),
                                             int(pooled_height), int(pooled_width), _lib.ptr(top), _lib.ptr(arg_a),
                                             _lib.ptr(arg_b), _lib.stream_ptr())
     _lib.check(rc, "roi_pool_pair")
@@ -76,7 +79,7 @@ def roi_pool_pair(data_a, scale_a, data_b, scale_b, rois, pooled_height, pooled_
 
 
 def roi_pool_grad(bottom_data, bottom_rois, argmax, grad, pooled_height, pooled_width, spatial_scale,
-                  pool_channel=0, name=None, num_rois=None, layout=0, out=None):
+                  pool_channel=0, name=None, num_rois=None, layout=0, out=None, batch_base=0):
     _lib.require_gpu(bottom_data, bottom_rois, argmax, grad)
     rois = bottom_rois.contiguous().float()
     if layout == 0:
@@ -88,7 +91,7 @@ def roi_pool_grad(bottom_data, bottom_rois, argmax, grad, pooled_height, pooled_
     ws = _lib.workspace(lib.pcnn_roi_pool_bwd_workspace_size(B, R), bottom_data.device, "roi_bwd")
     dd = out if out is not None else torch.empty(bottom_data.shape, dtype=torch.float32, device=bottom_data.device)
     rc = lib.pcnn_roi_pool_bwd(_lib.ptr(grad.contiguous()), _lib.ptr(argmax.contiguous()), B, H, W, C, layout,
-                               _lib.ptr(rois), R, stride, _lib.ptr(num_rois), float(spatial_scale),
+                               _lib.ptr(rois), R, stride, int(batch_base), _lib.ptr(num_rois), float(spatial_scale),
                                int(pooled_height), int(pooled_width), int(pool_channel), _lib.ptr(dd),
                                _lib.ptr(ws), ws.numel(), _lib.stream_ptr())
     _lib.check(rc, "roi_pool_grad")

@@ -1,0 +1,72 @@
+#!/bin/bash
+# One parameterised GPU runner (run through gpurun from the repo root):
+#   gpurun --timeout 1200 -- bash scripts/gpu.sh TASK [TASK ...]
+# Tasks run in order, each under its own time limit, and the script stops at
+# the first failure (no retries).  Outputs land under gpurun_out/.
+#   test [PYTEST_ARGS]  GPU parity suite (default: all of tests/ -m gpu)
+#   smoke               __graft_entry__.smoke()
+#   bench               default bench line (configs[2]) + vote_roi (configs[1])
+#   prof                rocprofv3 --kernel-trace --stats of the eager and graph steps
+#   pmc                 FETCH_SIZE / WRITE_SIZE passes -> profiles/pmc_traffic.json
+#   sq                  SQ instruction / stall counters of the eager step (two passes)
+#   ab V1,V2,...        alternating bench of the tree vs scratch/V.so (scripts/build_variant.sh)
+#   micro NAME          scripts/NAME.py microbench (gemm_bench, roi_bench, hough_bench, label_bench, pcie_rate)
+R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
+O=$R/gpurun_out
+mkdir -p $O
+export TMPDIR=/tmp
+prof() {  # prof NAME STEPS WARMUP [bench args] (eager launches, one dispatch per kernel)
+  local n=$1 s=$2 w=$3; shift 3
+  (cd /tmp && timeout -k 10 600 rocprofv3 "${PMC[@]}" --kernel-trace --output-format csv -d $O/$n -o run -- \
+     python3 $R/bench.py --steps $s --warmup $w --no-cpu-baseline "$@" > $O/$n.log 2>&1)
+}
+while [ $# -gt 0 ]; do
+  task=$1; shift
+  cd $R
+  case $task in
+    test)
+      args=(tests)
+      if [ $# -gt 0 ] && [[ $1 != test && $1 != smoke && $1 != bench && $1 != prof && $1 != pmc && $1 != sq && $1 != ab && $1 != micro ]]; then
+        args=($1); shift
+      fi
+      timeout -k 10 900 python -u -m pytest "${args[@]}" -m gpu -x -v --timeout 120 --timeout-method thread \
+        -p no:cacheprovider > $O/t_gpu.log 2>&1 || { echo "test failed"; exit 1; } ;;
+    smoke)
+      timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || exit 1 ;;
+    bench)
+      timeout -k 10 600 python bench.py > $O/bench_full.json 2> $O/bench_full.err || exit 1
+      timeout -k 10 300 python bench.py --workload vote_roi --steps 200 --warmup 20 --no-cpu-baseline \
+        > $O/bench_vr.json 2> $O/bench_vr.err || exit 1 ;;
+    prof)
+      PMC=(--stats)
+      prof prof 10 3 --no-graph || exit 1
+      prof prof_graph 20 5 || exit 1 ;;
+    pmc)
+      PMC=(--pmc FETCH_SIZE); prof pmc_fetch 4 2 --no-graph || exit 1
+      PMC=(--pmc WRITE_SIZE); prof pmc_write 4 2 --no-graph || exit 1
+      PMC=(--pmc FETCH_SIZE); prof pmc_fetch_vr 20 2 --workload vote_roi --no-graph || exit 1
+      PMC=(--pmc WRITE_SIZE); prof pmc_write_vr 20 2 --workload vote_roi --no-graph || exit 1
+      python scripts/pmc_traffic.py gpurun_out > $O/pmc_traffic.txt && cp profiles/pmc_traffic.json $O/ || exit 1 ;;
+    sq)
+      PMC=(--pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM)
+      prof sq1 2 1 --no-graph || exit 1
+      PMC=(--pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_SALU GRBM_GUI_ACTIVE SQ_WAVES)
+      prof sq2 2 1 --no-graph || exit 1 ;;
+    ab)
+      IFS=, read -ra vs <<< "$1"; shift
+      : > $O/ab_lib.log
+      for i in 1 2; do
+        for v in tree "${vs[@]}"; do
+          L=$R/posecnn_amd/libposecnn_hip.so; [ $v = tree ] || L=$R/scratch/$v.so
+          POSECNN_HIP_LIB=$L timeout -k 10 300 python bench.py --no-cpu-baseline --steps 30 2>/dev/null | \
+            python -c "import json,sys; d=json.load(sys.stdin); print('$v', d['value'], d['timing_ms_per_step'])" \
+            >> $O/ab_lib.log || exit 1
+        done
+      done ;;
+    micro)
+      n=$1; shift
+      timeout -k 10 300 python scripts/$n.py > $O/$n.log 2>&1 || exit 1 ;;
+    *) echo "unknown task $task"; exit 2 ;;
+  esac
+done
+echo "exit=0"

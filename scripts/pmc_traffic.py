@@ -1,5 +1,5 @@
 """Per-launch HBM traffic from rocprofv3 FETCH_SIZE / WRITE_SIZE passes
-(scripts/gpu_pmc.sh) -> profiles/pmc_traffic.json.
+(scripts/gpu.sh pmc) -> profiles/pmc_traffic.json.
 
 FETCH_SIZE / WRITE_SIZE are in KiB per dispatch.  On gfx950 FETCH_SIZE
 counts half the bytes of wide coalesced reads (MI355X_MICROARCH.md, HBM

@@ -95,7 +95,7 @@ def test_argument_validation_without_gpu(lib):
     assert lib.pcnn_gemm(4, 4, 4, ctypes.c_void_p(20), nul, 4, 0, ctypes.c_void_p(16), 4, 0, ctypes.c_void_p(16), 4,
                          nul, 0, nul, 0, nul, nul, 1, nul, 0, nul) == 1
     # roi pool: unknown layout
-    assert lib.pcnn_roi_pool_fwd(ctypes.c_void_p(16), 1, 8, 8, 4, 7, ctypes.c_void_p(16), 1, 5, nul, 1.0, 7, 7, 0,
+    assert lib.pcnn_roi_pool_fwd(ctypes.c_void_p(16), 1, 8, 8, 4, 7, ctypes.c_void_p(16), 1, 5, 0, nul, 1.0, 7, 7, 0,
                                  ctypes.c_void_p(16), ctypes.c_void_p(16), nul) == 1
 
 

@@ -67,3 +67,58 @@ def test_sharded_exchange_matches_single_device(orc, tmp_path, is_train):
     assert not rows[n:].any()
     # rows are image-major with global batch indices
     assert (np.diff(rows[:n, 0]) >= 0).all() and rows[:n, 0].max() < world * B_RANK
+
+
+# ---------------------------------------------------------------------------
+# GradShard: row-block ownership of the pose-head weight gradients
+
+
+def _ref_gemm(A, B, C, a_trans=0, M=None, N=None, K=None):
+    """Test-only stand-in for the HIP GEMM: C = A[:K]^T @ B[:K] in float64."""
+    assert a_trans == 1
+    C.copy_((A[:K].double().T @ B[:K].double()).float())
+
+
+def _ref_colsum(X, out):
+    out.copy_(X.double().sum(0).float())
+
+
+def _grad_worker(rank, world, port, out_dir, slot, rows):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from posecnn_amd.exchange import GradShard
+    din, dout = 24, 10
+    g = torch.Generator().manual_seed(100 + rank)
+    X = torch.randn((slot + 3, din), generator=g)          # capacity rows; rows >= n are stale
+    dY = torch.randn((slot + 3, dout), generator=g)
+    n = rows[rank]
+    gs = GradShard(dist, slot, [("w", (din, dout))], torch.device("cpu"))
+    gs.send_input("w", X)
+    gs.send_grad("w", dY, torch.tensor([n], dtype=torch.int32))
+    gw = torch.zeros((din // world, dout))
+    gb = torch.zeros((dout,))
+    gs.reduce("w", gw, gb, _ref_gemm, _ref_colsum)
+    np.save(os.path.join(out_dir, f"x{rank}.npy"), X[:n].numpy())
+    np.save(os.path.join(out_dir, f"dy{rank}.npy"), dY[:n].numpy())
+    np.save(os.path.join(out_dir, f"gw{rank}.npy"), gw.numpy())
+    np.save(os.path.join(out_dir, f"gb{rank}.npy"), gb.numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,rows", [(2, (5, 7)), (3, (7, 0, 2)), (4, (1, 7, 7, 3))])
+def test_grad_shard_row_blocks_equal_global_gradient(tmp_path, world, rows):
+    """Rank r's block equals rows_r of sum_r X_r^T dY_r over the live rows only
+    (padded slot rows and stale capacity rows contribute nothing); bias = full
+    column sum of every rank's live dY rows."""
+    slot = 7
+    mp.spawn(_grad_worker, args=(world, _free_port(), str(tmp_path), slot, rows), nprocs=world, join=True)
+    X = np.concatenate([np.load(tmp_path / f"x{r}.npy") for r in range(world)]).astype(np.float64)
+    dY = np.concatenate([np.load(tmp_path / f"dy{r}.npy") for r in range(world)]).astype(np.float64)
+    gw = X.T @ dY
+    blk = gw.shape[0] // world
+    for r in range(world):
+        np.testing.assert_allclose(np.load(tmp_path / f"gw{r}.npy"), gw[r * blk:(r + 1) * blk], rtol=1e-5,
+                                   atol=1e-5)
+        np.testing.assert_allclose(np.load(tmp_path / f"gb{r}.npy"), dY.sum(0), rtol=1e-5, atol=1e-5)

@@ -1,0 +1,142 @@
+"""Image-sharded pose step on 2 ranks vs the single-device step over the whole
+batch: rank r's pooled RoI rows, its dconv4_3 / dconv5_3
+images, the all-reduced loss and its row block of the fc6/fc7/fc8 weight
+gradients (exchange.GradShard) must reproduce the single-device run.
+
+The box has one GPU and RCCL wants one GPU per rank, so the two ranks share
+cuda:0 and talk over gloo through host copies (_HostStaged, test-only); the
+step code is the one that runs over RCCL."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+B_RANK, H, W, C, CH, UNITS = 2, 120, 160, 22, 64, 256
+pytestmark = pytest.mark.gpu
+
+
+class _Done:
+    def wait(self):
+        pass
+
+
+class _HostStaged:
+    """gloo collectives on host copies of device tensors (test-only)."""
+
+    def __init__(self, d):
+        self.d = d
+
+    def get_world_size(self):
+        return self.d.get_world_size()
+
+    def get_rank(self):
+        return self.d.get_rank()
+
+    def _ret(self, async_op):
+        torch.cuda.synchronize()
+        return _Done() if async_op else None
+
+    def all_reduce(self, t, async_op=False):
+        h = t.cpu()
+        self.d.all_reduce(h)
+        t.copy_(h)
+        return self._ret(async_op)
+
+    def all_gather_into_tensor(self, out, inp, async_op=False):
+        h = torch.empty(out.shape, dtype=out.dtype)
+        self.d.all_gather_into_tensor(h, inp.cpu())
+        out.copy_(h)
+        return self._ret(async_op)
+
+    def all_to_all_single(self, out, inp, async_op=False):
+        h = torch.empty(out.shape, dtype=out.dtype)
+        self.d.all_to_all_single(h, inp.contiguous().cpu())
+        out.copy_(h)
+        return self._ret(async_op)
+
+
+def _inputs(world):
+    from posecnn_amd import synth
+    fr = synth.make_frames(B_RANK * world, H=H, W=W, num_classes=C, objects_per_image=4, seed=77)
+    g = torch.Generator().manual_seed(5)
+    fr["conv4"] = torch.randn((B_RANK * world, H // 8, W // 8, CH), generator=g).numpy()
+    fr["conv5"] = torch.randn((B_RANK * world, H // 16, W // 16, CH), generator=g).numpy()
+    fr["points"], fr["symmetry"] = synth.rescaled_points(C)
+    return fr
+
+
+def _run(fr, sl, global_batch, batch_base, d):
+    from posecnn_amd.pipeline import PoseStep
+    dev = torch.device("cuda", 0)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    inputs = {k: t(fr[k][sl]) for k in ("label", "vertex", "meta", "conv4", "conv5")}
+    inputs.update(extents=t(fr["extents"]), gt=t(fr["gt"]), points=t(fr["points"]), symmetry=t(fr["symmetry"]))
+    nb = inputs["label"].shape[0]
+    step = PoseStep(nb, H, W, C, dev, channels=CH, units=UNITS, is_train=1, skip_pixels=3,
+                    global_batch=global_batch, batch_base=batch_base, dist=d)
+    for _ in range(2):  # second step: stale rows of the first must not leak into the gradients
+        step.step(inputs)
+    torch.cuda.synchronize()
+    n = int(step.hough["num_rois"][0].item())
+    out = dict(n=np.array(n), pool=step.pool[:n].cpu().numpy(), loss=step.loss.cpu().numpy(),
+               dconv4=step.dconv4.cpu().numpy(), dconv5=step.dconv5.cpu().numpy(),
+               box=step.hough["box"][:n].cpu().numpy())
+    for k, v in step.grads.items():
+        out["g_" + k] = v.cpu().numpy()
+    return out
+
+
+def _worker(rank, world, port, out_dir):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        fr = _inputs(world)
+        o = _run(fr, slice(rank * B_RANK, (rank + 1) * B_RANK), B_RANK * world, rank * B_RANK, _HostStaged(dist))
+        np.savez(os.path.join(out_dir, f"rank{rank}.npz"), **o)
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_sharded_step_matches_single_device(hip, tmp_path):
+    world = 2
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    fr = _inputs(world)
+    ref = _run(fr, slice(0, B_RANK * world), B_RANK * world, 0, None)
+    ranks = [dict(np.load(tmp_path / f"rank{r}.npz")) for r in range(world)]
+    n = [int(o["n"]) for o in ranks]
+    assert sum(n) == int(ref["n"]) and min(n) > 0
+    off = 0
+    for r, o in enumerate(ranks):
+        sl = slice(off, off + n[r])
+        np.testing.assert_array_equal(o["box"], ref["box"][sl])       # global batch column
+        np.testing.assert_array_equal(o["pool"], ref["pool"][sl])     # pooled from the rank's own maps
+        assert np.abs(o["pool"]).sum() > 0
+        img = slice(r * B_RANK, (r + 1) * B_RANK)
+        for k in ("dconv4", "dconv5"):
+            np.testing.assert_allclose(o[k], ref[k][img], rtol=1e-6, atol=1e-12)
+            assert np.abs(o[k]).sum() > 0
+        np.testing.assert_allclose(o["loss"], ref["loss"], rtol=1e-5)  # all-reduced, global normaliser
+        for k in ("w6", "w7", "w8"):
+            blk = ref["g_" + k].shape[0] // world
+            want = ref["g_" + k][r * blk:(r + 1) * blk]
+            assert o["g_" + k].shape == want.shape
+            np.testing.assert_allclose(o["g_" + k], want, rtol=1e-4, atol=1e-4 * np.abs(want).max())
+        for k in ("b6", "b7", "b8"):
+            want = ref["g_" + k]
+            np.testing.assert_allclose(o["g_" + k], want, rtol=1e-4, atol=1e-4 * np.abs(want).max())
+        off += n[r]
