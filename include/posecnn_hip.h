@@ -196,6 +196,7 @@ int pcnn_backproject_bwd(const float* top_diff, const float* depth, const float*
  *  precision: 0 = exact fp32 MFMA (v_mfma_f32_32x32x2_f32),
  *             1 = split-bf16 x3 MFMA (fp32-class accuracy, ~5x the fp32 rate)
  *  Deterministic (split-K partials are reduced in fixed order).
+ *  workspace: >= pcnn_gemm_workspace_size() bytes, one per stream.
  * ------------------------------------------------------------------------- */
 size_t pcnn_gemm_workspace_size(int M, int N, int K, int m_dynamic, int precision);
 

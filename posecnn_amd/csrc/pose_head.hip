@@ -17,13 +17,14 @@
 // across runs).  The pool5 + pool4 addition is fused into the A-tile load.
 #include "pcnn_common.h"
 #include <math.h>
+#include <stdlib.h>
+#include <type_traits>
 
 namespace {
 
 constexpr int BM = 128, BN = 128, BK = 16;
 constexpr int kGemmThreads = 256;
 constexpr int kMaxSplit = 8;   // fp32 kernel
-constexpr int kMaxSplitX = 16; // split-bf16 kernel (small-tile shapes such as fc8)
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -43,9 +44,10 @@ struct GemmArgs {
   int ldm;
   const int32_t* M_dev;
   const int32_t* K_dev;
-  float* slab;  // split-K partials [kMaxSplit][M][N]
+  float* slab;  // split-K partials [kMaxSplit][M][N] (fp32 path); x3: stream-K segment slabs
   int prec;     // 0 fp32 MFMA, 1 split-bf16 x3 (selects the split rule)
   int tile;     // x3 tile edge (256 or 128), chosen on the host
+  int xgrid;    // x3 launch grid (the plan depends on it; k_gemm_reduce re-derives the plan)
 };
 
 __device__ __forceinline__ int eff_dim(int full, const int32_t* dev) {
@@ -301,16 +303,56 @@ __host__ __device__ __forceinline__ int tile_x3(int M, int N, int K) {
   return (M <= 128 || N <= 128 || K <= 128) ? 128 : 256;
 }
 
-// split-K factor of the x3 kernel for the effective shape
-__host__ __device__ __forceinline__ int split_x3(int M, int N, int K, int T) {
-  const int tiles = ((M + T - 1) / T) * ((N + T - 1) / T);
-  const int grid = T == 256 ? XTile<256>::grid : XTile<128>::grid;
-  if (tiles >= grid / 2 || M == 0) return 1;
-  int s = grid / tiles;
-  const int smax = K / 128;
-  if (s > smax) s = smax;
-  if (s > kMaxSplitX) s = kMaxSplitX;
-  return s < 1 ? 1 : s;
+// Plan of the x3 kernel for an effective shape (M and K may live on the
+// device; the host evaluates the same plan for workspace sizing).
+//  - M tiles are balanced: mt = ceil(M / T) tiles of Tm rows each, Tm the
+//    smallest multiple of 32 >= M / mt (M = 405: 224 + 181 rows, not
+//    256 + 149), so the tiles of one N column carry about the same number of
+//    live 32-row accumulator blocks; rows past a tile's end are padding whose
+//    MFMAs the K loop skips.  The tiles of a column run side by side on one
+//    XCD, share their B panel through L2 and finish together (fc6 dX, 196
+//    tiles in one round: 318 -> 295 us).
+//  - Tile mode: whole tiles dealt round-robin.
+//  - Split-K (fewer than G/2 tiles, long K): S K slices per tile, partial
+//    slabs reduced in slice order by k_gemm_reduce (the forward shapes).
+//  Measured and dropped: stream-K over the tiles of a column (K ranges cut
+//  evenly over workgroup pairs, partial tiles fixed up in fixed order by the
+//  last segment to finish): fc6 dX 295 -> 343 us — the slab round trip and
+//  the per-segment fix-up cost more than the balance gains.
+constexpr int kMaxSplitX = 16;   // split-K slices
+struct XPlan {
+  int mt, nt, ns, Tm, tiles, mode, S;
+  bool m_fast;  // tile order: the dimension with fewer tiles runs fastest (its
+                // neighbours share the other operand's tile in L2)
+  __host__ __device__ int mi_of(int t) const { return m_fast ? t % mt : t / nt; }
+  __host__ __device__ int ni_of(int t) const { return m_fast ? t / mt : t % nt; }
+};
+
+__host__ __device__ __forceinline__ XPlan x_plan(int Meff, int N, int Keff, int T, int G) {
+  XPlan p;
+  p.mt = (Meff + T - 1) / T;
+  p.nt = (N + T - 1) / T;
+  p.ns = (Keff + XBK - 1) / XBK;
+  p.tiles = p.mt * p.nt;
+  p.m_fast = p.mt <= p.nt;
+  const int rows = p.mt ? (Meff + p.mt - 1) / p.mt : 0;
+  p.Tm = (rows + 31) / 32 * 32;
+  p.mode = 0;
+  p.S = 1;
+#ifdef PCNN_NOSPLIT
+  if (false) {
+#else
+  if (p.tiles > 0 && p.tiles < G / 2) {
+#endif
+    int s = G / p.tiles;
+    if (s > p.ns / 4) s = p.ns / 4;
+    if (s > kMaxSplitX) s = kMaxSplitX;
+    if (s > 1) {
+      p.mode = 1;
+      p.S = s;
+    }
+  }
+  return p;
 }
 
 // Operand view for buffer loads: SGPR descriptor + the extent in bytes.  All
@@ -406,38 +448,50 @@ __device__ __forceinline__ void x_load(const XOp& P, const XOp& P2, int r0, int 
   for (int q = 0; q < 4; q++) x_load_part<T, KC, RAGGED, A2>(P, P2, r0, rlim, k0, ke, v, q);
 }
 
+// Split of two fp32 values into packed bf16 (hi, lo) pairs: hi = bf16(x)
+// (RNE), lo = bf16(x - hi) (the subtraction is exact).  One pack-convert for
+// both hi halves, the fp32 value of each hi half by a shift / mask of that
+// pack, one pack-convert for both lo halves.
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void x_split2(float a, float b, unsigned& hi, unsigned& lo) {
+#ifdef PCNN_OLDSPLIT
+  const __bf16 ha = (__bf16)a, hb = (__bf16)b;
+  const __bf16 la = (__bf16)(a - (float)ha), lb = (__bf16)(b - (float)hb);
+  hi = (unsigned)__builtin_bit_cast(unsigned short, ha) | ((unsigned)__builtin_bit_cast(unsigned short, hb) << 16);
+  lo = (unsigned)__builtin_bit_cast(unsigned short, la) | ((unsigned)__builtin_bit_cast(unsigned short, lb) << 16);
+  return;
+#endif
+  const bf16x2 h = __builtin_convertvector((f32x2){a, b}, bf16x2);
+  hi = __builtin_bit_cast(unsigned, h);
+  const float ah = __uint_as_float(hi << 16), bh = __uint_as_float(hi & 0xffff0000u);
+  lo = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){a - ah, b - bh}, bf16x2));
+}
+
 // Part q of the split-and-store of a staged operand: KC rows (t >> 3) + T/4 q
 // (register quad q); NC row rb + q, i.e. element q of every register quad —
 // so an NC part needs all four loads of the operand, a KC part only its own.
 template <int T, bool KC>
 __device__ __forceinline__ void x_store_part(const float (&v)[16], char* hi, char* lo, int q) {
   const int t = threadIdx.x;
-  bf16x4 h, l4;
+  unsigned h0, h1, l0, l1;
   int o;
   if (KC) {
     const int kq = t & 7;
     const int row = (t >> 3) + (T / 4) * q;
-#pragma unroll
-    for (int e = 0; e < 4; e++) {
-      const __bf16 b = (__bf16)v[4 * q + e];
-      h[e] = b;
-      l4[e] = (__bf16)(v[4 * q + e] - (float)b);
-    }
+    x_split2(v[4 * q + 0], v[4 * q + 1], h0, l0);
+    x_split2(v[4 * q + 2], v[4 * q + 3], h1, l1);
     o = x_off(row, kq >> 1) + (kq & 1) * 8;
   } else {  // v[4 j + e] = (k = k-quad base + j, row = row-quad base + e): transpose into k-contiguous rows
     const int w = t >> 6, l = t & 63;
     const int row = 64 * (w >> 1) + 4 * (l >> 2) + q;
     const int kq = 4 * (w & 1) + (l & 3);  // k quad index 0..7 within the 32-k step
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-      const __bf16 b = (__bf16)v[4 * j + q];
-      h[j] = b;
-      l4[j] = (__bf16)(v[4 * j + q] - (float)b);
-    }
+    x_split2(v[q], v[4 + q], h0, l0);
+    x_split2(v[8 + q], v[12 + q], h1, l1);
     o = x_off(row, kq >> 1) + (kq & 1) * 8;
   }
-  *(bf16x4*)(hi + o) = h;
-  *(bf16x4*)(lo + o) = l4;
+  *(uint2*)(hi + o) = make_uint2(h0, h1);
+  *(uint2*)(lo + o) = make_uint2(l0, l1);
 }
 
 template <int T, bool KC>
@@ -446,22 +500,15 @@ __device__ __forceinline__ void x_store(const float (&v)[16], char* hi, char* lo
   for (int q = 0; q < 4; q++) x_store_part<T, KC>(v, hi, lo, q);
 }
 
-#ifndef PCNN_APF
-#define PCNN_APF 1
-#endif
-// PCNN_MFMA16: v_mfma_f32_16x16x32_bf16 instead of 32x32x16 (same cycles per
-// flop; the chip may hold a different clock on it, MI355X_MICROARCH.md DVFS
-// give-back item 7).  PCNN_PRIO: s_setprio(1) around each MFMA cluster.
-#ifndef PCNN_MFMA16
-#define PCNN_MFMA16 0
-#endif
-#ifndef PCNN_PRIO
-#define PCNN_PRIO 0
-#endif
-#if PCNN_MFMA16 && defined(PCNN_FUSED_STAGE) && !PCNN_FUSED_STAGE
-#error "PCNN_MFMA16 needs the fused staging loop"
-#endif
-template <int T, bool A_T, bool B_T, bool RAGGED, bool A2>
+template <int N>
+using IC = std::integral_constant<int, N>;
+
+
+// GEN: the general form (split-K and stream-K plans, for device-side M);
+// without it the kernel runs whole tiles only (a static-M shape whose plan
+// is tile mode, e.g. the weight gradients) and carries none of the partial-
+// sum code, which keeps its registers free of spills.
+template <int T, bool A_T, bool B_T, bool RAGGED, bool A2, bool GEN>
 __global__ void __launch_bounds__(XTile<T>::threads, T == 256 ? 1 : 2) k_gemm_x3(GemmArgs g) {
   using X = XTile<T>;
   constexpr int kXPart = X::part, kXStage = X::stage, AM = X::am;
@@ -469,10 +516,19 @@ __global__ void __launch_bounds__(XTile<T>::threads, T == 256 ? 1 : 2) k_gemm_x3
   constexpr bool A_KC = !A_T, B_KC = B_T;
   const int Meff = eff_dim(g.M, g.M_dev);
   const int Keff = eff_dim(g.K, g.K_dev);
-  const int mt = (Meff + T - 1) / T, nt = (g.N + T - 1) / T;
-  const int S = split_x3(Meff, g.N, Keff, T);
-  const int kchunk = ((Keff + S - 1) / S + XBK - 1) / XBK * XBK;
-  const int items = mt * nt * S;
+  XPlan pl = x_plan(Meff, g.N, Keff, T, g.xgrid);
+  if constexpr (!GEN) {
+    pl.mode = 0;
+    pl.S = 1;
+  }
+  const int active = min(g.xgrid, pl.tiles * pl.S);
+  // XCD-aware order: the first `active` blocks are dealt round-robin over the
+  // 8 XCDs; renumbered so the workgroups of one XCD take consecutive items —
+  // the M tiles of a column (one B panel) and neighbouring columns — and
+  // shared operand rows meet in one L2
+  int wg = blockIdx.x;
+  if (wg >= active) return;
+  if (active % 8 == 0) wg = (wg % 8) * (active / 8) + wg / 8;
   const int lane = pcnn::lane_id(), wave = threadIdx.x >> 6;
   const int wm = wave / X::wn, wn = wave % X::wn;
   const int r = lane & 31, hsel = lane >> 5;
@@ -481,13 +537,6 @@ __global__ void __launch_bounds__(XTile<T>::threads, T == 256 ? 1 : 2) k_gemm_x3
   const long b_el = B_T ? (long)(g.N - 1) * g.ldb + g.K : (long)(g.K - 1) * g.ldb + g.N;
   const XOp oa = x_op(g.A, g.lda, a_el), oa2 = x_op(g.A2, g.lda, a_el), ob = x_op(g.B, g.ldb, b_el),
             onull = x_op(nullptr, 0, 0);
-
-  // XCD-aware order: the G/8 workgroups of one XCD take consecutive items —
-  // the m/n tiles of one K slice — so shared operand rows meet in one L2.
-  const int G = gridDim.x;
-  const int wg = (G % 8 == 0) ? (int)(blockIdx.x % 8) * (G / 8) + (int)(blockIdx.x / 8) : (int)blockIdx.x;
-  const bool m_fast = mt <= nt;  // the dimension with fewer tiles runs fastest: its
-                                 // neighbours share the other operand's tile in L2
   // fragment offsets (bytes) inside an operand half, per k16 sub-step
   int a_off[2][AM], b_off[2][2];
 #pragma unroll
@@ -497,134 +546,48 @@ __global__ void __launch_bounds__(XTile<T>::threads, T == 256 ? 1 : 2) k_gemm_x3
 #pragma unroll
     for (int j = 0; j < 2; j++) b_off[ks][j] = x_off(wn * 64 + j * 32 + r, 2 * ks + hsel);
   }
-#if PCNN_MFMA16
-  // v_mfma_f32_16x16x32_bf16: lane -> row lane & 15 of a 16-row block, k chunk
-  // lane >> 4 (8 bf16 each: the whole 32-k step in one MFMA)
-  constexpr int AM16 = 2 * AM;  // 16-row accumulator blocks per wave along M
-  int a16[AM16], b16[4];
-#pragma unroll
-  for (int i = 0; i < AM16; i++) a16[i] = x_off(wm * (T / 2) + i * 16 + (lane & 15), lane >> 4);
-#pragma unroll
-  for (int j = 0; j < 4; j++) b16[j] = x_off(wn * 64 + j * 16 + (lane & 15), lane >> 4);
-#endif
-  for (int item = wg; item < items; item += G) {
-    const int tile = item % (mt * nt), z = item / (mt * nt);
-    const int mi = m_fast ? tile % mt : tile / nt;
-    const int ni = m_fast ? tile / mt : tile % nt;
-    const int m0 = mi * T, n0 = ni * T;
-    const int kb = z * kchunk, ke = min(Keff, kb + kchunk);
-    const int nsteps = kb < ke ? (ke - kb + XBK - 1) / XBK : 0;
-#if PCNN_MFMA16
-    f32x4 acc[AM16][4];
-#pragma unroll
-    for (int i = 0; i < AM16; i++)
-#pragma unroll
-      for (int j = 0; j < 4; j++) acc[i][j] = (f32x4){};
-#else
+
+  // One segment: K steps [kl, kh) of tile t, then its epilogue (whole tile)
+  // or its slab (+ the fix-up if it is the tile's last segment to finish).
+  auto segment = [&](int t, int kl, int kh, int z) {
+    const int mi = pl.mi_of(t);
+    const int m0 = mi * pl.Tm, n0 = pl.ni_of(t) * T;
+    const int rl = min(Meff, m0 + pl.Tm);  // the tile's rows: [m0, rl)
+    const int kb = kl * XBK, ke = min(Keff, kh * XBK);
+    const int nsteps = kh > kl ? kh - kl : 0;
+    // live 32-row accumulator blocks of this wave (rows past the tile are padding)
+    const int live = rl - (m0 + wm * (T / 2));
+    int amw = live <= 0 ? 0 : (live + 31) / 32;
+    amw = __builtin_amdgcn_readfirstlane(amw < AM ? amw : AM);
     f32x16 acc[AM][2];
 #pragma unroll
     for (int i = 0; i < AM; i++)
 #pragma unroll
       for (int j = 0; j < 2; j++) acc[i][j] = (f32x16){};
-#endif
     if (nsteps > 0) {
       float va[16], vb[16];
       // prologue: stage 0 -> LDS buffer 0, stage 1 -> registers
-      x_load<T, A_KC, RAGGED, A2>(oa, oa2, m0, Meff, kb, ke, va);
+      x_load<T, A_KC, RAGGED, A2>(oa, oa2, m0, rl, kb, ke, va);
       x_load<T, B_KC, RAGGED, false>(ob, onull, n0, g.N, kb, ke, vb);
       x_store<T, A_KC>(va, xl, xl + kXPart);
       x_store<T, B_KC>(vb, xl + 2 * kXPart, xl + 3 * kXPart);
       const int k1 = kb + (nsteps > 1 ? XBK : 0);
-      x_load<T, A_KC, RAGGED, A2>(oa, oa2, m0, Meff, k1, ke, va);
+      x_load<T, A_KC, RAGGED, A2>(oa, oa2, m0, rl, k1, ke, va);
       x_load<T, B_KC, RAGGED, false>(ob, onull, n0, g.N, k1, ke, vb);
       __syncthreads();
-      // steady state, one basic block per step: MFMAs on buffer s & 1, stage
-      // s+1 (registers) -> the other buffer, loads of stage s+2 (clamped to
-      // the last stage: the surplus stores land in a buffer nobody reads)
-#ifndef PCNN_STAGGER
-#define PCNN_STAGGER 0
-#endif
-      // PCNN_STAGGER: the SIMD partners (waves w, w + 4) run a step in
-      // opposite order (MFMAs then staging / staging then MFMAs).
-#if !PCNN_MFMA16
-      const bool late = PCNN_STAGGER && (threadIdx.x >> 6) >= 4;
-      auto compute = [&](const char* cur) {
-#pragma unroll
-          for (int ks = 0; ks < 2; ks++) {
-            bf16x8 bh[2], bl[2];
-#pragma unroll
-            for (int j = 0; j < 2; j++) {
-              bh[j] = *(const bf16x8*)(cur + 2 * kXPart + b_off[ks][j]);
-              bl[j] = *(const bf16x8*)(cur + 3 * kXPart + b_off[ks][j]);
-            }
-#if PCNN_APF
-            // A fragments one accumulator row ahead: the reads of row i + 1 are
-            // in flight while row i's six MFMAs issue
-            bf16x8 ah[2], al[2];
-            ah[0] = *(const bf16x8*)(cur + a_off[ks][0]);
-            al[0] = *(const bf16x8*)(cur + kXPart + a_off[ks][0]);
-#pragma unroll
-            for (int i = 0; i < AM; i++) {
-              if (i + 1 < AM) {
-                ah[(i + 1) & 1] = *(const bf16x8*)(cur + a_off[ks][i + 1]);
-                al[(i + 1) & 1] = *(const bf16x8*)(cur + kXPart + a_off[ks][i + 1]);
-              }
-#pragma unroll
-              for (int j = 0; j < 2; j++) {
-                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i & 1], bh[j], acc[i][j], 0, 0, 0);
-                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i & 1], bl[j], acc[i][j], 0, 0, 0);
-                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i & 1], bh[j], acc[i][j], 0, 0, 0);
-              }
-            }
-#else
-#pragma unroll
-            for (int i = 0; i < AM; i++) {
-              const bf16x8 ah = *(const bf16x8*)(cur + a_off[ks][i]);
-              const bf16x8 al = *(const bf16x8*)(cur + kXPart + a_off[ks][i]);
-#pragma unroll
-              for (int j = 0; j < 2; j++) {
-                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh[j], acc[i][j], 0, 0, 0);
-                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl[j], acc[i][j], 0, 0, 0);
-                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh[j], acc[i][j], 0, 0, 0);
-              }
-            }
-#endif
-          }
-      };
-      auto stage = [&](char* nxt, int s) {
-        x_store<T, A_KC>(va, nxt, nxt + kXPart);
-        x_store<T, B_KC>(vb, nxt + 2 * kXPart, nxt + 3 * kXPart);
-        const int s2 = s + 2 < nsteps ? s + 2 : nsteps - 1;
-        x_load<T, A_KC, RAGGED, A2>(oa, oa2, m0, Meff, kb + s2 * XBK, ke, va);
-        x_load<T, B_KC, RAGGED, false>(ob, onull, n0, g.N, kb + s2 * XBK, ke, vb);
-      };
-#endif  // !PCNN_MFMA16
-#ifndef PCNN_FUSED_STAGE
-#define PCNN_FUSED_STAGE 1
-#endif
-#if PCNN_FUSED_STAGE
-      // Staging spread through the MFMA stream: after each accumulator row
-      // (six MFMAs) one part of step s+1's split-and-store and the matching
-      // loads of step s+2, so the conversion VALU and LDS writes fill MFMA
-      // gaps instead of running as a separate phase after them (both waves of
-      // a SIMD reach that phase together).  The `nxt` buffer was last read in
-      // step s-1, before the barrier, so it may be written at any point here.
+      // Staging part c of step s+1 (registers -> the other LDS buffer) and the
+      // matching loads of step s+2 (clamped to the last step: the surplus
+      // stores land in a buffer nobody reads).  Parts 0-3 are A, 4-7 B.  The
+      // `nxt` buffer was last read in step s-1, before the barrier, so it may
+      // be written at any point of step s.
       auto stage_part = [&](int c, char* nxt, int kn) {
         if (c < 4) {
-#ifdef PCNN_ABL_ARAW
-          if (A_KC) {  // timing ablation: A stored as if already split (no conversion VALU; wrong results)
-            const int t = threadIdx.x, row = (t >> 3) + (T / 4) * c, kq = t & 7;
-            const int o = x_off(row, kq >> 1) + (kq & 1) * 8;
-            *(uint2*)(nxt + o) = make_uint2(__float_as_uint(va[4 * c]), __float_as_uint(va[4 * c + 1]));
-            *(uint2*)(nxt + kXPart + o) = make_uint2(__float_as_uint(va[4 * c + 2]), __float_as_uint(va[4 * c + 3]));
-          } else
-#endif
           x_store_part<T, A_KC>(va, nxt, nxt + kXPart, c);
           if (A_KC) {
-            x_load_part<T, true, RAGGED, A2>(oa, oa2, m0, Meff, kn, ke, va, c);
+            x_load_part<T, true, RAGGED, A2>(oa, oa2, m0, rl, kn, ke, va, c);
           } else if (c == 3) {
 #pragma unroll
-            for (int q = 0; q < 4; q++) x_load_part<T, false, RAGGED, A2>(oa, oa2, m0, Meff, kn, ke, va, q);
+            for (int q = 0; q < 4; q++) x_load_part<T, false, RAGGED, A2>(oa, oa2, m0, rl, kn, ke, va, q);
           }
         } else {
           x_store_part<T, B_KC>(vb, nxt + 2 * kXPart, nxt + 3 * kXPart, c - 4);
@@ -636,165 +599,166 @@ __global__ void __launch_bounds__(XTile<T>::threads, T == 256 ? 1 : 2) k_gemm_x3
           }
         }
       };
-      constexpr int kCPG = 8 / (2 * AM);  // staging parts per accumulator row
-      for (int s = 0; s < nsteps; s++) {
-        const char* cur = xl + (s & 1) * kXStage;
-        char* nxt = xl + ((s + 1) & 1) * kXStage;
-        const int kn = kb + (s + 2 < nsteps ? s + 2 : nsteps - 1) * XBK;
-#if PCNN_MFMA16
-        {
-          constexpr int kCPG16 = 8 / AM16;  // staging parts per 16-row block
-          bf16x8 bh[4], bl[4];
-#pragma unroll
-          for (int j = 0; j < 4; j++) {
-            bh[j] = *(const bf16x8*)(cur + 2 * kXPart + b16[j]);
-            bl[j] = *(const bf16x8*)(cur + 3 * kXPart + b16[j]);
-          }
-          bf16x8 ah[2], al[2];
-          ah[0] = *(const bf16x8*)(cur + a16[0]);
-          al[0] = *(const bf16x8*)(cur + kXPart + a16[0]);
-#pragma unroll
-          for (int i = 0; i < AM16; i++) {
-            if (i + 1 < AM16) {
-              ah[(i + 1) & 1] = *(const bf16x8*)(cur + a16[i + 1]);
-              al[(i + 1) & 1] = *(const bf16x8*)(cur + kXPart + a16[i + 1]);
-            }
-#if PCNN_PRIO
-            __builtin_amdgcn_s_setprio(1);
-#endif
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[i & 1], bh[j], acc[i][j], 0, 0, 0);
-              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i & 1], bl[j], acc[i][j], 0, 0, 0);
-              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i & 1], bh[j], acc[i][j], 0, 0, 0);
-            }
-#if PCNN_PRIO
-            __builtin_amdgcn_s_setprio(0);
-#endif
+      // The K loop, specialised on AMW = the wave's live accumulator blocks:
+      // at M = 405 in 256-row tiles the second tile's lower waves (rows
+      // 384-511) have one live block of four, so they issue a quarter of the
+      // MFMAs and their SIMD partners run the matrix pipe alone (the schedule
+      // weights that tile lighter).  Each specialisation keeps one basic block
+      // per K step: after each accumulator row (six MFMAs) its share of the
+      // eight staging parts, so the conversion VALU and LDS writes fill MFMA
+      // gaps.
+      auto kloop = [&](auto amw_c) {
+        constexpr int AMW = decltype(amw_c)::value;
+        constexpr int SLOTS = 2 * AMW;
+        for (int s = 0; s < nsteps; s++) {
+          const char* cur = xl + (s & 1) * kXStage;
+          char* nxt = xl + ((s + 1) & 1) * kXStage;
+          const int kn = kb + (s + 2 < nsteps ? s + 2 : nsteps - 1) * XBK;
+          if constexpr (AMW == 0) {
 #ifndef PCNN_ABL_NOSTAGE
 #pragma unroll
-            for (int q = 0; q < kCPG16; q++) stage_part(i * kCPG16 + q, nxt, kn);
+            for (int c = 0; c < 8; c++) stage_part(c, nxt, kn);
 #endif
-          }
-        }
-#else
+          } else {
 #pragma unroll
-        for (int ks = 0; ks < 2; ks++) {
-          bf16x8 bh[2], bl[2];
+            for (int ks = 0; ks < 2; ks++) {
+              bf16x8 bh[2], bl[2];
 #pragma unroll
-          for (int j = 0; j < 2; j++) {
-            bh[j] = *(const bf16x8*)(cur + 2 * kXPart + b_off[ks][j]);
-            bl[j] = *(const bf16x8*)(cur + 3 * kXPart + b_off[ks][j]);
-          }
-          bf16x8 ah[2], al[2];
-          ah[0] = *(const bf16x8*)(cur + a_off[ks][0]);
-          al[0] = *(const bf16x8*)(cur + kXPart + a_off[ks][0]);
+              for (int j = 0; j < 2; j++) {
+                bh[j] = *(const bf16x8*)(cur + 2 * kXPart + b_off[ks][j]);
+                bl[j] = *(const bf16x8*)(cur + 3 * kXPart + b_off[ks][j]);
+              }
+              // A fragments one accumulator row ahead: the reads of row i + 1
+              // are in flight while row i's six MFMAs issue
+              bf16x8 ah[2], al[2];
+              ah[0] = *(const bf16x8*)(cur + a_off[ks][0]);
+              al[0] = *(const bf16x8*)(cur + kXPart + a_off[ks][0]);
 #pragma unroll
-          for (int i = 0; i < AM; i++) {
-            if (i + 1 < AM) {
-              ah[(i + 1) & 1] = *(const bf16x8*)(cur + a_off[ks][i + 1]);
-              al[(i + 1) & 1] = *(const bf16x8*)(cur + kXPart + a_off[ks][i + 1]);
-            }
+              for (int i = 0; i < AMW; i++) {
+                if (i + 1 < AMW) {
+                  ah[(i + 1) & 1] = *(const bf16x8*)(cur + a_off[ks][i + 1]);
+                  al[(i + 1) & 1] = *(const bf16x8*)(cur + kXPart + a_off[ks][i + 1]);
+                }
 #pragma unroll
-            for (int j = 0; j < 2; j++) {
-              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i & 1], bh[j], acc[i][j], 0, 0, 0);
-              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i & 1], bl[j], acc[i][j], 0, 0, 0);
-              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i & 1], bh[j], acc[i][j], 0, 0, 0);
-            }
+                for (int j = 0; j < 2; j++) {
+                  acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i & 1], bh[j], acc[i][j], 0, 0, 0);
+                  acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i & 1], bl[j], acc[i][j], 0, 0, 0);
+                  acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i & 1], bh[j], acc[i][j], 0, 0, 0);
+                }
 #ifndef PCNN_ABL_NOSTAGE
+                const int slot = ks * AMW + i;
 #pragma unroll
-            for (int q = 0; q < kCPG; q++) stage_part((ks * AM + i) * kCPG + q, nxt, kn);
+                for (int c = slot * 8 / SLOTS; c < (slot + 1) * 8 / SLOTS; c++) stage_part(c, nxt, kn);
 #endif
+              }
+            }
           }
+          __syncthreads();
         }
-#endif  // PCNN_MFMA16
-#ifndef PCNN_ABL_NOBAR
-        __syncthreads();
-#endif
-      }
+      };
+#ifdef PCNN_NOAMW
+      kloop(IC<AM>{});
 #else
-      for (int s = 0; s < nsteps; s++) {
-        const char* cur = xl + (s & 1) * kXStage;
-        char* nxt = xl + ((s + 1) & 1) * kXStage;
-        if (late) {
-          stage(nxt, s);
-          compute(cur);
-        } else {
-          compute(cur);
-          stage(nxt, s);
-        }
-        __syncthreads();
+      if (amw == AM) kloop(IC<AM>{});
+      else if (amw == 0) kloop(IC<0>{});
+      else if (amw == 1) kloop(IC<1>{});
+      else if constexpr (AM >= 4) {
+        if (amw == 2) kloop(IC<2>{});
+        else kloop(IC<3>{});
       }
 #endif
     }
-    // epilogue, branch-free: bias / mask come in through buffer loads and
-    // results leave through buffer stores, out-of-range lanes masked by an
-    // out-of-extent offset (loads return 0, stores are dropped)
+
+    // epilogue (one uniform branch: slab or C), otherwise branch-free: bias /
+    // mask come in through buffer loads and results leave through buffer
+    // stores, out-of-range lanes masked by an out-of-extent offset (loads
+    // return 0, stores are dropped).  The 16 mask values of group (j, i) are
+    // issued one group ahead of their use, so the tile pays one mask latency,
+    // not 8.
+    // Accumulator blocks: EJ (N) x EI (M) blocks of EB x EB, EQ values per
+    // lane.  Value q of block (i, j) sits at row m0 + rlane + qrow(i, q),
+    // column n0 + clane + 32 j.  Every per-value term is uniform (a scalar
+    // add / compare against the lane's one base): left to itself the
+    // compiler precomputes a lane's 64 row indices once per kernel, spills
+    // them, and reloads one per store behind a full vmcnt drain.
+    constexpr int EJ = 2, EI = AM, EQ = 16, EB = 32;
+    const int rlane = wm * (T / 2) + 4 * hsel, clane = wn * 64 + r;
+    auto qrow = [](int i, int q) { return i * EB + (q & 3) + 8 * (q >> 2); };
+    const int rlim = rl - m0, clim = g.N - n0;  // rows / columns of the tile that exist
+    if (pl.mode == 1) {  // split-K slice: raw partial sums to slab z
+      const XOp oslab = x_op(g.slab, g.N, (long)pl.S * g.M * g.N);
+      const unsigned sb = (unsigned)(((z * g.M + m0 + rlane) * g.N + n0 + clane) * 4);
+#pragma unroll
+      for (int j = 0; j < EJ; j++)
+#pragma unroll
+        for (int i = 0; i < EI; i++)
+#pragma unroll
+          for (int q = 0; q < EQ; q++) {
+            const bool ok = clane < clim - j * EB && rlane < rlim - qrow(i, q);
+            // (a scalar copy first: __builtin_bit_cast of an ext-vector
+            // element subscript reads element 0 with this compiler)
+            const float v = acc[i][j][q];
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), oslab.rs,
+                                                  ok ? sb + (unsigned)((qrow(i, q) * g.N + j * EB) * 4) : kXOob,
+                                                  0, 0);
+          }
+      return;
+    }
+    const bool msk = g.mask != nullptr;
     const XOp oc = x_op(g.C, g.ldc, (long)(g.M - 1) * g.ldc + g.N);
-    const XOp oslab = x_op(g.slab, g.N, (long)S * g.M * g.N);
     const XOp obias = x_op(g.bias, 0, g.N);
     const XOp omask = x_op(g.mask, g.ldm, g.mask ? (long)(g.M - 1) * g.ldm + g.N : 0);
-    // Masked epilogue (S == 1): the 16 mask values of group (j, i) are issued
-    // one group ahead of their use, so the tile pays one mask latency, not 8.
-    const bool msk = S == 1 && g.mask;
-    // accumulator blocks: EJ (N) x EI (M) blocks of EB x EB, EQ values per lane;
-    // e_col / e_row: output coordinates of a lane's value q of block (i, j)
-#if PCNN_MFMA16
-    constexpr int EJ = 4, EI = AM16, EQ = 4, EB = 16;
-    auto e_col = [&](int j) { return n0 + wn * 64 + j * EB + (lane & 15); };
-    auto e_row = [&](int i, int q) { return m0 + wm * (T / 2) + i * EB + 4 * (lane >> 4) + q; };
-#else
-    constexpr int EJ = 2, EI = AM, EQ = 16, EB = 32;
-    auto e_col = [&](int j) { return n0 + wn * 64 + j * EB + r; };
-    auto e_row = [&](int i, int q) { return m0 + wm * (T / 2) + i * EB + (q & 3) + 8 * (q >> 2) + 4 * hsel; };
-#endif
+    const unsigned cbase = (unsigned)(((m0 + rlane) * g.ldc + n0 + clane) * 4);
+    const unsigned mbase = (unsigned)(((m0 + rlane) * g.ldm + n0 + clane) * 4);
     float mv[2][EQ];
     auto load_mask = [&](int gi, float (&d)[EQ]) {
-      const int n = e_col(gi / EI);
+      const int j = gi / EI, i = gi % EI;
 #pragma unroll
       for (int q = 0; q < EQ; q++) {
-        const int m = e_row(gi % EI, q);
-        d[q] = x_ld1(omask, (n < g.N && m < Meff) ? (unsigned)(m * g.ldm + n) * 4u : kXOob, 0);
+        const bool ok = clane < clim - j * EB && rlane < rlim - qrow(i, q);
+        d[q] = x_ld1(omask, ok ? mbase + (unsigned)((qrow(i, q) * g.ldm + j * EB) * 4) : kXOob, 0);
       }
     };
     if (msk) load_mask(0, mv[0]);
 #pragma unroll
     for (int j = 0; j < EJ; j++) {
-      const int n = e_col(j);
-      const bool nok = n < g.N;
-      const float bv = (S == 1 && g.bias) ? x_ld1(obias, nok ? (unsigned)n * 4u : kXOob, 0) : 0.f;
+      const bool nok = clane < clim - j * EB;
+      const float bv = g.bias ? x_ld1(obias, nok ? (unsigned)((n0 + clane + j * EB) * 4) : kXOob, 0) : 0.f;
 #pragma unroll
       for (int i = 0; i < EI; i++) {
         const int gi = EI * j + i;
         if (msk && gi + 1 < EJ * EI) load_mask(gi + 1, mv[(gi + 1) & 1]);
 #pragma unroll
         for (int q = 0; q < EQ; q++) {
-          const int m = e_row(i, q);
-          const bool ok = nok && m < Meff;
-          float v = acc[i][j][q];
-          if (S == 1) {
-            v += bv;
-            if (g.act == 1) v = v > 0.f ? v : 0.f;
-            if (msk && !(mv[gi & 1][q] > 0.f)) v = 0.f;
+          const bool ok = nok && rlane < rlim - qrow(i, q);
+          float v = acc[i][j][q] + bv;
+          if (g.act == 1) v = v > 0.f ? v : 0.f;
+          if (msk && !(mv[gi & 1][q] > 0.f)) v = 0.f;
 #ifdef PCNN_ABL_NOEPI
-            if (v != 1.2345e-30f) continue;
+          if (v != 1.2345e-30f) continue;
 #endif
-            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), oc.rs,
-                                                  ok ? (unsigned)(m * g.ldc + n) * 4u : kXOob, 0, 0);
-          } else {
-            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), oslab.rs,
-                                                  ok ? (unsigned)((z * g.M + m) * g.N + n) * 4u : kXOob, 0, 0);
-          }
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), oc.rs,
+                                                ok ? cbase + (unsigned)((qrow(i, q) * g.ldc + j * EB) * 4) : kXOob,
+                                                0, 0);
         }
       }
     }
+  };
+
+  // this workgroup's items: every active-th (tile, K slice); one call site,
+  // so the segment body is instantiated once
+  const int kstep = (pl.ns + pl.S - 1) / pl.S;  // split-K: K steps per slice
+  for (int item = wg; item < pl.tiles * pl.S; item += active) {
+    const int z = item / pl.tiles, t = item % pl.tiles;
+    const int kl = z * kstep;
+    segment(t, kl, min(pl.ns, kl + kstep), z);
   }
 }
 
 __global__ void __launch_bounds__(256) k_gemm_reduce(GemmArgs g) {
   const int Meff = eff_dim(g.M, g.M_dev);
   const int Keff = eff_dim(g.K, g.K_dev);
-  const int S = g.prec ? split_x3(Meff, g.N, Keff, g.tile) : split_for(Meff, g.N, Keff);
+  const int S = g.prec ? x_plan(Meff, g.N, Keff, g.tile, g.xgrid).S : split_for(Meff, g.N, Keff);
   if (S == 1) return;
   // slab sums in slice order z = 0, 1, ... (0 + s0 == s0, so starting from
   // s0 is the same fp32 sum); float4 along N when rows stay 16-B aligned
@@ -915,11 +879,18 @@ __global__ void __launch_bounds__(256) k_head_bwd(const float* __restrict__ dpre
 
 }  // namespace
 
+static int x3_max_grid(int T) { return T == 256 ? XTile<256>::grid : XTile<128>::grid; }
+
 extern "C" size_t pcnn_gemm_workspace_size(int M, int N, int K, int m_dynamic, int precision) {
   if (M <= 0 || N <= 0) return 256;
-  // split-K partial slabs; the split only grows when the device-side M shrinks
-  const int s = precision == 1 ? split_x3(m_dynamic ? 1 : M, N, K, tile_x3(M, N, K))
-                                : split_for(m_dynamic ? 1 : M, N, K);
+  if (precision == 1) {
+    // split-K slabs [S][M][N] at the largest split any effective M <= M can take (fewest tiles)
+    const int T = tile_x3(M, N, K);
+    const XPlan lo = x_plan(m_dynamic ? 1 : M, N, K, T, x3_max_grid(T));
+    return lo.mode == 1 ? pcnn::align_up((size_t)lo.S * M * N * sizeof(float), 256) + 256 : 256;
+  }
+  // fp32 path: split-K partial slabs; the split only grows when the device-side M shrinks
+  const int s = split_for(m_dynamic ? 1 : M, N, K);
   return s > 1 ? pcnn::align_up((size_t)s * M * N * sizeof(float), 256) + 256 : 256;
 }
 
@@ -936,55 +907,56 @@ extern "C" int pcnn_gemm(int M, int N, int K, const float* A, const float* A2, i
   PCNN_REQUIRE(precision == 0 || (lda % 4 == 0 && ldb % 4 == 0 && ((uintptr_t)A & 15) == 0 &&
                                   ((uintptr_t)B & 15) == 0 && (!A2 || ((uintptr_t)A2 & 15) == 0)));
   PCNN_REQUIRE(precision == 0 || ((long)(a_trans ? K : M) * lda < (1l << 29) && (long)(b_trans ? N : K) * ldb < (1l << 29) &&
-                                  (long)M * ldc < (1l << 29) &&
-                                  (long)split_x3(M_dev ? 1 : M, N, K, tile_x3(M, N, K)) * M * N < (1l << 29) &&
-                                  (!mask || (long)M * ldm < (1l << 29))));
+                                  (long)M * ldc < (1l << 29) && (!mask || (long)M * ldm < (1l << 29))));
   if (M == 0) return PCNN_OK;
   if (workspace_bytes < pcnn_gemm_workspace_size(M, N, K, M_dev != nullptr, precision) || !workspace)
     return PCNN_ECAPACITY;
   GemmArgs g{M, N, K, A, A2, lda, B, ldb, Cm, ldc, bias, act, mask, ldm, M_dev, K_dev, (float*)workspace, precision,
-             tile_x3(M, N, K)};
+             tile_x3(M, N, K), 0};
   hipStream_t st = (hipStream_t)stream;
   if (precision == 1) {
-    // persistent grid: one workgroup per CU (a multiple of 8 for the XCD-aware
-    // item order); the device-side M can only shrink the item count
     // ragged edges: a KC operand whose K (or device-side K) is not a multiple of
     // 4, or an NC operand whose row count is not -> element-wise edge loads
     const bool a_kc = !a_trans, b_kc = b_trans;
     const bool ragged = ((a_kc || b_kc) && (K % 4 != 0 || K_dev != nullptr)) || (!a_kc && M % 4 != 0) ||
                         (!b_kc && N % 4 != 0);
     const int T = g.tile;
-    const int mt = (M + T - 1) / T, nt = (N + T - 1) / T;
-    const int max_grid = T == 256 ? XTile<256>::grid : XTile<128>::grid;
-    const long cap_items = (long)mt * nt * kMaxSplitX;
-    long grid = cap_items < max_grid ? cap_items : max_grid;
+    const int max_grid = x3_max_grid(T);
+    long grid = max_grid;
+    bool may_split = true, gen = true;
     if (!M_dev) {
-      // static M: the item count is known up to a device-side K, which can
-      // only lower the split.  Use the fewest workgroups that keep the same
-      // number of rounds (fc6 dW: 1568 tiles -> 224 workgroups x 7): the
-      // makespan is unchanged and the spare CUs run the other stream's kernels.
-      const long items = (long)mt * nt * split_x3(M, N, K, T);
-      const long rounds = (items + max_grid - 1) / max_grid;
-      long g2 = (items + rounds - 1) / rounds;
-      g2 = (g2 + 7) / 8 * 8;
-      if (g2 < grid) grid = g2;
+      // static M: if the plan runs whole tiles (a device-side K can only lower
+      // the split), use the fewest workgroups that keep the same number of
+      // rounds (fc6 dW: 1568 tiles -> 224 workgroups x 7): the makespan is
+      // unchanged and the spare CUs run the other stream's kernels
+      const XPlan pl = x_plan(M, N, K, T, max_grid);
+      may_split = pl.mode == 1;
+      if (pl.mode == 0) {
+        gen = T != 256;  // the lean whole-tile kernel (instantiated for T = 256)
+        const long items = pl.tiles;
+        const long rounds = (items + max_grid - 1) / max_grid;
+        grid = (items + rounds - 1) / rounds;
+        grid = (grid + 7) / 8 * 8;
+        if (grid > max_grid) grid = max_grid;
+      }
     }
-    if (grid >= 8) grid -= grid % 8;
-#define PCNN_X3_LAUNCH_T(TT, AT, BT, RG, S2)                                                                   \
+    g.xgrid = (int)grid;
+#define PCNN_X3_LAUNCH_G(TT, AT, BT, RG, S2, GN)                                                              \
   do {                                                                                                          \
     static bool attr_set = false;                                                                               \
     if (!attr_set) {                                                                                            \
-      (void)hipFuncSetAttribute((const void*)k_gemm_x3<TT, AT, BT, RG, S2>,                                     \
+      (void)hipFuncSetAttribute((const void*)k_gemm_x3<TT, AT, BT, RG, S2, GN>,                                 \
                                 hipFuncAttributeMaxDynamicSharedMemorySize, XTile<TT>::lds);                    \
       attr_set = true;                                                                                          \
     }                                                                                                           \
-    hipLaunchKernelGGL((k_gemm_x3<TT, AT, BT, RG, S2>), dim3(grid), dim3(XTile<TT>::threads), XTile<TT>::lds, st, \
-                       g);                                                                                      \
+    hipLaunchKernelGGL((k_gemm_x3<TT, AT, BT, RG, S2, GN>), dim3(grid), dim3(XTile<TT>::threads), XTile<TT>::lds, \
+                       st, g);                                                                                  \
   } while (0)
-#define PCNN_X3_LAUNCH(AT, BT, RG, S2)                  \
-  do {                                                  \
-    if (T == 256) PCNN_X3_LAUNCH_T(256, AT, BT, RG, S2); \
-    else PCNN_X3_LAUNCH_T(128, AT, BT, RG, S2);          \
+#define PCNN_X3_LAUNCH(AT, BT, RG, S2)                          \
+  do {                                                          \
+    if (T != 256) PCNN_X3_LAUNCH_G(128, AT, BT, RG, S2, true);  \
+    else if (gen) PCNN_X3_LAUNCH_G(256, AT, BT, RG, S2, true);  \
+    else PCNN_X3_LAUNCH_G(256, AT, BT, RG, S2, false);          \
   } while (0)
 #define PCNN_X3_LAYOUT(RG, S2)                                     \
   do {                                                            \
@@ -998,33 +970,29 @@ extern "C" int pcnn_gemm(int M, int N, int K, const float* A, const float* A2, i
     else if (!A2) PCNN_X3_LAYOUT(true, false);
     else PCNN_X3_LAYOUT(true, true);
 #undef PCNN_X3_LAYOUT
-#undef PCNN_X3_LAUNCH_T
+#undef PCNN_X3_LAUNCH_G
 #undef PCNN_X3_LAUNCH
-  } else {
-    const int mt = (M + BM - 1) / BM, nt = (N + BN - 1) / BN;
-    // persistent grid sized for the capacity shape at its split
-    const long items = (long)mt * nt * split_for(M, N, K);
-    long grid = items < 2048 ? items : 2048;
-    if (grid < 512) grid = 512;
-    if (!a_trans && !b_trans) hipLaunchKernelGGL((k_gemm_f32<false, false>), dim3(grid), dim3(kGemmThreads), 0, st, g);
-    else if (!a_trans && b_trans) hipLaunchKernelGGL((k_gemm_f32<false, true>), dim3(grid), dim3(kGemmThreads), 0, st, g);
-    else if (a_trans && !b_trans) hipLaunchKernelGGL((k_gemm_f32<true, false>), dim3(grid), dim3(kGemmThreads), 0, st, g);
-    else hipLaunchKernelGGL((k_gemm_f32<true, true>), dim3(grid), dim3(kGemmThreads), 0, st, g);
+    // split-K slab reduction when the plan can split (a no-op launch is not
+    // free: queued behind a persistent GEMM on another stream it holds back
+    // everything after it on its own stream)
+    if (may_split) hipLaunchKernelGGL(k_gemm_reduce, dim3(1024), dim3(256), 0, st, g);
+    PCNN_CHECK_LAUNCH();
+    return PCNN_OK;
   }
+  const int mt = (M + BM - 1) / BM, nt = (N + BN - 1) / BN;
+  // persistent grid sized for the capacity shape at its split
+  const long items = (long)mt * nt * split_for(M, N, K);
+  long grid = items < 2048 ? items : 2048;
+  if (grid < 512) grid = 512;
+  if (!a_trans && !b_trans) hipLaunchKernelGGL((k_gemm_f32<false, false>), dim3(grid), dim3(kGemmThreads), 0, st, g);
+  else if (!a_trans && b_trans) hipLaunchKernelGGL((k_gemm_f32<false, true>), dim3(grid), dim3(kGemmThreads), 0, st, g);
+  else if (a_trans && !b_trans) hipLaunchKernelGGL((k_gemm_f32<true, false>), dim3(grid), dim3(kGemmThreads), 0, st, g);
+  else hipLaunchKernelGGL((k_gemm_f32<true, true>), dim3(grid), dim3(kGemmThreads), 0, st, g);
   // split-K slab reduction, unless no device-side M can make the shape split
   // (a static M whose tile count already fills the grid: split 1 for every K).
   // A no-op launch is not free: queued behind a persistent GEMM on another
   // stream it holds back everything after it on its own stream.
-  bool may_split = true;
-  if (!M_dev) {
-    if (precision == 1) {
-      const int T = g.tile;
-      const int tiles = ((M + T - 1) / T) * ((N + T - 1) / T);
-      may_split = tiles < (T == 256 ? XTile<256>::grid : XTile<128>::grid) / 2;
-    } else {
-      may_split = ((M + BM - 1) / BM) * ((N + BN - 1) / BN) < 256;
-    }
-  }
+  const bool may_split = M_dev || ((M + BM - 1) / BM) * ((N + BN - 1) / BN) < 256;
   if (may_split) hipLaunchKernelGGL(k_gemm_reduce, dim3(1024), dim3(256), 0, st, g);
   PCNN_CHECK_LAUNCH();
   return PCNN_OK;

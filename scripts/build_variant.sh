@@ -1,12 +1,18 @@
 #!/bin/bash
 # build_variant.sh NAME [-DFLAG ...]: the product library with extra defines,
 # into scratch/NAME.so (gitignored, travels to the GPU box) for A/B runs
-# selected with POSECNN_HIP_LIB.
+# selected with POSECNN_HIP_LIB.  REV=<git rev> builds that revision's
+# sources instead of the working tree (e.g. REV=HEAD for a before/after A/B).
 set -e
 cd "$(dirname "$0")/.."
 name=$1; shift
 mkdir -p scratch/$name.obj
 C=posecnn_amd/csrc
+if [ -n "$REV" ]; then
+  src=scratch/$name.src; rm -rf $src; mkdir -p $src
+  git archive "$REV" posecnn_amd/csrc include | tar -x -C $src
+  C=$src/posecnn_amd/csrc
+fi
 pids=""
 for f in capi hough_compact hough_vote hough_peak hough_emit roi_pooling average_distance backprojecting pose_head box_nms label_producer; do
   extra=""; [ $f = pose_head ] && extra="-fno-slp-vectorize"
@@ -16,4 +22,4 @@ for f in capi hough_compact hough_vote hough_peak hough_emit roi_pooling average
 done
 for p in $pids; do wait $p; done
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o scratch/$name.so scratch/$name.obj/*.o
-rm -rf scratch/$name.obj
+rm -rf scratch/$name.obj scratch/$name.src

@@ -11,6 +11,8 @@
 #   sq                  SQ instruction / stall counters of the eager step (two passes)
 #   ab V1,V2,...        alternating bench of the tree vs scratch/V.so (scripts/build_variant.sh)
 #   micro NAME          scripts/NAME.py microbench (gemm_bench, roi_bench, hough_bench, label_bench, pcie_rate)
+#   microab NAME V1,... alternating scripts/NAME.py runs of the tree vs scratch/V.so (two rounds)
+#   sqmicro NAME ARGS V1,...  the two SQ counter passes over scripts/NAME.py ARGS, tree and each scratch/V.so
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 O=$R/gpurun_out
 mkdir -p $O
@@ -26,7 +28,7 @@ while [ $# -gt 0 ]; do
   case $task in
     test)
       args=(tests)
-      if [ $# -gt 0 ] && [[ $1 != test && $1 != smoke && $1 != bench && $1 != prof && $1 != pmc && $1 != sq && $1 != ab && $1 != micro ]]; then
+      if [ $# -gt 0 ] && [[ $1 != test && $1 != smoke && $1 != bench && $1 != prof && $1 != pmc && $1 != sq && $1 != ab && $1 != micro && $1 != microab && $1 != sqmicro ]]; then
         args=($1); shift
       fi
       timeout -k 10 900 python -u -m pytest "${args[@]}" -m gpu -x -v --timeout 120 --timeout-method thread \
@@ -61,6 +63,27 @@ while [ $# -gt 0 ]; do
           POSECNN_HIP_LIB=$L timeout -k 10 300 python bench.py --no-cpu-baseline --steps 30 2>/dev/null | \
             python -c "import json,sys; d=json.load(sys.stdin); print('$v', d['value'], d['timing_ms_per_step'])" \
             >> $O/ab_lib.log || exit 1
+        done
+      done ;;
+    microab)
+      n=$1; IFS=, read -ra vs <<< "$2"; shift 2
+      : > $O/${n}_ab.log
+      for i in 1 2; do
+        for v in tree "${vs[@]}"; do
+          L=$R/posecnn_amd/libposecnn_hip.so; [ $v = tree ] || L=$R/scratch/$v.so
+          echo "== $v" >> $O/${n}_ab.log
+          POSECNN_HIP_LIB=$L timeout -k 10 300 python scripts/$n.py >> $O/${n}_ab.log 2>&1 || exit 1
+        done
+      done ;;
+    sqmicro)
+      n=$1; margs=$2; IFS=, read -ra vs <<< "$3"; shift 3
+      for v in tree "${vs[@]}"; do
+        L=$R/posecnn_amd/libposecnn_hip.so; [ $v = tree ] || L=$R/scratch/$v.so
+        for pass in 1 2; do
+          if [ $pass = 1 ]; then C="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM"
+          else C="SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_SALU GRBM_GUI_ACTIVE SQ_WAVES"; fi
+          (cd /tmp && POSECNN_HIP_LIB=$L timeout -s KILL 180 rocprofv3 --pmc $C --kernel-trace --output-format csv \
+             -d $O/sq_${v}_$pass -o run -- python3 $R/scripts/$n.py $margs > $O/sq_${v}_$pass.log 2>&1) || exit 1
         done
       done ;;
     micro)

@@ -74,9 +74,10 @@ def test_workspace_sizing(lib):
     assert 0 < a < b and c > a
     assert lib.pcnn_roi_pool_bwd_workspace_size(8, 1152) > 0
     assert lib.pcnn_add_loss_workspace_size(1152, 22, 2620) >= 1152 * 4
-    # GEMM: split-K slabs only when the tile count is small; fp32 / split-bf16 rules
-    big = lib.pcnn_gemm_workspace_size(1152, 4096, 25088, 1, 1)
-    assert big >= 8 * 1152 * 4096 * 4
+    # GEMM: split-K slabs only when the tile count is small (both precisions);
+    # the weight-gradient shapes run whole tiles
+    assert lib.pcnn_gemm_workspace_size(1152, 4096, 25088, 1, 0) >= 2 * 1152 * 4096 * 4
+    assert lib.pcnn_gemm_workspace_size(1152, 4096, 25088, 1, 1) >= 8 * 1152 * 4096 * 4
     assert lib.pcnn_gemm_workspace_size(25088, 4096, 1152, 0, 1) == 256
     assert lib.pcnn_gemm_workspace_size(0, 4096, 25088, 0, 0) == 256
 

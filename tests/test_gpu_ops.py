@@ -321,6 +321,27 @@ def test_gemm_weight_grad_unsplit(hip):
     np.testing.assert_allclose(C.cpu().numpy(), ref, **_gemm_tol(1, 405))
 
 
+@pytest.mark.parametrize("bt", [0, 1])
+def test_gemm_live_row_blocks(hip, bt):
+    """Device-side row counts that leave every number (0-4) of live 32-row
+    accumulator blocks in a wave's half of a 256-row tile (the K loop is
+    specialised on that count): fc7-like capacity shape, bias + relu + mask."""
+    rng = np.random.default_rng(11)
+    M, N, K = 1152, 512, 640
+    A = rng.normal(size=(M, K)).astype(np.float32)
+    B = rng.normal(size=(K, N)).astype(np.float32)
+    bias = rng.normal(size=N).astype(np.float32)
+    mask = rng.normal(size=(M, N)).astype(np.float32)
+    tA, tB = T(A), T(B.T.copy() if bt else B)
+    for live in (1, 31, 33, 70, 100, 128, 129, 200, 257, 290, 333, 405, 449, 511, 512, 700, 1152):
+        Mdev = torch.tensor([live], dtype=torch.int32, device=D)
+        C = torch.zeros((M, N), dtype=torch.float32, device=D)
+        ph.gemm(tA, tB, C, b_trans=bt, bias=T(bias), act=1, mask=T(mask), M_dev=Mdev, precision=1)
+        ref = np.maximum(A[:live].astype(np.float64) @ B + bias, 0) * (mask[:live] > 0)
+        np.testing.assert_allclose(C[:live].cpu().numpy(), ref, err_msg=f"live={live}", **_gemm_tol(1, K))
+        assert not C[live:].cpu().numpy().any(), live
+
+
 @pytest.mark.parametrize("prec", [0, 1])
 @pytest.mark.parametrize("at,bt", [(0, 0), (0, 1), (1, 0), (1, 1)])
 def test_gemm_ragged_padded(hip, at, bt, prec):
