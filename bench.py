@@ -14,7 +14,10 @@ all-reduces and the row-block reduction of the fc6/fc7/fc8 weight gradients
 
 A step = one pass over one batch; inputs are resident in HBM before timing.
 Prints ONE JSON line (rank 0).  --workload vote_roi times configs[1]
-(hough_voting_gpu + 2x roi_pool forward, B = 1, test mode) instead.
+(hough_voting_gpu + 2x roi_pool forward, B = 1, test mode) instead;
+--workload linemod times configs[4] per rank: LINEMOD C = 16, 4 objects per
+frame, the configs[2] step plus backproject forward + backward (G = 64,
+Ch = 64, NC = 16, kernel_size 1, threshold 0.02).
 """
 import argparse
 import json
@@ -35,7 +38,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=5)
-    p.add_argument("--workload", choices=["full", "vote_roi"], default="full")
+    p.add_argument("--workload", choices=["full", "vote_roi", "linemod"], default="full")
     p.add_argument("--batch", type=int, default=0, help="images per rank (default 8 full / 1 vote_roi)")
     p.add_argument("--classes", type=int, default=22)
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -71,14 +74,22 @@ def main():
     from posecnn_amd.roi_pooling_layer import roi_pooling_op as rp
     _lib.load()  # fails loudly without the HIP library
 
-    full = args.workload == "full"
+    linemod = args.workload == "linemod"
+    full = args.workload in ("full", "linemod")
     B = args.batch or (8 if full else 1)
-    C = args.classes
+    C = 16 if linemod else args.classes
     H, W = 480, 640
     gB = B * world
-    seed = 3 if full else 2  # configs[2] / configs[1] (seed = config index)
+    # seed = config index: configs[2] / configs[1] / configs[4]
+    seed = 5 if linemod else (3 if full else 2)
     t0 = time.time()
-    fr = synth.make_frames(B, H, W, num_classes=C, objects_per_image=6, seed=seed, image_offset=rank * B)
+    if linemod:
+        G_BP, CH_BP = 64, 64
+        voxel = ([2.0 / G_BP, 1.5 / G_BP, 1.7 / G_BP], [-1.0, -0.75, 0.4])
+        fr = synth.make_frames(B, H, W, num_classes=C, objects_per_image=4, seed=seed, image_offset=rank * B,
+                               extents=synth.models()["linemod_extents"], with_depth=True, voxel=voxel)
+    else:
+        fr = synth.make_frames(B, H, W, num_classes=C, objects_per_image=6, seed=seed, image_offset=rank * B)
     log(f"[rank {rank}] synthetic frames in {time.time() - t0:.1f}s")
     g = torch.Generator(device=dev)
     g.manual_seed(1234 + rank)
@@ -87,13 +98,27 @@ def main():
                   gt=to(fr["gt"]),
                   conv4=torch.randn((B, H // 8, W // 8, 512), generator=g, device=dev),
                   conv5=torch.randn((B, H // 16, W // 16, 512), generator=g, device=dev))
-    pts, sym = synth.rescaled_points(C)
+    pts, sym = synth.linemod_points() if linemod else synth.rescaled_points(C)
     inputs["points"], inputs["symmetry"] = to(pts), to(sym)
 
     if full:
         step = PoseStep(B, H, W, C, dev, is_train=1, skip_pixels=10, global_batch=gB, batch_base=rank * B,
                         dist=dist, precision=args.precision)
         run = lambda: step.step(inputs)
+    if linemod:  # + the depth back-projection op, forward and backward (no reference caller)
+        from posecnn_amd.backprojecting_layer import backprojecting_op as bpo
+        bp_in = dict(data=torch.randn((B, H, W, CH_BP), generator=g, device=dev),
+                     label=torch.rand((B, H, W, C), generator=g, device=dev),
+                     depth=to(fr["depth"]), label3d=torch.rand((B, G_BP, G_BP, G_BP, C), generator=g, device=dev),
+                     grad=torch.randn((B, G_BP, G_BP, G_BP, CH_BP), generator=g, device=dev))
+
+        def run():
+            step.step(inputs)
+            with step._t("backproject_fwd"):
+                bpo.backproject(bp_in["data"], bp_in["label"], bp_in["depth"], inputs["meta"], bp_in["label3d"],
+                                G_BP, 1, 0.02)
+            with step._t("backproject_bwd"):
+                bpo.backproject_grad(bp_in["data"], bp_in["depth"], inputs["meta"], bp_in["grad"], G_BP, 1, 0.02)
     else:
         hout = {}
         pool = {}
@@ -186,7 +211,7 @@ def main():
     # reported beside the line (the split-bf16 x3 GEMMs are fp32-class, not
     # fp32-rounded; the reference runs these layers as fp32 matmuls)
     fp32_leg = None
-    if full and world == 1 and args.precision == 1 and not args.no_fp32_leg:
+    if args.workload == "full" and world == 1 and args.precision == 1 and not args.no_fp32_leg:
         step0 = PoseStep(B, H, W, C, dev, is_train=1, skip_pixels=10, global_batch=gB, batch_base=rank * B,
                          dist=dist, precision=0, weights=step.weights)
         run0 = lambda: step0.step(inputs)
@@ -236,7 +261,7 @@ def main():
     if os.path.exists(pmc_path):
         try:
             pmc = json.load(open(pmc_path))
-            wl = pmc.get("full" if full else "vote_roi", {})
+            wl = pmc.get(args.workload, {})
             if roof is not None and full and args.precision == 1:
                 ent = wl.get(f"k_gemm_x3:{dom.replace('gemm_', '')}")
                 if ent:
@@ -249,7 +274,7 @@ def main():
             log(f"pmc traffic unavailable: {e}")
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not linemod:
         cpu = cpu_baseline(fr, full, args.cpu_seconds)
 
     if rank == 0:
@@ -269,9 +294,12 @@ def main():
             "vs_baseline": None,
             "dtype": "f32 (FC GEMMs split-bf16x3 MFMA, fp32 accumulate)" if args.precision == 1 else "f32",
             "data": "synthetic (seeded label/vertex maps per minibatch.py:517-575; random conv4_3/conv5_3; "
-                    "random-init FC weights)",
+                    "random-init FC weights" + ("; LINEMOD box-surface model points, rendered box depth, random "
+                                                "backprojection features" if linemod else "") + ")",
             "config": {
-                "workload": ("configs[2]/[3]: hough_voting_gpu(train) + roi_pool x2 + fc6/7/8 + l2norm + "
+                "workload": ("configs[4]: LINEMOD 15-class hough_voting_gpu(train) + roi_pool x2 + fc6/7/8 + "
+                             "l2norm + average_distance_loss fwd/bwd + backproject fwd/bwd (G=64, Ch=64)" if linemod
+                             else "configs[2]/[3]: hough_voting_gpu(train) + roi_pool x2 + fc6/7/8 + l2norm + "
                              "average_distance_loss fwd/bwd" if full else
                              "configs[1]: hough_voting_gpu(test) + roi_pool x2 forward"),
                 "global_batch": gB, "per_rank_batch": B, "height": H, "width": W, "num_classes": C,

@@ -10,7 +10,9 @@
 // c == 0 thread only, cu.cc:62-66, :88-93, which also races with the other
 // channel threads' writes of the same voxel); per-channel summation order over
 // the neighbourhood (x outer, y inner) is the reference's.
-// The output is write-bound: B*G^3*(2Ch+NC)*4 bytes.
+// The output is write-bound: B*G^3*(2Ch+NC)*4 bytes.  These scalar kernels
+// serve channel counts that are not multiples of 4; the step's sizes take
+// the vector forms below.
 #include "pcnn_common.h"
 #include <math.h>
 
@@ -100,6 +102,129 @@ __global__ void __launch_bounds__(256) k_bp_bwd(const float* __restrict__ top_di
   }
 }
 
+// Vector forms (Ch and NC multiples of 4, at most 256): a voxel (forward) or
+// pixel (backward) owns LPV lanes, one float4 of channels each, so a
+// wave-instruction moves LPV * 16 bytes of one row and 64 / LPV rows at
+// once; 32-bit indexing, no 64-bit div/mod.  Per channel the neighbourhood
+// sum runs in the same (x outer, y inner) order as the scalar kernel, so
+// results are bitwise the same.
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+// KS >= 0: the neighbourhood size at compile time, so its (2KS+1)^2 depth
+// reads issue together (one memory round trip per voxel, not one per
+// neighbour); KS < 0: runtime kernel size.
+template <int KS>
+__global__ void __launch_bounds__(256) k_bp_fwd4(const f4* __restrict__ data, const f4* __restrict__ label,
+                                                  const float* __restrict__ depth, const float* __restrict__ meta,
+                                                  int num_meta, const f4* __restrict__ label_3d, int B, int H, int W,
+                                                  int Ch4, int NC4, int G, int ks_rt, float threshold, int lpv_log2,
+                                                  f4* __restrict__ top_data, f4* __restrict__ top_label,
+                                                  f4* __restrict__ top_flag) {
+  const int ks = KS >= 0 ? KS : ks_rt;
+  const int lane = threadIdx.x & 63;
+  const int sub = lane >> lpv_log2, cq = lane & ((1 << lpv_log2) - 1);
+  const int vpw = 64 >> lpv_log2;
+  const int GG = G * G, G3 = GG * G, nvox = B * G3;
+  const int wv = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = (gridDim.x * blockDim.x) >> 6;
+  for (int v0 = wv * vpw; v0 < nvox; v0 += nw * vpw) {
+    const int vox = v0 + sub;
+    if (vox >= nvox) continue;
+    const int n = vox / G3, r3 = vox - n * G3, d = r3 / GG, r2 = r3 - d * GG, h = r2 / G, w = r2 - h * G;
+    const float* m = meta + (size_t)n * num_meta;
+    // voxel centre -> live frame -> image (cu.cc:43-60)
+    const float X = (float)d * m[42] + m[45];
+    const float Y = (float)h * m[43] + m[46];
+    const float Z = (float)w * m[44] + m[47];
+    const float X1 = m[18] * X + m[19] * Y + m[20] * Z + m[21];
+    const float Y1 = m[22] * X + m[23] * Y + m[24] * Z + m[25];
+    const float Z1 = m[26] * X + m[27] * Y + m[28] * Z + m[29];
+    const float x1 = m[0] * X1 + m[1] * Y1 + m[2] * Z1;
+    const float x2 = m[3] * X1 + m[4] * Y1 + m[5] * Z1;
+    const float x3 = m[6] * X1 + m[7] * Y1 + m[8] * Z1;
+    const int px = (int)roundf(x1 / x3);
+    const int py = (int)roundf(x2 / x3);
+    const bool do_data = cq < Ch4, do_label = cq < NC4;
+    f4 sd = {0.f, 0.f, 0.f, 0.f}, sl = {0.f, 0.f, 0.f, 0.f};
+    int count = 0;
+    auto visit = [&](int x, int y, bool hit) {
+      if (hit) {
+        const int ip = (n * H + y) * W + x;
+        count++;
+        if (do_data) sd += data[(size_t)ip * Ch4 + cq];
+        if (do_label) sl += label[(size_t)ip * NC4 + cq];
+      }
+    };
+    if constexpr (KS >= 0) {
+      constexpr int S = 2 * KS + 1;
+      bool hit[S * S];
+#pragma unroll
+      for (int i = 0; i < S * S; i++) {  // all depth reads first
+        const int x = px - KS + i / S, y = py - KS + i % S;
+        const bool in = x >= 0 && x < W && y >= 0 && y < H;
+        const float dep = depth[in ? (n * H + y) * W + x : 0];
+        hit[i] = in && fabsf(dep - Z1) < threshold;  // cu.cc:79
+      }
+#pragma unroll
+      for (int i = 0; i < S * S; i++) visit(px - KS + i / S, py - KS + i % S, hit[i]);  // x outer, y inner
+    } else {
+      for (int x = px - ks; x <= px + ks; x++)
+        for (int y = py - ks; y <= py + ks; y++) {
+          const bool in = x >= 0 && x < W && y >= 0 && y < H;
+          visit(x, y, in && fabsf(depth[in ? (n * H + y) * W + x : 0] - Z1) < threshold);
+        }
+    }
+    if (do_data) {
+      const float cf = (float)count;
+      top_data[(size_t)vox * Ch4 + cq] = count ? sd / cf : (f4){0.f, 0.f, 0.f, 0.f};
+      const float fl = count ? 1.f : 0.f;
+      top_flag[(size_t)vox * Ch4 + cq] = (f4){fl, fl, fl, fl};
+    }
+    if (do_label)
+      top_label[(size_t)vox * NC4 + cq] = count ? sl / (float)count : label_3d[(size_t)vox * NC4 + cq];
+  }
+}
+
+__global__ void __launch_bounds__(256) k_bp_bwd4(const f4* __restrict__ top_diff, const float* __restrict__ depth,
+                                                  const float* __restrict__ meta, int num_meta, int B, int H, int W,
+                                                  int Ch4, int G, int lpv_log2, f4* __restrict__ bottom_diff) {
+  const int lane = threadIdx.x & 63;
+  const int sub = lane >> lpv_log2, cq = lane & ((1 << lpv_log2) - 1);
+  const int ppw = 64 >> lpv_log2;
+  const int HW = H * W, npix = B * HW;
+  const int wv = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = (gridDim.x * blockDim.x) >> 6;
+  for (int p0 = wv * ppw; p0 < npix; p0 += nw * ppw) {
+    const int pix = p0 + sub;
+    if (pix >= npix || cq >= Ch4) continue;
+    const int n = pix / HW, r = pix - n * HW, h = r / W, w = r - h * W;
+    const float* m = meta + (size_t)n * num_meta;
+    const float dep = depth[pix];
+    // pixel -> camera ray (Kinv) -> live2world -> voxel (cu.cc:188-210)
+    const float RX = m[9] * (float)w + m[10] * (float)h + m[11];
+    const float RY = m[12] * (float)w + m[13] * (float)h + m[14];
+    const float RZ = m[15] * (float)w + m[16] * (float)h + m[17];
+    const float X = dep * RX, Y = dep * RY, Z = dep * RZ;
+    const float X1 = m[30] * X + m[31] * Y + m[32] * Z + m[33];
+    const float Y1 = m[34] * X + m[35] * Y + m[36] * Z + m[37];
+    const float Z1 = m[38] * X + m[39] * Y + m[40] * Z + m[41];
+    const int vd = (int)roundf((X1 - m[45]) / m[42]);
+    const int vh = (int)roundf((Y1 - m[46]) / m[43]);
+    const int vw = (int)roundf((Z1 - m[47]) / m[44]);
+    f4 g = {0.f, 0.f, 0.f, 0.f};
+    if (vd >= 0 && vd < G && vh >= 0 && vh < G && vw >= 0 && vw < G)
+      g = top_diff[((((size_t)n * G + vd) * G + vh) * G + vw) * Ch4 + cq];
+    bottom_diff[(size_t)pix * Ch4 + cq] = g;
+  }
+}
+
+static int lpv_log2_for(int c4) {  // lanes per row: the smallest power of two >= c4 (c4 <= 64)
+  int l = 0;
+  while ((1 << l) < c4) l++;
+  return l;
+}
+static bool bp_vec_ok(const void* a, const void* b, int ch) {
+  return ch % 4 == 0 && ch <= 256 && ((((uintptr_t)a) | ((uintptr_t)b)) & 15) == 0;
+}
+
 }  // namespace
 
 extern "C" int pcnn_backproject_fwd(const float* data, const float* label, const float* depth, const float* meta,
@@ -109,7 +234,25 @@ extern "C" int pcnn_backproject_fwd(const float* data, const float* label, const
   PCNN_REQUIRE(data && label && depth && meta && label_3d && top_data && top_label && top_flag);
   PCNN_REQUIRE(B > 0 && H > 0 && W > 0 && Ch > 0 && NC > 0 && grid_size > 0 && kernel_size >= 0 && num_meta >= 48);
   const int CL = Ch > NC ? Ch : NC;
-  const long total = (long)B * grid_size * grid_size * grid_size * CL;
+  const long nvox = (long)B * grid_size * grid_size * grid_size;
+  if (bp_vec_ok(data, top_data, Ch) && bp_vec_ok(label, top_label, NC) && bp_vec_ok(label_3d, top_flag, NC) &&
+      nvox * (CL / 4) < (1l << 31) && (long)B * H * W < (1l << 31)) {
+    const int lg = lpv_log2_for(CL / 4);
+    const long waves = (nvox + (64 >> lg) - 1) / (64 >> lg);
+    const int blocks = (int)((waves + 3) / 4 < 65536 ? (waves + 3) / 4 : 65536);
+#define PCNN_BP_FWD4(KS)                                                                                     \
+  hipLaunchKernelGGL(k_bp_fwd4<KS>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const f4*)data,            \
+                     (const f4*)label, depth, meta, num_meta, (const f4*)label_3d, B, H, W, Ch / 4, NC / 4,      \
+                     grid_size, kernel_size, threshold, lg, (f4*)top_data, (f4*)top_label, (f4*)top_flag)
+    if (kernel_size == 0) PCNN_BP_FWD4(0);
+    else if (kernel_size == 1) PCNN_BP_FWD4(1);
+    else if (kernel_size == 2) PCNN_BP_FWD4(2);
+    else PCNN_BP_FWD4(-1);
+#undef PCNN_BP_FWD4
+    PCNN_CHECK_LAUNCH();
+    return PCNN_OK;
+  }
+  const long total = nvox * CL;
   const int blocks = (int)((total + 255) / 256 < 65536 ? (total + 255) / 256 : 65536);
   hipLaunchKernelGGL(k_bp_fwd, dim3(blocks), dim3(256), 0, (hipStream_t)stream, data, label, depth, meta, num_meta,
                      label_3d, B, H, W, Ch, NC, grid_size, kernel_size, threshold, CL, top_data, top_label, top_flag);
@@ -121,7 +264,17 @@ extern "C" int pcnn_backproject_bwd(const float* top_diff, const float* depth, c
                                     int H, int W, int Ch, int grid_size, float* bottom_diff, void* stream) {
   PCNN_REQUIRE(top_diff && depth && meta && bottom_diff && B > 0 && H > 0 && W > 0 && Ch > 0 && grid_size > 0);
   PCNN_REQUIRE(num_meta >= 48);
-  const long total = (long)B * H * W * Ch;
+  const long npix = (long)B * H * W;
+  if (bp_vec_ok(top_diff, bottom_diff, Ch) && npix * (Ch / 4) < (1l << 31)) {
+    const int lg = lpv_log2_for(Ch / 4);
+    const long waves = (npix + (64 >> lg) - 1) / (64 >> lg);
+    const int blocks = (int)((waves + 3) / 4 < 65536 ? (waves + 3) / 4 : 65536);
+    hipLaunchKernelGGL(k_bp_bwd4, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const f4*)top_diff, depth, meta,
+                       num_meta, B, H, W, Ch / 4, grid_size, lg, (f4*)bottom_diff);
+    PCNN_CHECK_LAUNCH();
+    return PCNN_OK;
+  }
+  const long total = npix * Ch;
   const int blocks = (int)((total + 255) / 256 < 65536 ? (total + 255) / 256 : 65536);
   hipLaunchKernelGGL(k_bp_bwd, dim3(blocks), dim3(256), 0, (hipStream_t)stream, top_diff, depth, meta, num_meta, B,
                      H, W, Ch, grid_size, bottom_diff);

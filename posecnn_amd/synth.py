@@ -170,3 +170,36 @@ def rescaled_points(num_classes=22, symmetric=True):
     if not symmetric:
         sym = np.zeros_like(sym)
     return pts.astype(np.float32), sym.astype(np.float32)
+
+
+def box_points(extents, P=2620, seed=0):
+    """(C, P, 3) model points for datasets whose meshes are not in the
+    reference (LINEMOD: only data/LINEMOD/extents.txt ships): P points spread
+    uniformly over each class's 3-D box surface (class 0, background, zero)."""
+    ext = np.asarray(extents, np.float64)
+    rng = np.random.default_rng(seed)
+    out = np.zeros((len(ext), P, 3), np.float32)
+    for c in range(1, len(ext)):
+        e = ext[c] / 2.0
+        areas = np.array([e[1] * e[2], e[0] * e[2], e[0] * e[1]])
+        face = rng.choice(3, size=P, p=areas / areas.sum())
+        pts = rng.uniform(-1.0, 1.0, size=(P, 3)) * e
+        side = np.where(rng.uniform(size=P) < 0.5, -1.0, 1.0)
+        pts[np.arange(P), face] = side * e[face]
+        out[c] = pts.astype(np.float32)
+    return out
+
+
+def linemod_points(P=2620, symmetric=True):
+    """LINEMOD (C = 16) model points on the class boxes, rescaled as
+    minibatch.py:50-60 does, and the symmetry vector (linemod.py:44)."""
+    mdl = models()
+    ext = mdl["linemod_extents"]
+    pts = box_points(ext, P, seed=16)
+    sym = mdl["linemod_symmetry"].copy()
+    for i in range(1, len(ext)):
+        w = max(2.0 / np.amax(ext[i]), 10.0)
+        pts[i] = (4 * w if sym[i] > 0 and symmetric else w) * pts[i]
+    if not symmetric:
+        sym = np.zeros_like(sym)
+    return pts.astype(np.float32), sym.astype(np.float32)

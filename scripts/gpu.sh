@@ -20,7 +20,7 @@ export TMPDIR=/tmp
 prof() {  # prof NAME STEPS WARMUP [bench args] (eager launches, one dispatch per kernel)
   local n=$1 s=$2 w=$3; shift 3
   (cd /tmp && timeout -k 10 600 rocprofv3 "${PMC[@]}" --kernel-trace --output-format csv -d $O/$n -o run -- \
-     python3 $R/bench.py --steps $s --warmup $w --no-cpu-baseline "$@" > $O/$n.log 2>&1)
+     python3 $R/bench.py --steps $s --warmup $w --no-cpu-baseline --no-fp32-leg "$@" > $O/$n.log 2>&1)
 }
 while [ $# -gt 0 ]; do
   task=$1; shift

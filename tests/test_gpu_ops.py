@@ -214,17 +214,21 @@ def test_add_loss_symmetric_large(hip, orc, P, near):
     np.testing.assert_allclose(diff.cpu().numpy(), od, rtol=1e-4, atol=1e-6 * np.abs(od).max())
 
 
-def test_backproject(hip, orc):
+@pytest.mark.parametrize("Ch,NC,ks", [(16, 5, 1), (12, 8, 1), (64, 16, 2), (20, 4, 0), (8, 8, 3)])
+def test_backproject(hip, orc, Ch, NC, ks):
+    """Scalar kernels (NC = 5) and the float4 vector forms (lanes per row 4 /
+    16 / 8 / 2), kernel sizes 0-2 (compile-time) and 3 (runtime), bit-exact
+    against the restated op."""
     rng = np.random.default_rng(4)
-    B, H, W, Ch, NC, G = 2, 48, 64, 16, 5, 12
+    B, H, W, G = 2, 48, 64, 12
     K = np.array([[80.0, 0, 32], [0, 80.0, 24], [0, 0, 1]])
     meta = synth.make_meta(K, B, voxel=([0.1, 0.08, 0.1], [-0.6, -0.48, 0.5]))
     depth = rng.uniform(0.5, 1.7, size=(B, H, W, 1)).astype(np.float32)
     data = rng.normal(size=(B, H, W, Ch)).astype(np.float32)
     label = rng.uniform(size=(B, H, W, NC)).astype(np.float32)
     l3 = rng.uniform(size=(B, G, G, G, NC)).astype(np.float32)
-    td, tl, tf = bp.backproject(T(data), T(label), T(depth), T(meta), T(l3), G, 1, 0.3)
-    od, ol, of = orc.backproject_fwd(data, label, depth, meta, l3, G, 1, 0.3)
+    td, tl, tf = bp.backproject(T(data), T(label), T(depth), T(meta), T(l3), G, ks, 0.3)
+    od, ol, of = orc.backproject_fwd(data, label, depth, meta, l3, G, ks, 0.3)
     np.testing.assert_array_equal(td.cpu().numpy(), od)
     np.testing.assert_array_equal(tl.cpu().numpy(), ol)
     np.testing.assert_array_equal(tf.cpu().numpy(), of)
