@@ -119,7 +119,7 @@ def main():
                                 G_BP, 1, 0.02)
             with step._t("backproject_bwd"):
                 bpo.backproject_grad(bp_in["data"], bp_in["depth"], inputs["meta"], bp_in["grad"], G_BP, 1, 0.02)
-    else:
+    if not full:  # vote_roi
         hout = {}
         pool = {}
 
