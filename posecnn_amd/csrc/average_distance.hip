@@ -31,7 +31,7 @@ constexpr int kSymLanes = ADD_LANES;           // symmetric rows: lanes per cand
 #define ADD_GRID 768
 #endif
 #ifndef ADD_PPL
-#define ADD_PPL 2
+#define ADD_PPL 4
 #endif
 constexpr int kPPL = ADD_PPL;                  // query points per lane (independent min chains)
 constexpr int kPts = kSymLanes * kPPL;         // query points per (row, chunk) item
@@ -131,11 +131,13 @@ __device__ __forceinline__ void add_plain_row(int n, const float* __restrict__ p
   }
 }
 
-// Symmetric rows: a 512-thread workgroup owns (row, chunk of kPts = 128 query
+// Symmetric rows: a 512-thread workgroup owns (row, chunk of kPts = 256 query
 // points); its eight one-wave groups scan disjoint eighths of the candidate
 // list for the same query points (the first-minimum update is a dependent
-// chain, so latency, not issue, bounds a lone wave: 8 waves per item, kPPL = 2
-// chains per lane, three items per CU), then merge in LDS in group order with a strict < —
+// chain, so latency, not issue, bounds a lone wave: 8 waves per item, kPPL = 4
+// chains per lane — each broadcast candidate read serves four distances: 155
+// -> 148 us against kPPL = 2 on the bench rows — three items per CU), then
+// merge in LDS in group order with a strict < —
 // a later range wins only with a strictly smaller distance, which is exactly
 // the reference's sequential first minimum (cu.cc:150-172).
 #ifndef ADD_GROUPS
