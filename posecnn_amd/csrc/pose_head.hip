@@ -48,6 +48,7 @@ struct GemmArgs {
   int prec;     // 0 fp32 MFMA, 1 split-bf16 x3 (selects the split rule)
   int tile;     // x3 tile edge (256 or 128), chosen on the host
   int xgrid;    // x3 launch grid (the plan depends on it; k_gemm_reduce re-derives the plan)
+  int c_stream; // x3: store C non-temporally (outputs far beyond the caches, e.g. the fc6 weight gradient)
 };
 
 __device__ __forceinline__ int eff_dim(int full, const int32_t* dev) {
@@ -376,6 +377,7 @@ __device__ __forceinline__ float x_ld1(const XOp& o, unsigned voff, int soff) {
   return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(o.rs, voff, soff, 0));
 }
 typedef float xf4 __attribute__((ext_vector_type(4)));
+constexpr int kXNonTemporal = 2;  // buffer cache-policy bit: nt
 __device__ __forceinline__ xf4 x_ld4(const XOp& o, unsigned voff, int soff) {
   return __builtin_bit_cast(xf4, __builtin_amdgcn_raw_buffer_load_b128(o.rs, voff, soff, 0));
 }
@@ -737,9 +739,11 @@ __global__ void __launch_bounds__(XTile<T>::threads, T == 256 ? 1 : 2) k_gemm_x3
 #ifdef PCNN_ABL_NOEPI
           if (v != 1.2345e-30f) continue;
 #endif
-          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), oc.rs,
-                                                ok ? cbase + (unsigned)((qrow(i, q) * g.ldc + j * EB) * 4) : kXOob,
-                                                0, 0);
+          const unsigned co = ok ? cbase + (unsigned)((qrow(i, q) * g.ldc + j * EB) * 4) : kXOob;
+          if (g.c_stream)  // non-temporal: the output is far larger than L2 + MALL
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), oc.rs, co, 0, kXNonTemporal);
+          else
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), oc.rs, co, 0, 0);
         }
       }
     }
@@ -912,7 +916,7 @@ extern "C" int pcnn_gemm(int M, int N, int K, const float* A, const float* A2, i
   if (workspace_bytes < pcnn_gemm_workspace_size(M, N, K, M_dev != nullptr, precision) || !workspace)
     return PCNN_ECAPACITY;
   GemmArgs g{M, N, K, A, A2, lda, B, ldb, Cm, ldc, bias, act, mask, ldm, M_dev, K_dev, (float*)workspace, precision,
-             tile_x3(M, N, K), 0};
+             tile_x3(M, N, K), 0, 0};
   hipStream_t st = (hipStream_t)stream;
   if (precision == 1) {
     // ragged edges: a KC operand whose K (or device-side K) is not a multiple of
@@ -941,6 +945,10 @@ extern "C" int pcnn_gemm(int M, int N, int K, const float* A, const float* A2, i
       }
     }
     g.xgrid = (int)grid;
+    // an output larger than the 256 MB MALL is written through without cache
+    // allocation (fc6 dW, 411 MB: 316 -> 300 us; the 64 MB fc7 dW and the
+    // small activations, re-read by the next GEMM, lose a little with it)
+    g.c_stream = (long)M * N * 4 > (256l << 20);
 #define PCNN_X3_LAUNCH_G(TT, AT, BT, RG, S2, GN)                                                              \
   do {                                                                                                          \
     static bool attr_set = false;                                                                               \

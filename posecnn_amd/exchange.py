@@ -124,6 +124,6 @@ class GradShard:
             if w is not None:
                 w.wait()
         din, dout = self.layers[name]
+        colsum(self.dy_all[name], gb)  # short launch ahead of the long dW GEMM
         gemm(self.x_recv[name], self.dy_all[name], gw_rows, a_trans=1, M=din // self.ws, N=dout,
              K=self.ws * self.slot)
-        colsum(self.dy_all[name], gb)

@@ -207,8 +207,10 @@ class PoseStep:
                 if gs is not None:
                     gs.reduce(name, g[name], g["b" + name[1:]], self._gemm, ph.colsum)
                 else:
-                    ph.gemm(X, dY, g[name], a_trans=1, K_dev=nr, M=M, N=N, K=K_loc, precision=self.prec)
+                    # the bias sum first: a short launch ahead of the long dW GEMM, not
+                    # a tail after it (fc6: it ran 44 us behind the dW, beside the pool bwd)
                     ph.colsum(dY, g["b" + name[1:]], M_dev=nr)
+                    ph.gemm(X, dY, g[name], a_trans=1, K_dev=nr, M=M, N=N, K=K_loc, precision=self.prec)
 
         with self._t("add_loss_head_bwd"):
             adl.average_distance_loss_grad(self.diff, self.one, num_rois=nr, out=self.dpred)
