@@ -223,6 +223,13 @@ def main():
         del step0
     elapsed = modes[mode]
     frames = gB * args.steps
+    # per-step distribution of the reported mode (after the timed region, which
+    # it does not touch): one HIP event pair per step (median and
+    # p10 / p90), and the practical HBM peak (device-to-device copy) beside the
+    # spec peak of the roofline
+    dist_steps = distribution(graph_replay if mode == "hipgraph" else run, min(max(args.steps, 20), 200))
+    dist_steps["mode"] = mode
+    practical = d2d_gbs(dev)
     value = frames / elapsed
     nrows = int((step.hough if step else hout["o"])["num_rois"][0].item())
 
@@ -237,7 +244,8 @@ def main():
         roof_vote = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
                      "kernel": "hough_voting_gpu op (label compaction + interval vote + peak + emit)",
-                     "bytes_per_launch": vote_bytes}
+                     "bytes_per_launch": vote_bytes, "practical_peak": practical,
+                     "frac_of_practical": round(ach / practical["GB/s"], 4)}
     if full and ops:
         R = max(nrows, 1)
         K6, U = 49 * 512, 4096
@@ -268,8 +276,12 @@ def main():
                     roof["traffic"] = round(ent["traffic_bytes"])
                     roof["traffic_unit"] = "bytes/launch (rocprofv3 2*FETCH_SIZE + WRITE_SIZE)"
             if roof_vote is not None and "hough_voting_gpu op" in wl:
-                roof_vote["traffic"] = round(wl["hough_voting_gpu op"]["traffic_bytes"])
+                hop = wl["hough_voting_gpu op"]
+                roof_vote["traffic"] = round(hop["traffic_bytes"])
                 roof_vote["traffic_unit"] = "bytes/launch (rocprofv3 2*FETCH_SIZE + WRITE_SIZE)"
+                if "valu_busy_pct" in hop:  # the voting limiter is VALU / LDS, not HBM
+                    roof_vote["valu_busy_pct"] = hop["valu_busy_pct"]
+                    roof_vote["valu_busy_vote_kernel_pct"] = wl.get("k_hough_vote", {}).get("valu_busy_pct")
         except Exception as e:  # pragma: no cover - a stale file must not break the bench
             log(f"pmc traffic unavailable: {e}")
 
@@ -313,12 +325,49 @@ def main():
             "ops_ms_per_step": {k: round(v, 4) for k, v in ops.items()},
             "timing": mode,
             "timing_ms_per_step": {k: round(v / args.steps * 1e3, 4) for k, v in modes.items()},
+            "step_ms_distribution": dist_steps,
+            "hbm_practical_peak": practical,
             "cpu_baseline": cpu,
             "fp32_mfma_step": fp32_leg,
         }
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+def distribution(fn, n):
+    """ms per step of n single steps, each between its own HIP event pair on
+    the current stream (the step joins its side stream before it ends)."""
+    import numpy as np
+    import torch
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n)]
+    for a, b in evs:
+        a.record()
+        fn()
+        b.record()
+    torch.cuda.synchronize()
+    t = np.array([a.elapsed_time(b) for a, b in evs])
+    return {"median": round(float(np.median(t)), 4), "p10": round(float(np.percentile(t, 10)), 4),
+            "p90": round(float(np.percentile(t, 90)), 4), "n": n}
+
+
+def d2d_gbs(dev, nbytes=1 << 30, reps=5):
+    """Measured device-to-device copy rate (read + write bytes / time): the
+    practical HBM peak reported next to the 8 TB/s spec."""
+    import torch
+    src = torch.empty(nbytes // 4, dtype=torch.float32, device=dev)
+    dst = torch.empty_like(src)
+    dst.copy_(src)
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(reps):
+        dst.copy_(src)
+    b.record()
+    torch.cuda.synchronize()
+    gbs = 2.0 * nbytes * reps / (a.elapsed_time(b) / 1e3) / 1e9
+    del src, dst
+    return {"GB/s": round(gbs, 1), "method": f"torch copy_ D2D of {nbytes >> 20} MiB x{reps} (read + write bytes)"}
 
 
 def cpu_baseline(fr, train, budget_s):

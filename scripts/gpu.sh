@@ -7,7 +7,7 @@
 #   smoke               __graft_entry__.smoke()
 #   bench               default bench line (configs[2]) + vote_roi (configs[1])
 #   prof                rocprofv3 --kernel-trace --stats of the eager and graph steps
-#   pmc                 FETCH_SIZE / WRITE_SIZE passes -> profiles/pmc_traffic.json
+#   pmc                 FETCH_SIZE / WRITE_SIZE / VALUBusy passes -> profiles/pmc_traffic.json
 #   sq                  SQ instruction / stall counters of the eager step (two passes)
 #   ab V1,V2,...        alternating bench of the tree vs scratch/V.so (scripts/build_variant.sh)
 #   micro NAME          scripts/NAME.py microbench (gemm_bench, roi_bench, hough_bench, label_bench, pcie_rate)
@@ -48,6 +48,8 @@ while [ $# -gt 0 ]; do
       PMC=(--pmc WRITE_SIZE); prof pmc_write 4 2 --no-graph || exit 1
       PMC=(--pmc FETCH_SIZE); prof pmc_fetch_vr 20 2 --workload vote_roi --no-graph || exit 1
       PMC=(--pmc WRITE_SIZE); prof pmc_write_vr 20 2 --workload vote_roi --no-graph || exit 1
+      PMC=(--pmc VALUBusy); prof pmc_valu 4 2 --no-graph || exit 1
+      PMC=(--pmc VALUBusy); prof pmc_valu_vr 20 2 --workload vote_roi --no-graph || exit 1
       python scripts/pmc_traffic.py gpurun_out > $O/pmc_traffic.txt && cp profiles/pmc_traffic.json $O/ || exit 1 ;;
     sq)
       PMC=(--pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM)

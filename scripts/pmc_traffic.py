@@ -1,5 +1,5 @@
-"""Per-launch HBM traffic from rocprofv3 FETCH_SIZE / WRITE_SIZE passes
-(scripts/gpu.sh pmc) -> profiles/pmc_traffic.json.
+"""Per-launch HBM traffic from rocprofv3 FETCH_SIZE / WRITE_SIZE passes, plus
+the VALUBusy of the voting kernels (scripts/gpu.sh pmc) -> profiles/pmc_traffic.json.
 
 FETCH_SIZE / WRITE_SIZE are in KiB per dispatch.  On gfx950 FETCH_SIZE
 counts half the bytes of wide coalesced reads (MI355X_MICROARCH.md, HBM
@@ -67,18 +67,45 @@ def summarize(fetch_csv, write_csv):
     return out
 
 
+def valu_busy(path):
+    """{kernel: mean rocprofv3 VALUBusy %} and the duration-weighted mean over
+    the Hough op's kernels (derived metric, gfx94x formula on ROCm 7.2)."""
+    if not os.path.exists(path):
+        return None
+    per, dur = defaultdict(list), defaultdict(list)
+    for row in csv.DictReader(open(path)):
+        if row["Counter_Name"] != "VALUBusy":
+            continue
+        k = short(row["Kernel_Name"])
+        per[k].append(float(row["Counter_Value"]))
+        dur[k].append(int(row["End_Timestamp"]) - int(row["Start_Timestamp"]))
+    out = {k: sum(v) / len(v) for k, v in per.items()}
+    hk = [k for k in HOUGH if k in out]
+    if hk:
+        tot = sum(sum(dur[k]) / len(dur[k]) for k in hk)
+        out["hough_voting_gpu op"] = sum(out[k] * sum(dur[k]) / len(dur[k]) for k in hk) / tot
+    return out
+
+
 def main():
     root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out"
     res = {"full": summarize(f"{root}/pmc_fetch/run_counter_collection.csv",
                              f"{root}/pmc_write/run_counter_collection.csv"),
            "vote_roi": summarize(f"{root}/pmc_fetch_vr/run_counter_collection.csv",
                                  f"{root}/pmc_write_vr/run_counter_collection.csv"),
-           "note": "bytes per launch; read = 2 x FETCH_SIZE (gfx950 half-count), write = WRITE_SIZE"}
+           "note": "bytes per launch; read = 2 x FETCH_SIZE (gfx950 half-count), write = WRITE_SIZE; "
+                   "valu_busy_pct = rocprofv3 VALUBusy (derived, gfx94x formula), duration-weighted over the op"}
+    for wl, d in (("full", "pmc_valu"), ("vote_roi", "pmc_valu_vr")):
+        vb = valu_busy(f"{root}/{d}/run_counter_collection.csv")
+        for k, v in (vb or {}).items():
+            if k in res[wl]:
+                res[wl][k]["valu_busy_pct"] = round(v, 2)
     os.makedirs("profiles", exist_ok=True)
     json.dump(res, open("profiles/pmc_traffic.json", "w"), indent=1, sort_keys=True)
     for wl in ("full", "vote_roi"):
         for k, v in sorted(res[wl].items(), key=lambda kv: -kv[1]["traffic_bytes"])[:14]:
-            print(wl, k.ljust(40), f"{v['traffic_bytes'] / 1e6:10.2f} MB")
+            vb = f"  VALUBusy {v['valu_busy_pct']:.1f} %" if "valu_busy_pct" in v else ""
+            print(wl, k.ljust(40), f"{v['traffic_bytes'] / 1e6:10.2f} MB{vb}")
 
 
 if __name__ == "__main__":
