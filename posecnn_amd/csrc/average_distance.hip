@@ -20,6 +20,7 @@
 // ~1e-6 relative).
 #include "pcnn_common.h"
 #include <cfloat>
+#include <type_traits>
 
 namespace {
 
@@ -184,7 +185,19 @@ __global__ void __launch_bounds__(kSymThreads) k_add_rows(const float* __restric
                   nchunk, rcls, partial, red);
     continue;  // the loop head synchronises before red is reused
   }
-  const int n = sym_rows[item / nchunk], chunk = item % nchunk;
+  // full chunks of every symmetric row first, the rows' short last chunks
+  // (P % kPts points: cheaper, see the scan below) after them, so the short
+  // ones fill the tail of the queue instead of opening a second round of
+  // full-cost items
+  const int nfull = P / kPts, nsym_rows = *nsym;
+  int n, chunk;
+  if (item < nsym_rows * nfull) {
+    n = sym_rows[item / nfull];
+    chunk = item % nfull;
+  } else {
+    n = sym_rows[item - nsym_rows * nfull];
+    chunk = nfull;
+  }
   const int PC = 4 * C;
   const int cls = rcls[n];
   float* out = partial + ((size_t)n * nchunk + chunk) * 5;
@@ -242,35 +255,43 @@ __global__ void __launch_bounds__(kSymThreads) k_add_rows(const float* __restric
     py[h] = (f2){qy[2 * h], qy[2 * h + 1]};
     pz[h] = (f2){qz[2 * h], qz[2 * h + 1]};
   }
-  int i = c0;
-  for (; i + 4 <= c1; i += 4) {
-    float4 c[4];
+  // NP query pairs per lane: an item whose queries fit in the first
+  // 2 * kSymLanes lanes' slots (a row's short last chunk) scans with one pair
+  auto scan = [&](auto np_c) {
+    constexpr int NP = decltype(np_c)::value;
+    int i = c0;
+    for (; i + 4 <= c1; i += 4) {
+      float4 c[4];
 #pragma unroll
-    for (int j = 0; j < 4; j++) c[j] = gpts[i + j];
+      for (int j = 0; j < 4; j++) c[j] = gpts[i + j];
 #pragma unroll
-    for (int h = 0; h < kPPL / 2; h++) {
-      f2 d[4];
+      for (int h = 0; h < NP; h++) {
+        f2 d[4];
 #pragma unroll
-      for (int j = 0; j < 4; j++) {
-        const f2 ex = px[h] - c[j].x, ey = py[h] - c[j].y, ez = pz[h] - c[j].z;
-        d[j] = ex * ex + ey * ey + ez * ez;
-      }
+        for (int j = 0; j < 4; j++) {
+          const f2 ex = px[h] - c[j].x, ey = py[h] - c[j].y, ez = pz[h] - c[j].z;
+          d[j] = ex * ex + ey * ey + ez * ez;
+        }
 #pragma unroll
-      for (int e = 0; e < 2; e++) {
-        const int k = 2 * h + e;
-        const float bm = fminf(fminf(d[0][e], d[1][e]), fminf(d[2][e], d[3][e]));
-        if (bm < dmin[k]) { dmin[k] = bm; iblk[k] = i; }
+        for (int e = 0; e < 2; e++) {
+          const int k = 2 * h + e;
+          const float bm = fminf(fminf(d[0][e], d[1][e]), fminf(d[2][e], d[3][e]));
+          if (bm < dmin[k]) { dmin[k] = bm; iblk[k] = i; }
+        }
       }
     }
-  }
-  for (; i < c1; i++) {  // ragged tail: blocks of one
-    const float4 c = gpts[i];
+    for (; i < c1; i++) {  // ragged tail: blocks of one
+      const float4 c = gpts[i];
 #pragma unroll
-    for (int k = 0; k < kPPL; k++) {
-      const float d = dist_to(k, c);
-      if (d < dmin[k]) { dmin[k] = d; iblk[k] = i; }
+      for (int k = 0; k < 2 * NP; k++) {
+        const float d = dist_to(k, c);
+        if (d < dmin[k]) { dmin[k] = d; iblk[k] = i; }
+      }
     }
-  }
+  };
+  const int nq = min(kPts, P - chunk * kPts);  // query points of this item
+  if (nq > 2 * kSymLanes) scan(std::integral_constant<int, kPPL / 2>{});
+  else scan(std::integral_constant<int, 1>{});
   if (grp > 0) {
 #pragma unroll
     for (int k = 0; k < kPPL; k++) {

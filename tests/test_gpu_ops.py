@@ -186,11 +186,14 @@ def test_add_loss_symmetric_ties(hip, orc):
     np.testing.assert_allclose(diff.cpu().numpy(), od, rtol=1e-4, atol=1e-6 * np.abs(od).max())
 
 
-@pytest.mark.parametrize("P,near", [(4096, True), (4096, False), (2620, True), (4200, False), (700, True)])
+@pytest.mark.parametrize("P,near", [(4096, True), (4096, False), (2620, True), (4200, False), (700, True),
+                                    (100, True), (300, False), (512, True)])
 def test_add_loss_symmetric_large(hip, orc, P, near):
     """ADD-S at up to 4200 model points: predictions near the target and
     arbitrary ones, duplicated model points and lattice coordinates (exact
-    distance ties), against the oracle's sequential first-minimum scan."""
+    distance ties), against the oracle's sequential first-minimum scan.  P
+    covers whole 256-point chunks only (4096, 512), a short last chunk of <= 128
+    points (the one-pair scan: 2620, 4200, 300, 100) and of > 128 (700)."""
     rng = np.random.default_rng(P + int(near))
     C, R = 3, 7
     pts = rng.normal(size=(C, P, 3)).astype(np.float32)
