@@ -122,17 +122,28 @@ def main():
     if not full:  # vote_roi
         hout = {}
         pool = {}
+        vr_timer = {}  # op -> [(event, event)] while the breakdown pass runs
+
+        def timed(name, fn):
+            if "on" not in vr_timer:
+                return fn()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            r = fn()
+            e1.record()
+            vr_timer.setdefault(name, []).append((e0, e1))
+            return r
 
         def run():
-            o = hv.hough_voting_gpu_capacity(inputs["label"], inputs["vertex"], inputs["extents"], inputs["meta"],
-                                             inputs["gt"], 0, -1.0, 0.02, 10, global_batch=gB, batch_base=rank * B,
-                                             out=hout.get("o"))
+            o = timed("hough_voting_gpu", lambda: hv.hough_voting_gpu_capacity(
+                inputs["label"], inputs["vertex"], inputs["extents"], inputs["meta"], inputs["gt"], 0, -1.0, 0.02, 10,
+                global_batch=gB, batch_base=rank * B, out=hout.get("o")))
             hout["o"] = o
             nr = o["num_rois"][1:2]
-            pool["p5"] = rp.roi_pool(inputs["conv5"], o["box"], 7, 7, 1.0 / 16, 0, num_rois=nr, batch_base=rank * B,
-                                     out=pool.get("p5"))
-            pool["p4"] = rp.roi_pool(inputs["conv4"], o["box"], 7, 7, 1.0 / 8, 0, num_rois=nr, batch_base=rank * B,
-                                     out=pool.get("p4"))
+            pool["p5"] = timed("roi_pool_conv5", lambda: rp.roi_pool(
+                inputs["conv5"], o["box"], 7, 7, 1.0 / 16, 0, num_rois=nr, batch_base=rank * B, out=pool.get("p5")))
+            pool["p4"] = timed("roi_pool_conv4", lambda: rp.roi_pool(
+                inputs["conv4"], o["box"], 7, 7, 1.0 / 8, 0, num_rois=nr, batch_base=rank * B, out=pool.get("p4")))
         step = None
 
     def barrier():
@@ -156,6 +167,16 @@ def main():
         for k, evs in step.timer.items():
             ops[k] = sum(a.elapsed_time(b) for a, b in evs) / nb
         step.timer = None
+    else:
+        vr_timer["on"] = True
+        nb = max(3, min(args.steps, 20))
+        for _ in range(nb):
+            run()
+        barrier()
+        del vr_timer["on"]
+        for k, evs in vr_timer.items():
+            ops[k] = sum(a.elapsed_time(b) for a, b in evs) / nb
+        vr_timer.clear()
 
     # (2) timed region: K steps bracketed by a barrier + device sync on both
     # sides, max over ranks.  On one GPU the step runs both as a HIP-graph

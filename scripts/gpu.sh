@@ -37,7 +37,7 @@ while [ $# -gt 0 ]; do
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || exit 1 ;;
     bench)
       timeout -k 10 600 python bench.py > $O/bench_full.json 2> $O/bench_full.err || exit 1
-      timeout -k 10 300 python bench.py --workload vote_roi --steps 200 --warmup 20 --no-cpu-baseline \
+      timeout -k 10 300 python bench.py --workload vote_roi --steps 200 --warmup 20 \
         > $O/bench_vr.json 2> $O/bench_vr.err || exit 1 ;;
     prof)
       PMC=(--stats)
