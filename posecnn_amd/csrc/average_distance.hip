@@ -146,6 +146,10 @@ __device__ __forceinline__ void add_plain_row(int n, const float* __restrict__ p
 #endif
 constexpr int kSymGroups = ADD_GROUPS;
 constexpr int kSymThreads = kSymLanes * kSymGroups;
+#ifndef ADD_BLK
+#define ADD_BLK 8
+#endif
+constexpr int kBlk = ADD_BLK;  // candidates per block of the running-minimum scan
 
 __global__ void __launch_bounds__(kSymThreads) k_add_rows(const float* __restrict__ pred,
                                                            const float* __restrict__ target,
@@ -169,7 +173,7 @@ __global__ void __launch_bounds__(kSymThreads) k_add_rows(const float* __restric
   const int sym_items = *nsym * nchunk;
   const int items = sym_items + R;  // then one plain item per row (add_plain_row)
   const int grp = threadIdx.x / kSymLanes, lt = threadIdx.x % kSymLanes;
-  const int quarter = ((P + kSymGroups - 1) / kSymGroups + 3) / 4 * 4;
+  const int quarter = ((P + kSymGroups - 1) / kSymGroups + kBlk - 1) / kBlk * kBlk;
   const int c0 = grp * quarter, c1 = min(P, c0 + quarter);
   // items are handed out by an atomic counter (zeroed by k_add_prep), so a
   // workgroup that finishes early takes the next (row, chunk)
@@ -232,11 +236,12 @@ __global__ void __launch_bounds__(kSymThreads) k_add_rows(const float* __restric
   // Nearest GT-rotated model point of this group's range [c0, c1) with the
   // reference's first-minimum semantics (strict <, index order, NaN never
   // wins; cu.cc:150-172), in two exact steps: a running minimum over blocks
-  // of 4 candidates (block minimum by v_min3 -- fminf drops NaN like the
+  // of kBlk candidates (block minimum by v_min3 -- fminf drops NaN like the
   // strict < does; the running minimum updates only on a strictly smaller
   // block minimum, remembering the block), then the first index of that block
   // whose distance, recomputed by the same expression, equals the minimum.
-  // The per-candidate compare/select pair of a direct scan becomes ~1/2 min.
+  // The per-candidate compare/select pair of a direct scan becomes ~1/2 min
+  // (kBlk 8: one compare + two selects per 8 candidates instead of per 4).
   auto dist_to = [&](int k, const float4& c) {
     return (qx[k] - c.x) * (qx[k] - c.x) + (qy[k] - c.y) * (qy[k] - c.y) + (qz[k] - c.z) * (qz[k] - c.z);
   };
@@ -260,22 +265,24 @@ __global__ void __launch_bounds__(kSymThreads) k_add_rows(const float* __restric
   auto scan = [&](auto np_c) {
     constexpr int NP = decltype(np_c)::value;
     int i = c0;
-    for (; i + 4 <= c1; i += 4) {
-      float4 c[4];
+    for (; i + kBlk <= c1; i += kBlk) {
+      float4 c[kBlk];
 #pragma unroll
-      for (int j = 0; j < 4; j++) c[j] = gpts[i + j];
+      for (int j = 0; j < kBlk; j++) c[j] = gpts[i + j];
 #pragma unroll
       for (int h = 0; h < NP; h++) {
-        f2 d[4];
+        f2 d[kBlk];
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
+        for (int j = 0; j < kBlk; j++) {
           const f2 ex = px[h] - c[j].x, ey = py[h] - c[j].y, ez = pz[h] - c[j].z;
           d[j] = ex * ex + ey * ey + ez * ez;
         }
 #pragma unroll
         for (int e = 0; e < 2; e++) {
           const int k = 2 * h + e;
-          const float bm = fminf(fminf(d[0][e], d[1][e]), fminf(d[2][e], d[3][e]));
+          float bm = fminf(d[0][e], d[1][e]);  // min3 chains: (kBlk - 1) / 2 instructions
+#pragma unroll
+          for (int j = 2; j < kBlk; j += 2) bm = fminf(bm, fminf(d[j][e], d[j + 1][e]));
           if (bm < dmin[k]) { dmin[k] = bm; iblk[k] = i; }
         }
       }
@@ -310,7 +317,7 @@ __global__ void __launch_bounds__(kSymThreads) k_add_rows(const float* __restric
       }
       int im = -1;
       if (iblk[k] >= 0) {
-        const int e = min(iblk[k] + 4, P);
+        const int e = min(iblk[k] + kBlk, P);
         for (int j = iblk[k]; j < e; j++)
           if (dist_to(k, gpts[j]) == dmin[k]) { im = j; break; }
       }
