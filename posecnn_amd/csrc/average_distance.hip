@@ -57,6 +57,21 @@ __device__ __forceinline__ void quat2rot(float s, float u, float v, float w, flo
   r[8] = s * s - u * u - v * v + w * w;
 }
 
+// x / b correctly rounded, for a b fixed per launch (the loss normaliser):
+// y = RN(x * r) with r = RN(1 / b) is a faithful quotient, its remainder
+// x - b y is exact in one fma, and RN(y + r (x - b y)) is the correctly
+// rounded x / b (Markstein's theorem; no underflow at these magnitudes) -- the
+// reference's IEEE division (cu.cc:181,196-202) in three instructions instead
+// of the ten of the generic division sequence.  Same for the double form.
+__device__ __forceinline__ float div_rn(float x, float b, float r) {
+  const float y = x * r;
+  return fmaf(fmaf(-y, b, x), r, y);
+}
+__device__ __forceinline__ double div_rn(double x, double b, double r) {
+  const double y = x * r;
+  return fma(fma(-y, b, x), r, y);
+}
+
 __device__ __forceinline__ int row_class(const float* __restrict__ weight, int n, int C) {
   const int PC = 4 * C;
   for (int i = 0; i < C; i++)  // first class with weight > 0 (cu.cc:47-52)
@@ -91,8 +106,8 @@ __device__ __forceinline__ void add_plain_row(int n, const float* __restrict__ p
   const float d2[9] = {-2 * v, 2 * u, 2 * s, 2 * u, 2 * v, 2 * w, -2 * s, 2 * w, -2 * v};
   const float d3[9] = {-2 * w, -2 * s, 2 * u, 2 * s, -2 * w, 2 * v, 2 * u, 2 * v, 2 * w};
   const int Rn = norm_rows_dev ? *norm_rows_dev : (norm_rows > 0 ? norm_rows : R);
-  const float bn = (float)(Rn * P);
-  const double ln = 2.0 * (double)Rn * (double)P;
+  const float bn = (float)(Rn * P), rbn = 1.f / bn;
+  const double ln = 2.0 * (double)Rn * (double)P, rln = 1.0 / ln;
   const float* pts = points + (size_t)cls * P * 3;
   float acc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
   for (int p = threadIdx.x; p < P; p += blockDim.x) {
@@ -105,7 +120,7 @@ __device__ __forceinline__ void add_plain_row(int n, const float* __restrict__ p
     const float z2 = Rg[6] * X0 + Rg[7] * X1 + Rg[8] * X2;
     const float dist = (x1 - x2) * (x1 - x2) + (y1 - y2) * (y1 - y2) + (z1 - z2) * (z1 - z2);
     if (dist < margin) continue;
-    acc[0] += (float)((double)(dist - margin) / ln);
+    acc[0] += (float)div_rn((double)(dist - margin), ln, rln);
     const float X[3] = {X0, X1, X2};
     const float df[3] = {x1 - x2, y1 - y2, z1 - z2};
     float e0 = 0.f, e1 = 0.f, e2 = 0.f, e3 = 0.f;  // this point's terms, reference order
@@ -113,10 +128,10 @@ __device__ __forceinline__ void add_plain_row(int n, const float* __restrict__ p
     for (int j = 0; j < 3; j++)
 #pragma unroll
       for (int k = 0; k < 3; k++) {
-        e0 += df[j] * X[k] * d0[j * 3 + k] / bn;
-        e1 += df[j] * X[k] * d1[j * 3 + k] / bn;
-        e2 += df[j] * X[k] * d2[j * 3 + k] / bn;
-        e3 += df[j] * X[k] * d3[j * 3 + k] / bn;
+        e0 += div_rn(df[j] * X[k] * d0[j * 3 + k], bn, rbn);
+        e1 += div_rn(df[j] * X[k] * d1[j * 3 + k], bn, rbn);
+        e2 += div_rn(df[j] * X[k] * d2[j * 3 + k], bn, rbn);
+        e3 += div_rn(df[j] * X[k] * d3[j * 3 + k], bn, rbn);
       }
     acc[1] += e0; acc[2] += e1; acc[3] += e2; acc[4] += e3;
   }
@@ -339,11 +354,11 @@ __global__ void __launch_bounds__(kSymThreads) k_add_rows(const float* __restric
     const float4 cm = gpts[im];
     const float x2 = cm.x, y2 = cm.y, z2 = cm.z;
     const int Rn = norm_rows_dev ? *norm_rows_dev : (norm_rows > 0 ? norm_rows : R);
-    const float bn = (float)(Rn * P);
-    const double ln = 2.0 * (double)Rn * (double)P;
+    const float bn = (float)(Rn * P), rbn = 1.f / bn;
+    const double ln = 2.0 * (double)Rn * (double)P, rln = 1.0 / ln;
     const float dist = (x1 - x2) * (x1 - x2) + (y1 - y2) * (y1 - y2) + (z1 - z2) * (z1 - z2);
     if (!(dist < margin)) {  // cu.cc:178-179
-      acc[0] += (float)((double)(dist - margin) / ln);  // cu.cc:181
+      acc[0] += (float)div_rn((double)(dist - margin), ln, rln);  // cu.cc:181
       // derivative matrices of Rp w.r.t. (s, u, v, w) (cu.cc:97-139)
       const float d0[9] = {2 * s, -2 * w, 2 * v, 2 * w, 2 * s, -2 * u, -2 * v, 2 * u, 2 * s};
       const float d1[9] = {2 * u, 2 * v, 2 * w, 2 * v, -2 * u, -2 * s, 2 * w, 2 * s, -2 * u};
@@ -356,10 +371,10 @@ __global__ void __launch_bounds__(kSymThreads) k_add_rows(const float* __restric
       for (int a = 0; a < 3; a++)
 #pragma unroll
         for (int b = 0; b < 3; b++) {  // cu.cc:183-203, same operation order
-          e0 += df[a] * X[b] * d0[a * 3 + b] / bn;
-          e1 += df[a] * X[b] * d1[a * 3 + b] / bn;
-          e2 += df[a] * X[b] * d2[a * 3 + b] / bn;
-          e3 += df[a] * X[b] * d3[a * 3 + b] / bn;
+          e0 += div_rn(df[a] * X[b] * d0[a * 3 + b], bn, rbn);
+          e1 += div_rn(df[a] * X[b] * d1[a * 3 + b], bn, rbn);
+          e2 += div_rn(df[a] * X[b] * d2[a * 3 + b], bn, rbn);
+          e3 += div_rn(df[a] * X[b] * d3[a * 3 + b], bn, rbn);
         }
       acc[1] += e0; acc[2] += e1; acc[3] += e2; acc[4] += e3;
     }

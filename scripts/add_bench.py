@@ -39,5 +39,7 @@ for _ in range(a.iters):
     fn()
 e1.record()
 torch.cuda.synchronize()
-print(f"rows {int(nr.item())} add_fwd {e0.elapsed_time(e1) / a.iters * 1e3:9.1f} us loss {float(loss.item()):.6e}",
-      flush=True)
+import hashlib  # noqa: E402
+dig = hashlib.sha256(diff.cpu().numpy().tobytes()).hexdigest()[:16]
+print(f"rows {int(nr.item())} add_fwd {e0.elapsed_time(e1) / a.iters * 1e3:9.1f} us loss {float(loss.item()).hex()} "
+      f"diff sha {dig}", flush=True)
