@@ -213,9 +213,13 @@ int pcnn_colsum(const float* X, int M, int N, int ldx, const int32_t* M_dev, flo
 int pcnn_pose_head_fwd(const float* y8, const float* poses_weight, int R_cap, const int32_t* num_rois_dev, int D,
                        float* tanh_out, float* pred, void* stream);
 
-/* Backward of the tail: d_pred -> d_y8 (through l2_normalize, multiply, tanh). */
-int pcnn_pose_head_bwd(const float* d_pred, const float* tanh_out, const float* poses_weight, const float* pred,
-                       int R_cap, const int32_t* num_rois_dev, int D, float* d_y8, void* stream);
+/* Backward of the tail: d_pred -> d_y8 (through l2_normalize, multiply, tanh).
+ * d_pred_scale (optional device scalar): d_pred is taken as d_pred_scale[0] * d_pred,
+ * i.e. the ADD-loss gradient op (AveragedistanceBackward, average_distance_loss_op_gpu.cu.cc:346-354:
+ * top_diff[0] * bottom_diff) folded into this pass; NULL = d_pred as given. */
+int pcnn_pose_head_bwd(const float* d_pred, const float* d_pred_scale, const float* tanh_out,
+                       const float* poses_weight, const float* pred, int R_cap, const int32_t* num_rois_dev, int D,
+                       float* d_y8, void* stream);
 
 /* ---------------------------------------------------------------------------
  * Class-aware greedy box NMS + pose combination (inference consumer of the

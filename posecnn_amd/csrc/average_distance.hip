@@ -73,9 +73,17 @@ __device__ __forceinline__ double div_rn(double x, double b, double r) {
 }
 
 __device__ __forceinline__ int row_class(const float* __restrict__ weight, int n, int C) {
-  const int PC = 4 * C;
-  for (int i = 0; i < C; i++)  // first class with weight > 0 (cu.cc:47-52)
-    if (weight[(size_t)n * PC + 4 * i] > 0) return i;
+  // first class with weight > 0 (cu.cc:47-52); the row's weights are loaded
+  // eight at a time with independent loads, not one dependent load per class
+  const float* w = weight + (size_t)n * 4 * C;
+  for (int i0 = 0; i0 < C; i0 += 8) {
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) v[j] = i0 + j < C ? w[4 * (i0 + j)] : 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; j++)
+      if (v[j] > 0) return i0 + j;
+  }
   return -1;
 }
 
@@ -398,7 +406,8 @@ __global__ void __launch_bounds__(kSymThreads) k_add_rows(const float* __restric
 __global__ void __launch_bounds__(1024) k_add_prep(const float* __restrict__ weight, const float* __restrict__ symmetry,
                                                     int R_cap, const int32_t* __restrict__ num_rois_dev, int C,
                                                     int32_t* __restrict__ rcls, int32_t* __restrict__ sym_rows,
-                                                    int32_t* __restrict__ nsym, int32_t* __restrict__ queue) {
+                                                    int32_t* __restrict__ nsym, int32_t* __restrict__ queue,
+                                                    uint32_t* __restrict__ done) {
   __shared__ int wcount[16];
   __shared__ int base;
   const int R = rows_of(num_rois_dev, R_cap);
@@ -430,19 +439,13 @@ __global__ void __launch_bounds__(1024) k_add_prep(const float* __restrict__ wei
   if (threadIdx.x == 0) {
     *nsym = base;
     *queue = 0;
+    *done = 0;
   }
 }
 
-// One wave per row: fold the chunk partials (fixed tree), write the row of
-// bottom_diff (zeros except the class's 4 channels) and the row loss.
-__global__ void __launch_bounds__(256) k_add_finish_rows(int R_cap, const int32_t* __restrict__ num_rois_dev, int C,
-                                                          int nchunk, const int32_t* __restrict__ rcls,
-                                                          const float* __restrict__ partial,
-                                                          float* __restrict__ row_loss,
-                                                          float* __restrict__ bottom_diff) {
-  const int R = rows_of(num_rois_dev, R_cap);
-  const int n = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const int lane = pcnn::lane_id();
+__device__ __forceinline__ void finish_row(int n, int R, int C, int nchunk, const int32_t* __restrict__ rcls,
+                                           const float* __restrict__ partial, float* __restrict__ row_loss,
+                                           float* __restrict__ bottom_diff, int lane) {
   if (n >= R) return;
   const int cls = rcls[n];
   float s[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
@@ -459,22 +462,55 @@ __global__ void __launch_bounds__(256) k_add_finish_rows(int R_cap, const int32_
   if (lane == 0) row_loss[n] = cls >= 0 ? s[0] : 0.f;
 }
 
-// Scalar loss: fixed-order sum of the row losses (thrust::reduce, cu.cc:333-334).
-__global__ void __launch_bounds__(1024) k_add_total(int R_cap, const int32_t* __restrict__ num_rois_dev,
-                                                     const float* __restrict__ row_loss, float* __restrict__ loss) {
-  __shared__ float red[16];
-  const int R = rows_of(num_rois_dev, R_cap);
-  float my = 0.f;
-  for (int n = threadIdx.x; n < R; n += blockDim.x) my += row_loss[n];
-  my = pcnn::wave_sum(my);
-  if (pcnn::lane_id() == 0) red[threadIdx.x >> 6] = my;
+// Scalar loss: fixed-order sum of the row losses (thrust::reduce, cu.cc:333-334)
+// in the order of a 1024-thread pass — thread t sums rows t, t + 1024, ...,
+// waves of 64 threads reduce by wave_sum, the 16 wave sums add in wave order —
+// evaluated by the `nthreads` threads of one workgroup.
+__device__ __forceinline__ void add_total(int R, const float* __restrict__ row_loss, float* __restrict__ loss,
+                                          float* red /* [16] */) {
+  constexpr int kT = 1024;
+  const int nw = blockDim.x >> 6;
+  for (int j = 0; j < kT / (int)blockDim.x; j++) {
+    const int t = threadIdx.x + j * blockDim.x;
+    float my = 0.f;
+    for (int n = t; n < R; n += kT) my += row_loss[n];
+    my = pcnn::wave_sum(my);
+    if (pcnn::lane_id() == 0) red[j * nw + (threadIdx.x >> 6)] = my;
+  }
   __syncthreads();
   if (threadIdx.x == 0) {
     float t = 0.f;
-    for (int i = 0; i < (int)(blockDim.x >> 6); i++) t += red[i];
+    for (int i = 0; i < kT / 64; i++) t += red[i];
     loss[0] = t;
   }
 }
+
+// One wave per row: fold the chunk partials (fixed tree), write the row of
+// bottom_diff (zeros except the class's 4 channels) and the row loss.  The
+// last workgroup to finish (device-scope counter, zeroed by k_add_prep) then
+// adds the row losses into the scalar loss.
+__global__ void __launch_bounds__(256) k_add_finish_rows(int R_cap, const int32_t* __restrict__ num_rois_dev, int C,
+                                                          int nchunk, const int32_t* __restrict__ rcls,
+                                                          const float* __restrict__ partial,
+                                                          float* __restrict__ row_loss,
+                                                          float* __restrict__ bottom_diff,
+                                                          uint32_t* __restrict__ done, float* __restrict__ loss) {
+  __shared__ float red[16];
+  __shared__ bool last;
+  const int R = rows_of(num_rois_dev, R_cap);
+  const int n = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = pcnn::lane_id();
+  finish_row(n, R, C, nchunk, rcls, partial, row_loss, bottom_diff, lane);
+  __threadfence();  // this workgroup's row losses before its count
+  __syncthreads();
+  if (threadIdx.x == 0) last = atomicAdd(done, 1u) == gridDim.x - 1;
+  __syncthreads();
+  if (!last) return;
+  __threadfence();  // every other workgroup's row losses after the count
+  add_total(R, row_loss, loss, red);
+}
+
+
 
 __global__ void k_add_bwd(const float* __restrict__ top_diff, const float* __restrict__ bottom_diff, int n,
                           float* __restrict__ out) {
@@ -516,8 +552,9 @@ extern "C" int pcnn_add_loss_fwd(const float* pred, const float* target, const f
   int32_t* nsym = cv.take<int32_t>(1);
   int32_t* queue = cv.take<int32_t>(1);
   float* row_loss = cv.take<float>(R_cap);
+  uint32_t* done = cv.take<uint32_t>(1);
   hipLaunchKernelGGL(k_add_prep, dim3(1), dim3(1024), 0, st, weight, symmetry, R_cap, num_rois_dev, C, rcls,
-                     sym_rows, nsym, queue);
+                     sym_rows, nsym, queue, done);
   // one persistent grid: symmetric (row, chunk) items of the device-side list, then the plain rows
   const long sym_items = (long)R_cap * nchunk + R_cap;  // symmetric (row, chunk) items, then plain rows
   const int sym_grid = (int)(sym_items < ADD_GRID ? sym_items : ADD_GRID);
@@ -525,8 +562,7 @@ extern "C" int pcnn_add_loss_fwd(const float* pred, const float* target, const f
                      target, weight, points, symmetry, R_cap, num_rois_dev, C, P, margin, loss_norm_rows,
                      loss_norm_rows_dev, nchunk, rcls, sym_rows, nsym, queue, partial);
   hipLaunchKernelGGL(k_add_finish_rows, dim3((R_cap + 3) / 4), dim3(256), 0, st, R_cap, num_rois_dev, C, nchunk,
-                     rcls, partial, row_loss, bottom_diff);
-  hipLaunchKernelGGL(k_add_total, dim3(1), dim3(1024), 0, st, R_cap, num_rois_dev, row_loss, loss);
+                     rcls, partial, row_loss, bottom_diff, done, loss);
   PCNN_CHECK_LAUNCH();
   return PCNN_OK;
 }

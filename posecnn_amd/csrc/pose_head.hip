@@ -848,8 +848,11 @@ __global__ void __launch_bounds__(256) k_head_fwd(const float* __restrict__ y8, 
 __global__ void __launch_bounds__(256) k_head_bwd(const float* __restrict__ dpred, const float* __restrict__ t_in,
                                                    const float* __restrict__ pw, const float* __restrict__ pred,
                                                    int R_cap, const int32_t* __restrict__ num_rois_dev, int D,
-                                                   float* __restrict__ dy8) {
+                                                   const float* __restrict__ dscale, float* __restrict__ dy8) {
   const int R = eff_dim(R_cap, num_rois_dev);
+  // d_pred = top_diff[0] * bottom_diff when the ADD-loss gradient op is folded
+  // in (AveragedistanceBackward, cu.cc:346-354: the same product); 1 * x == x
+  const float g = dscale ? dscale[0] : 1.f;
   const int row = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int lane = pcnn::lane_id();
   if (row >= R) return;
@@ -860,7 +863,7 @@ __global__ void __launch_bounds__(256) k_head_bwd(const float* __restrict__ dpre
     if (c < D) {
       const float mv = t_in[(size_t)row * D + c] * pw[(size_t)row * D + c];
       ss += mv * mv;
-      dot += pred[(size_t)row * D + c] * dpred[(size_t)row * D + c];
+      dot += pred[(size_t)row * D + c] * (g * dpred[(size_t)row * D + c]);
     }
   }
   ss = pcnn::wave_sum(ss);
@@ -873,7 +876,8 @@ __global__ void __launch_bounds__(256) k_head_bwd(const float* __restrict__ dpre
     if (c < D) {
       const size_t o = (size_t)row * D + c;
       // d/dm of m * rsqrt(max(sum m^2, eps))
-      const float dm = clamp ? dpred[o] * inv : (dpred[o] - pred[o] * dot) * inv;
+      const float dp = g * dpred[o];
+      const float dm = clamp ? dp * inv : (dp - pred[o] * dot) * inv;
       const float dt = dm * pw[o];
       const float t = t_in[o];
       dy8[o] = dt * (1.f - t * t);
@@ -1023,13 +1027,13 @@ extern "C" int pcnn_pose_head_fwd(const float* y8, const float* poses_weight, in
   return PCNN_OK;
 }
 
-extern "C" int pcnn_pose_head_bwd(const float* d_pred, const float* tanh_out, const float* poses_weight,
-                                  const float* pred, int R_cap, const int32_t* num_rois_dev, int D, float* d_y8,
-                                  void* stream) {
+extern "C" int pcnn_pose_head_bwd(const float* d_pred, const float* d_pred_scale, const float* tanh_out,
+                                  const float* poses_weight, const float* pred, int R_cap,
+                                  const int32_t* num_rois_dev, int D, float* d_y8, void* stream) {
   PCNN_REQUIRE(d_pred && tanh_out && poses_weight && pred && d_y8 && R_cap >= 0 && D > 0 && D <= 256);
   if (R_cap == 0) return PCNN_OK;
   hipLaunchKernelGGL(k_head_bwd, dim3((R_cap + 3) / 4), dim3(256), 0, (hipStream_t)stream, d_pred, tanh_out,
-                     poses_weight, pred, R_cap, num_rois_dev, D, d_y8);
+                     poses_weight, pred, R_cap, num_rois_dev, D, d_pred_scale, d_y8);
   PCNN_CHECK_LAUNCH();
   return PCNN_OK;
 }

@@ -70,7 +70,6 @@ class PoseStep:
         self.loss = torch.zeros((1,), **f32)
         self.diff = torch.zeros((CAP, D), **f32)
         self.one = torch.ones((1,), **f32)
-        self.dpred = torch.zeros((CAP, D), **f32)
         self.dy8 = torch.zeros((CAP, D), **f32)
         self.dy7 = torch.zeros((CAP, units), **f32)
         self.dy6 = torch.zeros((CAP, units), **f32)
@@ -213,8 +212,9 @@ class PoseStep:
                     ph.gemm(X, dY, g[name], a_trans=1, K_dev=nr, M=M, N=N, K=K_loc, precision=self.prec)
 
         with self._t("add_loss_head_bwd"):
-            adl.average_distance_loss_grad(self.diff, self.one, num_rois=nr, out=self.dpred)
-            ph.head_bwd(self.dpred, self.t8, h["weight"], self.pred, self.dy8, num_rois=nr)
+            # average_distance_loss_grad (top_diff[0] * bottom_diff) folded into
+            # the head backward: one pass over the (R, 4C) rows instead of two
+            ph.head_bwd(self.diff, self.t8, h["weight"], self.pred, self.dy8, num_rois=nr, d_pred_scale=self.one)
         with self._t("gemm_fc8_fc7_dw_bias"):  # fc8 weight / bias gradients
             weight_grads("w8", self.y7, self.dy8, CAP, w.units, self.D)
         with self._t("gemm_fc8_fc7_dx"):

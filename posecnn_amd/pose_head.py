@@ -50,11 +50,13 @@ def head_fwd(y8, poses_weight, tanh_out, pred, num_rois=None, stream=None):
     _lib.check(rc, "pose_head_fwd")
 
 
-def head_bwd(d_pred, tanh_out, poses_weight, pred, d_y8, num_rois=None, stream=None):
+def head_bwd(d_pred, tanh_out, poses_weight, pred, d_y8, num_rois=None, d_pred_scale=None, stream=None):
+    """d_y8 from d_pred; with d_pred_scale (device scalar) d_pred is taken as
+    d_pred_scale[0] * d_pred -- the ADD-loss gradient op folded into this pass."""
     R, D = d_pred.shape
-    rc = _lib.load().pcnn_pose_head_bwd(_lib.ptr(d_pred), _lib.ptr(tanh_out), _lib.ptr(poses_weight),
-                                        _lib.ptr(pred), R, _lib.ptr(num_rois), D, _lib.ptr(d_y8),
-                                        _lib.stream_ptr(stream))
+    rc = _lib.load().pcnn_pose_head_bwd(_lib.ptr(d_pred), _lib.ptr(d_pred_scale), _lib.ptr(tanh_out),
+                                        _lib.ptr(poses_weight), _lib.ptr(pred), R, _lib.ptr(num_rois), D,
+                                        _lib.ptr(d_y8), _lib.stream_ptr(stream))
     _lib.check(rc, "pose_head_bwd")
 
 
