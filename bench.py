@@ -44,6 +44,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (bounded sample)")
     p.add_argument("--no-graph", action="store_true", help="time eager launches instead of a HIP graph")
+    p.add_argument("--flat-argmax", action="store_true",
+                   help="RoI-pool argmax as the reference's int32 flat index instead of uint16 pixel indices (A/B)")
     p.add_argument("--precision", type=int, choices=[0, 1], default=1,
                    help="FC GEMMs: 1 = split-bf16 x3 MFMA (fp32-class), 0 = fp32 MFMA")
     p.add_argument("--no-fp32-leg", action="store_true",
@@ -103,7 +105,7 @@ def main():
 
     if full:
         step = PoseStep(B, H, W, C, dev, is_train=1, skip_pixels=10, global_batch=gB, batch_base=rank * B,
-                        dist=dist, precision=args.precision)
+                        dist=dist, precision=args.precision, pixel_argmax=not args.flat_argmax)
         run = lambda: step.step(inputs)
     if linemod:  # + the depth back-projection op, forward and backward (no reference caller)
         from posecnn_amd.backprojecting_layer import backprojecting_op as bpo

@@ -138,12 +138,32 @@ int pcnn_roi_pool_fwd_pair(const float* data_a, int Ha, int Wa, float scale_a, c
                            int batch_base, const int32_t* num_rois_dev, int pooled_h, int pooled_w, float* top_sum,
                            int32_t* argmax_a, int32_t* argmax_b, void* stream);
 
+/* pcnn_roi_pool_fwd_pair with the compact argmax of the fused pose step: per
+ * output element the uint16 pixel index h*W + w of the max within its image
+ * (the channel is the element's own; 0xFFFF = empty bin, so H*W < 0xFFFF for
+ * both maps), i.e. the reference's flat index argmax = pixel*C + c
+ * (roi_pooling_op_gpu.cu.cc:87-97) in half the bytes. argmax 8-B aligned.
+ * Consumed by pcnn_roi_pool_bwd_px. */
+int pcnn_roi_pool_fwd_pair_px(const float* data_a, int Ha, int Wa, float scale_a, const float* data_b, int Hb,
+                              int Wb, float scale_b, int B, int C, const float* rois, int R_cap, int roi_stride,
+                              int batch_base, const int32_t* num_rois_dev, int pooled_h, int pooled_w,
+                              float* top_sum, uint16_t* argmax_a, uint16_t* argmax_b, void* stream);
+
 size_t pcnn_roi_pool_bwd_workspace_size(int B, int R_cap);
 
 int pcnn_roi_pool_bwd(const float* top_diff, const int32_t* argmax, int B, int H, int W, int C, int layout,
                       const float* rois, int R_cap, int roi_stride, int batch_base, const int32_t* num_rois_dev,
                       float spatial_scale, int pooled_h, int pooled_w, int pool_channel, float* bottom_diff,
                       void* workspace, size_t workspace_bytes, void* stream);
+
+/* pcnn_roi_pool_bwd on the pixel-index argmax of pcnn_roi_pool_fwd_pair_px:
+ * NHWC, all channels (pool_channel 0), C even, H*W < 0xFFFF; the same
+ * entry-list gather and (RoI, ph, pw) summation order, so bit-equal to
+ * pcnn_roi_pool_bwd on the flat argmax. */
+int pcnn_roi_pool_bwd_px(const float* top_diff, const uint16_t* argmax_px, int B, int H, int W, int C,
+                         const float* rois, int R_cap, int roi_stride, int batch_base, const int32_t* num_rois_dev,
+                         float spatial_scale, int pooled_h, int pooled_w, float* bottom_diff, void* workspace,
+                         size_t workspace_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------
  * ADD / ADD-S pose loss (Averagedistance / AveragedistanceGrad).

@@ -48,7 +48,12 @@ _SIGS = {
     "pcnn_roi_pool_fwd_pair": (c_int, [c_void_p, c_int, c_int, c_float, c_void_p, c_int, c_int, c_float, c_int, c_int,
                                        c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p,
                                        c_void_p, c_void_p]),
+    "pcnn_roi_pool_fwd_pair_px": (c_int, [c_void_p, c_int, c_int, c_float, c_void_p, c_int, c_int, c_float, c_int,
+                                          c_int, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p,
+                                          c_void_p, c_void_p, c_void_p]),
     "pcnn_roi_pool_bwd_workspace_size": (c_size_t, [c_int, c_int]),
+    "pcnn_roi_pool_bwd_px": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_int,
+                                     c_void_p, c_float, c_int, c_int, c_void_p, c_void_p, c_size_t, c_void_p]),
     "pcnn_roi_pool_bwd": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int,
                                   c_int, c_void_p, c_float, c_int, c_int, c_int, c_void_p, c_void_p, c_size_t, c_void_p]),
     "pcnn_add_loss_workspace_size": (c_size_t, [c_int, c_int, c_int]),

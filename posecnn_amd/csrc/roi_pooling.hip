@@ -119,6 +119,9 @@ static inline unsigned fwd_grid(int R_cap, int nbins) {
 // Max / argmax of one bin over lane channels c..c+3 (cu.cc:45-97): bin
 // bounds as bin_bounds, strict > first max in raster order, empty bin (or a
 // RoI batch index outside [0, B)) -> 0 / -1.
+// PX: the argmax is the pixel index h * W + w within the image (the channel is
+// the output's own), the compact form of the fused pose step.
+template <bool PX = false>
 __device__ __forceinline__ void bin_max4(const float* __restrict__ data, int B, int H, int W, int C,
                                          const RoiGeo& g, int ph, int pw, int c, float4& m, int4& a) {
   const bool bad = g.b < 0 || g.b >= B;
@@ -136,13 +139,24 @@ __device__ __forceinline__ void bin_max4(const float* __restrict__ data, int B, 
         const int i0 = (h * W + w) * C + c, i1 = i0 + C;
         const float4 v0 = *(const float4*)(bd + i0);
         const float4 v1 = *(const float4*)(bd + i1);
-        upd(v0.x, i0 + 0, m0, a0); upd(v0.y, i0 + 1, m1, a1); upd(v0.z, i0 + 2, m2, a2); upd(v0.w, i0 + 3, m3, a3);
-        upd(v1.x, i1 + 0, m0, a0); upd(v1.y, i1 + 1, m1, a1); upd(v1.z, i1 + 2, m2, a2); upd(v1.w, i1 + 3, m3, a3);
+        if (PX) {
+          const int p0 = h * W + w, p1 = p0 + 1;
+          upd(v0.x, p0, m0, a0); upd(v0.y, p0, m1, a1); upd(v0.z, p0, m2, a2); upd(v0.w, p0, m3, a3);
+          upd(v1.x, p1, m0, a0); upd(v1.y, p1, m1, a1); upd(v1.z, p1, m2, a2); upd(v1.w, p1, m3, a3);
+        } else {
+          upd(v0.x, i0 + 0, m0, a0); upd(v0.y, i0 + 1, m1, a1); upd(v0.z, i0 + 2, m2, a2); upd(v0.w, i0 + 3, m3, a3);
+          upd(v1.x, i1 + 0, m0, a0); upd(v1.y, i1 + 1, m1, a1); upd(v1.z, i1 + 2, m2, a2); upd(v1.w, i1 + 3, m3, a3);
+        }
       }
       if (w < we) {
         const int i0 = (h * W + w) * C + c;
         const float4 v0 = *(const float4*)(bd + i0);
-        upd(v0.x, i0 + 0, m0, a0); upd(v0.y, i0 + 1, m1, a1); upd(v0.z, i0 + 2, m2, a2); upd(v0.w, i0 + 3, m3, a3);
+        if (PX) {
+          const int p0 = h * W + w;
+          upd(v0.x, p0, m0, a0); upd(v0.y, p0, m1, a1); upd(v0.z, p0, m2, a2); upd(v0.w, p0, m3, a3);
+        } else {
+          upd(v0.x, i0 + 0, m0, a0); upd(v0.y, i0 + 1, m1, a1); upd(v0.z, i0 + 2, m2, a2); upd(v0.w, i0 + 3, m3, a3);
+        }
       }
     }
   }
@@ -184,13 +198,16 @@ __global__ void __launch_bounds__(128) k_roi_fwd_nhwc4(const float* __restrict__
 // (roi, bin) takes the bin on both maps, so the two maps' loads are in flight
 // together, and writes pool5 + pool4 (the same single fp32 add as the
 // accumulate pass) and both argmax tensors — no pool5 round trip through HBM.
+// PX: argmax as uint16 pixel indices (h * W + w; 0xFFFF = empty bin), half the
+// argmax bytes written here and read back by k_roi_bwd_ent<.., true>.
+template <bool PX>
 __global__ void __launch_bounds__(128) k_roi_fwd_pair_nhwc4(const float* __restrict__ data_a, int Ha, int Wa,
                                                              float scale_a, const float* __restrict__ data_b, int Hb,
                                                              int Wb, float scale_b, int B, int C,
                                                              const float* __restrict__ rois, int R_cap, int stride,
                                                              int batch_base, const int32_t* __restrict__ num_rois_dev,
                                                              int PH, int PW, float* __restrict__ top,
-                                                             int32_t* __restrict__ arg_a, int32_t* __restrict__ arg_b) {
+                                                             void* __restrict__ arg_a, void* __restrict__ arg_b) {
   int r, bin;
   if (!fwd_item(rows_of(num_rois_dev, R_cap), PH * PW, r, bin)) return;
   const int ph = bin / PW, pw = bin % PW;
@@ -200,11 +217,20 @@ __global__ void __launch_bounds__(128) k_roi_fwd_pair_nhwc4(const float* __restr
   for (int c = threadIdx.x * 4; c < C; c += blockDim.x * 4) {
     float4 ma, mb;
     int4 aa, ab;
-    bin_max4(data_a, B, Ha, Wa, C, ga, ph, pw, c, ma, aa);
-    bin_max4(data_b, B, Hb, Wb, C, gb, ph, pw, c, mb, ab);
+    bin_max4<PX>(data_a, B, Ha, Wa, C, ga, ph, pw, c, ma, aa);
+    bin_max4<PX>(data_b, B, Hb, Wb, C, gb, ph, pw, c, mb, ab);
     *(float4*)(top + o + c) = make_float4(ma.x + mb.x, ma.y + mb.y, ma.z + mb.z, ma.w + mb.w);
-    *(int4*)(arg_a + o + c) = aa;
-    *(int4*)(arg_b + o + c) = ab;
+    if (PX) {
+      auto pk = [](int4 a) {  // -1 -> 0xFFFF
+        return make_uint2(((unsigned)a.x & 0xFFFFu) | ((unsigned)a.y << 16),
+                          ((unsigned)a.z & 0xFFFFu) | ((unsigned)a.w << 16));
+      };
+      *(uint2*)((uint16_t*)arg_a + o + c) = pk(aa);
+      *(uint2*)((uint16_t*)arg_b + o + c) = pk(ab);
+    } else {
+      *(int4*)((int32_t*)arg_a + o + c) = aa;
+      *(int4*)((int32_t*)arg_b + o + c) = ab;
+    }
   }
 }
 
@@ -309,9 +335,9 @@ constexpr int kBGroup = 16;             // RoIs expanded per list round (<= 16 *
 constexpr int kBCap = kBGroup * 49;
 constexpr int kBBatch = 8;              // entries per fetch (two fetches in flight per wave)
 
-template <int kBTH, int kBTW>
+template <int kBTH, int kBTW, bool PX>
 __global__ void __launch_bounds__(64 * kBWaves) k_roi_bwd_ent(const float* __restrict__ top_diff,
-                                                               const int32_t* __restrict__ argmax, int B, int H, int W,
+                                                               const void* __restrict__ argmax, int B, int H, int W,
                                                                int C, const int32_t* __restrict__ geo,
                                                                const int32_t* __restrict__ lo,
                                                                const int32_t* __restrict__ hi, int PH, int PW,
@@ -343,14 +369,17 @@ __global__ void __launch_bounds__(64 * kBWaves) k_roi_bwd_ent(const float* __res
 #pragma unroll
   for (int p = 0; p < kBPix; p++) {
     acc[p] = make_float2(0.f, 0.f);
-    expv[p] = ((h0 + p / kBTW) * W + w0 + p % kBTW) * C + c;
+    const int pix = (h0 + p / kBTW) * W + w0 + p % kBTW;
+    expv[p] = PX ? pix : pix * C + c;  // PX: pixel index, the same for both channels
   }
+  constexpr int kNext = PX ? 0 : 1;  // argmax of channel c + 1 is expv + kNext
   const int r0 = lo[b], r1 = hi[b];
   // buffer views: per-lane channel offset in a VGPR, the entry offset as the
   // scalar soffset; lanes past C read out of range (-> 0 / never a match)
   const __amdgpu_buffer_rsrc_t rs_t = __builtin_amdgcn_make_buffer_rsrc((void*)top_diff, (short)0, 0x7fffffff, 0x00020000);
   const __amdgpu_buffer_rsrc_t rs_a = __builtin_amdgcn_make_buffer_rsrc((void*)argmax, (short)0, 0x7fffffff, 0x00020000);
   const unsigned voff = cok ? (unsigned)c * 4u : 0x80000000u;
+  const unsigned voff_a = cok ? (unsigned)c * (PX ? 2u : 4u) : 0x80000000u;
   for (int rb = r0; rb <= r1; rb += 64) {
     // wave 0: RoIs of image b whose box meets the tile, in order (cu.cc:154-177),
     // with per-bin row / column acceptance bits for the tile pixels (cu.cc:196-204)
@@ -427,7 +456,12 @@ __global__ void __launch_bounds__(64 * kBWaves) k_roi_bwd_ent(const float* __res
 #pragma unroll
         for (int k = 0; k < kBBatch; k++) {
           const int so = __builtin_amdgcn_readlane(my.x, k) * 4;
-          av[k] = __builtin_bit_cast(int2, __builtin_amdgcn_raw_buffer_load_b64(rs_a, voff, so, 0));
+          if (PX) {  // two uint16 pixel indices (lanes past C read 0: they never store)
+            const unsigned a2 = __builtin_amdgcn_raw_buffer_load_b32(rs_a, voff_a, so >> 1, 0);
+            av[k] = make_int2((int)(a2 & 0xFFFFu), (int)(a2 >> 16));
+          } else {
+            av[k] = __builtin_bit_cast(int2, __builtin_amdgcn_raw_buffer_load_b64(rs_a, voff_a, so, 0));
+          }
           dv[k] = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rs_t, voff, so, 0));
         }
       };
@@ -441,7 +475,7 @@ __global__ void __launch_bounds__(64 * kBWaves) k_roi_bwd_ent(const float* __res
             if (!((m >> q) & 1)) continue;
             // adding +0.0f leaves every partial sum bit-identical (none is ever -0)
             acc[q].x += av[k].x == expv[q] ? dv[k].x : 0.f;
-            acc[q].y += av[k].y == expv[q] + 1 ? dv[k].y : 0.f;
+            acc[q].y += av[k].y == expv[q] + kNext ? dv[k].y : 0.f;
           }
         }
       };
@@ -562,23 +596,46 @@ extern "C" int pcnn_roi_pool_fwd_accumulate(const float* data, int B, int H, int
                       pooled_w, pool_channel, 1, top, argmax, stream);
 }
 
-extern "C" int pcnn_roi_pool_fwd_pair(const float* data_a, int Ha, int Wa, float scale_a, const float* data_b, int Hb,
-                                      int Wb, float scale_b, int B, int C, const float* rois, int R_cap, int roi_stride,
-                                      int batch_base, const int32_t* num_rois_dev, int pooled_h, int pooled_w, float* top_sum,
-                                      int32_t* argmax_a, int32_t* argmax_b, void* stream) {
+static int roi_pool_fwd_pair(const float* data_a, int Ha, int Wa, float scale_a, const float* data_b, int Hb, int Wb,
+                             float scale_b, int B, int C, const float* rois, int R_cap, int roi_stride, int batch_base,
+                             const int32_t* num_rois_dev, int pooled_h, int pooled_w, float* top_sum, void* argmax_a,
+                             void* argmax_b, bool px, void* stream) {
   PCNN_REQUIRE(data_a && data_b && rois && top_sum && argmax_a && argmax_b && B > 0 && C > 0 && C % 4 == 0);
   PCNN_REQUIRE(Ha > 0 && Wa > 0 && Hb > 0 && Wb > 0 && pooled_h > 0 && pooled_w > 0 && R_cap >= 0);
   PCNN_REQUIRE(roi_stride >= 5);
   PCNN_REQUIRE((long)Ha * Wa * C < (1l << 31) && (long)Hb * Wb * C < (1l << 31));
-  PCNN_REQUIRE(((((uintptr_t)data_a) | ((uintptr_t)data_b) | ((uintptr_t)top_sum) | ((uintptr_t)argmax_a) |
-                 ((uintptr_t)argmax_b)) & 15) == 0);
+  PCNN_REQUIRE(!px || ((long)Ha * Wa < 0xFFFF && (long)Hb * Wb < 0xFFFF));  // 0xFFFF marks an empty bin
+  PCNN_REQUIRE(((((uintptr_t)data_a) | ((uintptr_t)data_b) | ((uintptr_t)top_sum)) & 15) == 0);
+  PCNN_REQUIRE(((((uintptr_t)argmax_a) | ((uintptr_t)argmax_b)) & (px ? 7 : 15)) == 0);
   if (R_cap == 0) return PCNN_OK;
   const int threads = C / 4 >= 128 ? 128 : ((C / 4 + 63) / 64) * 64;
-  hipLaunchKernelGGL(k_roi_fwd_pair_nhwc4, dim3(fwd_grid(R_cap, pooled_h * pooled_w)), dim3(threads), 0, (hipStream_t)stream,
-                     data_a, Ha, Wa, scale_a, data_b, Hb, Wb, scale_b, B, C, rois, R_cap, roi_stride, batch_base, num_rois_dev,
-                     pooled_h, pooled_w, top_sum, argmax_a, argmax_b);
+  if (px)
+    hipLaunchKernelGGL(k_roi_fwd_pair_nhwc4<true>, dim3(fwd_grid(R_cap, pooled_h * pooled_w)), dim3(threads), 0,
+                       (hipStream_t)stream, data_a, Ha, Wa, scale_a, data_b, Hb, Wb, scale_b, B, C, rois, R_cap,
+                       roi_stride, batch_base, num_rois_dev, pooled_h, pooled_w, top_sum, argmax_a, argmax_b);
+  else
+    hipLaunchKernelGGL(k_roi_fwd_pair_nhwc4<false>, dim3(fwd_grid(R_cap, pooled_h * pooled_w)), dim3(threads), 0,
+                       (hipStream_t)stream, data_a, Ha, Wa, scale_a, data_b, Hb, Wb, scale_b, B, C, rois, R_cap,
+                       roi_stride, batch_base, num_rois_dev, pooled_h, pooled_w, top_sum, argmax_a, argmax_b);
   PCNN_CHECK_LAUNCH();
   return PCNN_OK;
+}
+
+extern "C" int pcnn_roi_pool_fwd_pair(const float* data_a, int Ha, int Wa, float scale_a, const float* data_b, int Hb,
+                                      int Wb, float scale_b, int B, int C, const float* rois, int R_cap, int roi_stride,
+                                      int batch_base, const int32_t* num_rois_dev, int pooled_h, int pooled_w, float* top_sum,
+                                      int32_t* argmax_a, int32_t* argmax_b, void* stream) {
+  return roi_pool_fwd_pair(data_a, Ha, Wa, scale_a, data_b, Hb, Wb, scale_b, B, C, rois, R_cap, roi_stride, batch_base,
+                           num_rois_dev, pooled_h, pooled_w, top_sum, argmax_a, argmax_b, false, stream);
+}
+
+extern "C" int pcnn_roi_pool_fwd_pair_px(const float* data_a, int Ha, int Wa, float scale_a, const float* data_b,
+                                         int Hb, int Wb, float scale_b, int B, int C, const float* rois, int R_cap,
+                                         int roi_stride, int batch_base, const int32_t* num_rois_dev, int pooled_h,
+                                         int pooled_w, float* top_sum, uint16_t* argmax_a, uint16_t* argmax_b,
+                                         void* stream) {
+  return roi_pool_fwd_pair(data_a, Ha, Wa, scale_a, data_b, Hb, Wb, scale_b, B, C, rois, R_cap, roi_stride, batch_base,
+                           num_rois_dev, pooled_h, pooled_w, top_sum, argmax_a, argmax_b, true, stream);
 }
 
 extern "C" size_t pcnn_roi_pool_bwd_workspace_size(int B, int R_cap) {
@@ -586,10 +643,10 @@ extern "C" size_t pcnn_roi_pool_bwd_workspace_size(int B, int R_cap) {
          pcnn::align_up((size_t)(R_cap > 0 ? R_cap : 1) * 8 * sizeof(int32_t), 256) + 256;
 }
 
-extern "C" int pcnn_roi_pool_bwd(const float* top_diff, const int32_t* argmax, int B, int H, int W, int C, int layout,
-                                 const float* rois, int R_cap, int roi_stride, int batch_base,
-                                 const int32_t* num_rois_dev, float spatial_scale, int pooled_h, int pooled_w,
-                                 int pool_channel, float* bottom_diff, void* workspace, size_t workspace_bytes, void* stream) {
+static int roi_pool_bwd(const float* top_diff, const void* argmax, bool px, int B, int H, int W, int C, int layout,
+                        const float* rois, int R_cap, int roi_stride, int batch_base, const int32_t* num_rois_dev,
+                        float spatial_scale, int pooled_h, int pooled_w, int pool_channel, float* bottom_diff,
+                        void* workspace, size_t workspace_bytes, void* stream) {
   PCNN_REQUIRE(top_diff && argmax && rois && bottom_diff && workspace && B > 0 && H > 0 && W > 0 && C > 0);
   PCNN_REQUIRE(pooled_h > 0 && pooled_w > 0 && (layout == 0 || layout == 1) && R_cap >= 0);
   PCNN_REQUIRE(roi_stride >= 6 || (roi_stride == 5 && !pool_channel));
@@ -611,23 +668,43 @@ extern "C" int pcnn_roi_pool_bwd(const float* top_diff, const int32_t* argmax, i
   const int tbh = narrow ? 1 : 2, tbw = 4;
   const bool vec = layout == 0 && !pool_channel && C % 2 == 0 && pooled_h * tbh <= 32 && pooled_w * tbw <= 32 &&
                    (long)H * W * C < (1l << 30) && (long)R_cap * pooled_h * pooled_w * C < (1l << 29) &&
-                   (((uintptr_t)top_diff | (uintptr_t)argmax | (uintptr_t)bottom_diff) & 7) == 0;
+                   (((uintptr_t)top_diff | (uintptr_t)argmax | (uintptr_t)bottom_diff) & (px ? 3 : 7)) == 0;
+  PCNN_REQUIRE(!px || (vec && (long)H * W < 0xFFFF));  // pixel-index argmax: the entry-list kernel only
   if (vec) {
     const int tiles = ((H + tbh - 1) / tbh) * ((W + tbw - 1) / tbw);
     const unsigned nwg = (unsigned)((B * tiles * nchunk + 7) / 8 * 8);
-    if (narrow)
-      hipLaunchKernelGGL((k_roi_bwd_ent<1, 4>), dim3(nwg), dim3(64 * kBWaves), 0, st, top_diff, argmax,
-                         B, H, W, C, geo, lo, hi, pooled_h, pooled_w, bottom_diff);
-    else
-      hipLaunchKernelGGL((k_roi_bwd_ent<2, 4>), dim3(nwg), dim3(64 * kBWaves), 0, st, top_diff, argmax,
-                         B, H, W, C, geo, lo, hi, pooled_h, pooled_w, bottom_diff);
+#define PCNN_RBW(TH, PXV)                                                                                  \
+  hipLaunchKernelGGL((k_roi_bwd_ent<TH, 4, PXV>), dim3(nwg), dim3(64 * kBWaves), 0, st, top_diff, argmax, B, H, W, C, \
+                     geo, lo, hi, pooled_h, pooled_w, bottom_diff)
+    if (narrow) {
+      if (px) PCNN_RBW(1, true); else PCNN_RBW(1, false);
+    } else {
+      if (px) PCNN_RBW(2, true); else PCNN_RBW(2, false);
+    }
+#undef PCNN_RBW
   } else {
     if (hipMemsetAsync(bottom_diff, 0, (size_t)B * H * W * C * sizeof(float), st) != hipSuccess) return PCNN_EHIP;
     const long npix = (long)B * H * W;
     const int blocks = (int)((npix + 255) / 256 < 8192 ? (npix + 255) / 256 : 8192);
-    hipLaunchKernelGGL(k_roi_bwd_generic, dim3(blocks), dim3(256), 0, st, top_diff, argmax, B, H, W, C, layout, geo,
-                       pooled_h, pooled_w, pool_channel, lo, hi, bottom_diff);
+    hipLaunchKernelGGL(k_roi_bwd_generic, dim3(blocks), dim3(256), 0, st, top_diff, (const int32_t*)argmax, B, H, W,
+                       C, layout, geo, pooled_h, pooled_w, pool_channel, lo, hi, bottom_diff);
   }
   PCNN_CHECK_LAUNCH();
   return PCNN_OK;
+}
+
+extern "C" int pcnn_roi_pool_bwd(const float* top_diff, const int32_t* argmax, int B, int H, int W, int C, int layout,
+                                 const float* rois, int R_cap, int roi_stride, int batch_base,
+                                 const int32_t* num_rois_dev, float spatial_scale, int pooled_h, int pooled_w,
+                                 int pool_channel, float* bottom_diff, void* workspace, size_t workspace_bytes, void* stream) {
+  return roi_pool_bwd(top_diff, argmax, false, B, H, W, C, layout, rois, R_cap, roi_stride, batch_base, num_rois_dev,
+                      spatial_scale, pooled_h, pooled_w, pool_channel, bottom_diff, workspace, workspace_bytes, stream);
+}
+
+extern "C" int pcnn_roi_pool_bwd_px(const float* top_diff, const uint16_t* argmax_px, int B, int H, int W, int C,
+                                    const float* rois, int R_cap, int roi_stride, int batch_base,
+                                    const int32_t* num_rois_dev, float spatial_scale, int pooled_h, int pooled_w,
+                                    float* bottom_diff, void* workspace, size_t workspace_bytes, void* stream) {
+  return roi_pool_bwd(top_diff, argmax_px, true, B, H, W, C, 0, rois, R_cap, roi_stride, batch_base, num_rois_dev,
+                      spatial_scale, pooled_h, pooled_w, 0, bottom_diff, workspace, workspace_bytes, stream);
 }

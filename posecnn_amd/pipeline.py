@@ -37,7 +37,7 @@ class PoseStep:
     def __init__(self, B, H, W, num_classes, device, conv4_hw=None, conv5_hw=None, channels=512, units=4096,
                  is_train=1, skip_pixels=10, vote_threshold=-1.0, vote_percentage=0.02, margin=0.01,
                  global_batch=None, batch_base=0, weights=None, dist=None, backward=True, precision=1,
-                 overlap_weight_grads=True):
+                 overlap_weight_grads=True, pixel_argmax=True):
         self.B, self.H, self.W, self.C = B, H, W, num_classes
         self.dev = device
         self.is_train, self.skip, self.vthr, self.vper, self.margin = is_train, skip_pixels, vote_threshold, \
@@ -60,8 +60,13 @@ class PoseStep:
                           target=torch.zeros((CAP, D), **f32), weight=torch.zeros((CAP, D), **f32),
                           domain=torch.zeros((CAP,), **i32), num_rois=torch.zeros((2,), **i32))
         self.pool = torch.zeros((CAP, 7, 7, channels), **f32)  # pool5 + pool4 (vgg16_convs.py:184)
-        self.arg5 = torch.zeros((CAP, 7, 7, channels), **i32)
-        self.arg4 = torch.zeros((CAP, 7, 7, channels), **i32)
+        # argmax as uint16 pixel indices (half the bytes of the flat int32 form,
+        # written by the pool pair and re-read by both pool backwards) when
+        # both maps have fewer than 0xFFFF pixels
+        px = pixel_argmax and max(self.h4 * self.w4, self.h5 * self.w5) < 0xFFFF
+        adt = dict(dtype=torch.int16 if px else torch.int32, device=device)
+        self.arg5 = torch.zeros((CAP, 7, 7, channels), **adt)
+        self.arg4 = torch.zeros((CAP, 7, 7, channels), **adt)
         self.y6 = torch.zeros((CAP, units), **f32)
         self.y7 = torch.zeros((CAP, units), **f32)
         self.y8 = torch.zeros((CAP, D), **f32)

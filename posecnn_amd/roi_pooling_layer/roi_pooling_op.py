@@ -49,10 +49,13 @@ def roi_pool(bottom_data, bottom_rois, pooled_height, pooled_width, spatial_scal
 
 
 def roi_pool_pair(data_a, scale_a, data_b, scale_b, rois, pooled_height, pooled_width, num_rois=None, out=None,
-                  batch_base=0):
+                  batch_base=0, pixel_argmax=False):
     """pool_a + pool_b and both argmax tensors in one pass (vgg16_convs.py:177-184:
     roi_pool(conv5_3, 1/16) + roi_pool(conv4_3, 1/8)); NHWC, all channels.
-    Equal to roi_pool(data_a) then roi_pool(data_b, accumulate=True)."""
+    Equal to roi_pool(data_a) then roi_pool(data_b, accumulate=True).
+    Argmax tensors of dtype int16 (or pixel_argmax=True) hold the compact form:
+    the uint16 pixel index h*W + w (flat argmax = pixel*C + c; 0xFFFF = empty
+    bin), which roi_pool_grad accepts as well."""
     _lib.require_gpu(data_a, data_b, rois)
     if data_a.dim() != 4 or data_b.dim() != 4 or rois.dim() != 2:
         raise ValueError("data must be 4-dimensional and rois 2-dimensional")
@@ -65,15 +68,17 @@ def roi_pool_pair(data_a, scale_a, data_b, scale_b, rois, pooled_height, pooled_
     R, stride = rois.shape
     shape = (R, pooled_height, pooled_width, C)
     if out is None:
+        adt = torch.int16 if pixel_argmax else torch.int32
         out = (torch.empty(shape, dtype=torch.float32, device=da.device),
-               torch.empty(shape, dtype=torch.int32, device=da.device),
-               torch.empty(shape, dtype=torch.int32, device=da.device))
+               torch.empty(shape, dtype=adt, device=da.device),
+               torch.empty(shape, dtype=adt, device=da.device))
     top, arg_a, arg_b = out
-    rc = _lib.load().pcnn_roi_pool_fwd_pair(_lib.ptr(da), Ha, Wa, float(scale_a), _lib.ptr(db), Hb, Wb,
-                                            float(scale_b), B, C, _lib.ptr(rois), R, stride, int(batch_base),
-                                            _lib.ptr(num_rois),
-                                            int(pooled_height), int(pooled_width), _lib.ptr(top), _lib.ptr(arg_a),
-                                            _lib.ptr(arg_b), _lib.stream_ptr())
+    if arg_a.dtype != arg_b.dtype or arg_a.dtype not in (torch.int16, torch.int32):
+        raise ValueError("argmax tensors must both be int32 (flat index) or int16 (pixel index)")
+    fn = _lib.load().pcnn_roi_pool_fwd_pair_px if arg_a.dtype == torch.int16 else _lib.load().pcnn_roi_pool_fwd_pair
+    rc = fn(_lib.ptr(da), Ha, Wa, float(scale_a), _lib.ptr(db), Hb, Wb, float(scale_b), B, C, _lib.ptr(rois), R, stride,
+            int(batch_base), _lib.ptr(num_rois), int(pooled_height), int(pooled_width), _lib.ptr(top), _lib.ptr(arg_a),
+            _lib.ptr(arg_b), _lib.stream_ptr())
     _lib.check(rc, "roi_pool_pair")
     return top, arg_a, arg_b
 
@@ -90,10 +95,18 @@ def roi_pool_grad(bottom_data, bottom_rois, argmax, grad, pooled_height, pooled_
     lib = _lib.load()
     ws = _lib.workspace(lib.pcnn_roi_pool_bwd_workspace_size(B, R), bottom_data.device, "roi_bwd")
     dd = out if out is not None else torch.empty(bottom_data.shape, dtype=torch.float32, device=bottom_data.device)
-    rc = lib.pcnn_roi_pool_bwd(_lib.ptr(grad.contiguous()), _lib.ptr(argmax.contiguous()), B, H, W, C, layout,
-                               _lib.ptr(rois), R, stride, int(batch_base), _lib.ptr(num_rois), float(spatial_scale),
-                               int(pooled_height), int(pooled_width), int(pool_channel), _lib.ptr(dd),
-                               _lib.ptr(ws), ws.numel(), _lib.stream_ptr())
+    if argmax.dtype == torch.int16:  # pixel-index argmax of roi_pool_pair(pixel_argmax=True)
+        if layout != 0 or pool_channel:
+            raise ValueError("a pixel-index argmax needs NHWC data and pool_channel 0")
+        rc = lib.pcnn_roi_pool_bwd_px(_lib.ptr(grad.contiguous()), _lib.ptr(argmax.contiguous()), B, H, W, C,
+                                      _lib.ptr(rois), R, stride, int(batch_base), _lib.ptr(num_rois),
+                                      float(spatial_scale), int(pooled_height), int(pooled_width), _lib.ptr(dd),
+                                      _lib.ptr(ws), ws.numel(), _lib.stream_ptr())
+    else:
+        rc = lib.pcnn_roi_pool_bwd(_lib.ptr(grad.contiguous()), _lib.ptr(argmax.contiguous()), B, H, W, C, layout,
+                                   _lib.ptr(rois), R, stride, int(batch_base), _lib.ptr(num_rois),
+                                   float(spatial_scale), int(pooled_height), int(pooled_width), int(pool_channel),
+                                   _lib.ptr(dd), _lib.ptr(ws), ws.numel(), _lib.stream_ptr())
     _lib.check(rc, "roi_pool_grad")
     return dd
 

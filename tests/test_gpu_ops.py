@@ -119,6 +119,48 @@ def test_roi_pool_pair(hip, orc):
     assert (top[23:] == 7.0).all() and (a5[23:] == -7).all()
 
 
+def test_roi_pool_pair_pixel_argmax(hip, orc):
+    """Compact argmax of the fused step (uint16 pixel index, 0xFFFF = empty
+    bin): the oracle's flat argmax // C, pooled sums unchanged, and both pool
+    backwards on it bit-equal to the oracle's (jittered overlapping RoIs, RoIs
+    past the map edges, empty bins, a device row count)."""
+    rng = np.random.default_rng(13)
+    B, C = 2, 64
+    d5 = rng.normal(size=(B, 30, 40, C)).astype(np.float32)
+    d4 = rng.normal(size=(B, 60, 80, C)).astype(np.float32)
+    d4[1, 10:20, 10:30] = 0.25  # plateaus -> first-max ties
+    base = _rois(rng, 9, B, 480, 640, 1)
+    rows = []
+    for r in base:
+        for dx in (-0.05, 0.0, 0.05):
+            q = r.copy()
+            w = q[4] - q[2]
+            q[2] += dx * w; q[4] += dx * w
+            rows.append(q)
+    rois = np.array(rows, np.float32)
+    rois = rois[np.argsort(rois[:, 0], kind="stable")]
+    rois[0, 2:6] = [700.0, 500.0, 760.0, 560.0]  # entirely past the map: empty bins
+    R, live = len(rois), len(rois) - 2
+    nr = torch.tensor([live], dtype=torch.int32, device=D)
+    top = torch.full((R, 7, 7, C), 7.0, device=D)
+    a5 = torch.full((R, 7, 7, C), -7, dtype=torch.int16, device=D)
+    a4 = torch.full((R, 7, 7, C), -7, dtype=torch.int16, device=D)
+    rp.roi_pool_pair(T(d5), 1.0 / 16, T(d4), 1.0 / 8, T(rois), 7, 7, num_rois=nr, out=(top, a5, a4))
+    o5, oa5 = orc.roi_pool_fwd(d5, rois, 7, 7, 1.0 / 16, 0)
+    o4, oa4 = orc.roi_pool_fwd(d4, rois, 7, 7, 1.0 / 8, 0)
+    np.testing.assert_array_equal(top[:live].cpu().numpy(), (o5 + o4)[:live])
+    px = lambda oa: np.where(oa < 0, 0xFFFF, oa // C).astype(np.int64)
+    assert (oa5[:live] < 0).any()
+    np.testing.assert_array_equal(a5[:live].cpu().numpy().astype(np.int64) & 0xFFFF, px(oa5[:live]))
+    np.testing.assert_array_equal(a4[:live].cpu().numpy().astype(np.int64) & 0xFFFF, px(oa4[:live]))
+    assert (a5[live:] == -7).all()
+    g = rng.normal(size=(R, 7, 7, C)).astype(np.float32)
+    for data, arg, oa, s in ((d5, a5, oa5, 1.0 / 16), (d4, a4, oa4, 1.0 / 8)):
+        dd = rp.roi_pool_grad(T(data), T(rois), arg, T(g), 7, 7, s, 0, num_rois=nr)
+        od = orc.roi_pool_bwd(g[:live], oa[:live], data.shape, rois[:live], 7, 7, s, 0)
+        np.testing.assert_array_equal(dd.cpu().numpy(), od)
+
+
 def _add_inputs(rng, R, C=22, sym_rows=True):
     pts, sym = synth.rescaled_points(C)
     pred = rng.normal(size=(R, 4 * C)).astype(np.float32) * 0.5
