@@ -183,6 +183,19 @@ int pcnn_add_loss_fwd(const float* pred, const float* target, const float* weigh
                       int loss_norm_rows, const int32_t* loss_norm_rows_dev, float* loss, float* bottom_diff,
                       void* workspace, size_t workspace_bytes, void* stream);
 
+/* pcnn_add_loss_fwd split in two: pcnn_add_loss_prep classifies the rows
+ * (first class with weight > 0, cu.cc:47-52; the symmetric-row list) from the
+ * weights alone, so a caller may run it as soon as the Hough targets exist, on
+ * another stream; pcnn_add_loss_fwd_prepared is then pcnn_add_loss_fwd without
+ * that step, on the same workspace, weights and row count (ordered after the
+ * prep by the caller). */
+int pcnn_add_loss_prep(const float* weight, const float* symmetry, int R_cap, const int32_t* num_rois_dev, int C,
+                       int P, void* workspace, size_t workspace_bytes, void* stream);
+int pcnn_add_loss_fwd_prepared(const float* pred, const float* target, const float* weight, const float* points,
+                               const float* symmetry, int R_cap, const int32_t* num_rois_dev, int C, int P,
+                               float margin, int loss_norm_rows, const int32_t* loss_norm_rows_dev, float* loss,
+                               float* bottom_diff, void* workspace, size_t workspace_bytes, void* stream);
+
 /* out[i] = top_diff[0] * bottom_diff[i], n = rows * 4C */
 int pcnn_add_loss_bwd(const float* top_diff, const float* bottom_diff, int n, const int32_t* num_rois_dev,
                       int row_len, float* out, void* stream);

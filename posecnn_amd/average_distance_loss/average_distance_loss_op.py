@@ -12,8 +12,27 @@ import torch
 from .. import _lib
 
 
+def workspace_bytes(R, num_classes, num_points):
+    return _lib.load().pcnn_add_loss_workspace_size(R, num_classes, num_points)
+
+
+def average_distance_loss_prep(bottom_weight, bottom_symmetry, num_points, workspace, num_rois=None):
+    """Row classification of the loss (pcnn_add_loss_prep) into `workspace`
+    (uint8, >= workspace_bytes); may run on another stream as soon as the
+    weights exist.  Follow with average_distance_loss(..., prepared=True,
+    workspace=workspace) ordered after it."""
+    _lib.require_gpu(bottom_weight, bottom_symmetry, workspace)
+    w = bottom_weight.contiguous().float()
+    R, PC = w.shape
+    rc = _lib.load().pcnn_add_loss_prep(_lib.ptr(w), _lib.ptr(bottom_symmetry.contiguous().float()), R,
+                                        _lib.ptr(num_rois), PC // 4, int(num_points), _lib.ptr(workspace),
+                                        workspace.numel(), _lib.stream_ptr())
+    _lib.check(rc, "average_distance_loss_prep")
+
+
 def average_distance_loss(bottom_prediction, bottom_target, bottom_weight, bottom_point, bottom_symmetry, margin,
-                          name=None, num_rois=None, loss_norm_rows=0, loss_norm_rows_dev=None, out=None):
+                          name=None, num_rois=None, loss_norm_rows=0, loss_norm_rows_dev=None, out=None,
+                          workspace=None, prepared=False):
     _lib.require_gpu(bottom_prediction, bottom_target, bottom_weight, bottom_point, bottom_symmetry)
     if margin < 0:
         raise ValueError(f"Need margin >= 0, got {margin}")  # average_distance_loss_op.cc:64-65
@@ -22,18 +41,20 @@ def average_distance_loss(bottom_prediction, bottom_target, bottom_weight, botto
     C = PC // 4
     P = bottom_point.shape[1]
     lib = _lib.load()
-    ws = _lib.workspace(lib.pcnn_add_loss_workspace_size(R, C, P), pred.device, "add_loss")
+    if prepared and workspace is None:
+        raise ValueError("prepared=True needs the workspace average_distance_loss_prep wrote")
+    ws = workspace if workspace is not None else _lib.workspace(lib.pcnn_add_loss_workspace_size(R, C, P),
+                                                                pred.device, "add_loss")
     if out is None:
         loss = torch.empty((1,), dtype=torch.float32, device=pred.device)
         diff = torch.empty((R, PC), dtype=torch.float32, device=pred.device)
     else:
         loss, diff = out
-    rc = lib.pcnn_add_loss_fwd(_lib.ptr(pred), _lib.ptr(bottom_target.contiguous().float()),
-                               _lib.ptr(bottom_weight.contiguous().float()),
-                               _lib.ptr(bottom_point.contiguous().float()),
-                               _lib.ptr(bottom_symmetry.contiguous().float()), R, _lib.ptr(num_rois), C, P,
-                               float(margin), int(loss_norm_rows), _lib.ptr(loss_norm_rows_dev), _lib.ptr(loss),
-                               _lib.ptr(diff), _lib.ptr(ws), ws.numel(), _lib.stream_ptr())
+    fn = lib.pcnn_add_loss_fwd_prepared if prepared else lib.pcnn_add_loss_fwd
+    rc = fn(_lib.ptr(pred), _lib.ptr(bottom_target.contiguous().float()), _lib.ptr(bottom_weight.contiguous().float()),
+            _lib.ptr(bottom_point.contiguous().float()), _lib.ptr(bottom_symmetry.contiguous().float()), R,
+            _lib.ptr(num_rois), C, P, float(margin), int(loss_norm_rows), _lib.ptr(loss_norm_rows_dev), _lib.ptr(loss),
+            _lib.ptr(diff), _lib.ptr(ws), ws.numel(), _lib.stream_ptr())
     _lib.check(rc, "average_distance_loss")
     return loss, diff
 

@@ -406,8 +406,7 @@ __global__ void __launch_bounds__(kSymThreads) k_add_rows(const float* __restric
 __global__ void __launch_bounds__(1024) k_add_prep(const float* __restrict__ weight, const float* __restrict__ symmetry,
                                                     int R_cap, const int32_t* __restrict__ num_rois_dev, int C,
                                                     int32_t* __restrict__ rcls, int32_t* __restrict__ sym_rows,
-                                                    int32_t* __restrict__ nsym, int32_t* __restrict__ queue,
-                                                    uint32_t* __restrict__ done) {
+                                                    int32_t* __restrict__ nsym, int32_t* __restrict__ queue) {
   __shared__ int wcount[16];
   __shared__ int base;
   const int R = rows_of(num_rois_dev, R_cap);
@@ -439,7 +438,6 @@ __global__ void __launch_bounds__(1024) k_add_prep(const float* __restrict__ wei
   if (threadIdx.x == 0) {
     *nsym = base;
     *queue = 0;
-    *done = 0;
   }
 }
 
@@ -462,55 +460,37 @@ __device__ __forceinline__ void finish_row(int n, int R, int C, int nchunk, cons
   if (lane == 0) row_loss[n] = cls >= 0 ? s[0] : 0.f;
 }
 
-// Scalar loss: fixed-order sum of the row losses (thrust::reduce, cu.cc:333-334)
-// in the order of a 1024-thread pass — thread t sums rows t, t + 1024, ...,
-// waves of 64 threads reduce by wave_sum, the 16 wave sums add in wave order —
-// evaluated by the `nthreads` threads of one workgroup.
-__device__ __forceinline__ void add_total(int R, const float* __restrict__ row_loss, float* __restrict__ loss,
-                                          float* red /* [16] */) {
-  constexpr int kT = 1024;
-  const int nw = blockDim.x >> 6;
-  for (int j = 0; j < kT / (int)blockDim.x; j++) {
-    const int t = threadIdx.x + j * blockDim.x;
-    float my = 0.f;
-    for (int n = t; n < R; n += kT) my += row_loss[n];
-    my = pcnn::wave_sum(my);
-    if (pcnn::lane_id() == 0) red[j * nw + (threadIdx.x >> 6)] = my;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    float t = 0.f;
-    for (int i = 0; i < kT / 64; i++) t += red[i];
-    loss[0] = t;
-  }
-}
-
 // One wave per row: fold the chunk partials (fixed tree), write the row of
-// bottom_diff (zeros except the class's 4 channels) and the row loss.  The
-// last workgroup to finish (device-scope counter, zeroed by k_add_prep) then
-// adds the row losses into the scalar loss.
+// bottom_diff (zeros except the class's 4 channels) and the row loss.
+// Measured and dropped: the scalar total added by the last workgroup to
+// finish (device-scope counter): the agent-scope release fence of each of the
+// 288 workgroups writes back the XCD's L2, 12 -> 25 us for the pair of launches.
 __global__ void __launch_bounds__(256) k_add_finish_rows(int R_cap, const int32_t* __restrict__ num_rois_dev, int C,
                                                           int nchunk, const int32_t* __restrict__ rcls,
                                                           const float* __restrict__ partial,
                                                           float* __restrict__ row_loss,
-                                                          float* __restrict__ bottom_diff,
-                                                          uint32_t* __restrict__ done, float* __restrict__ loss) {
-  __shared__ float red[16];
-  __shared__ bool last;
+                                                          float* __restrict__ bottom_diff) {
   const int R = rows_of(num_rois_dev, R_cap);
   const int n = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const int lane = pcnn::lane_id();
-  finish_row(n, R, C, nchunk, rcls, partial, row_loss, bottom_diff, lane);
-  __threadfence();  // this workgroup's row losses before its count
-  __syncthreads();
-  if (threadIdx.x == 0) last = atomicAdd(done, 1u) == gridDim.x - 1;
-  __syncthreads();
-  if (!last) return;
-  __threadfence();  // every other workgroup's row losses after the count
-  add_total(R, row_loss, loss, red);
+  finish_row(n, R, C, nchunk, rcls, partial, row_loss, bottom_diff, pcnn::lane_id());
 }
 
-
+// Scalar loss: fixed-order sum of the row losses (thrust::reduce, cu.cc:333-334).
+__global__ void __launch_bounds__(1024) k_add_total(int R_cap, const int32_t* __restrict__ num_rois_dev,
+                                                     const float* __restrict__ row_loss, float* __restrict__ loss) {
+  __shared__ float red[16];
+  const int R = rows_of(num_rois_dev, R_cap);
+  float my = 0.f;
+  for (int n = threadIdx.x; n < R; n += blockDim.x) my += row_loss[n];
+  my = pcnn::wave_sum(my);
+  if (pcnn::lane_id() == 0) red[threadIdx.x >> 6] = my;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+    for (int i = 0; i < (int)(blockDim.x >> 6); i++) t += red[i];
+    loss[0] = t;
+  }
+}
 
 __global__ void k_add_bwd(const float* __restrict__ top_diff, const float* __restrict__ bottom_diff, int n,
                           float* __restrict__ out) {
@@ -536,10 +516,10 @@ extern "C" size_t pcnn_add_loss_workspace_size(int R_cap, int C, int P) {
          pcnn::align_up(R * sizeof(float), 256) + 3 * 256;
 }
 
-extern "C" int pcnn_add_loss_fwd(const float* pred, const float* target, const float* weight, const float* points,
-                                 const float* symmetry, int R_cap, const int32_t* num_rois_dev, int C, int P,
-                                 float margin, int loss_norm_rows, const int32_t* loss_norm_rows_dev, float* loss,
-                                 float* bottom_diff, void* workspace, size_t workspace_bytes, void* stream) {
+static int add_loss_fwd(const float* pred, const float* target, const float* weight, const float* points,
+                        const float* symmetry, int R_cap, const int32_t* num_rois_dev, int C, int P, float margin,
+                        int loss_norm_rows, const int32_t* loss_norm_rows_dev, float* loss, float* bottom_diff,
+                        void* workspace, size_t workspace_bytes, bool prepared, void* stream) {
   PCNN_REQUIRE(pred && target && weight && points && symmetry && loss && bottom_diff && workspace);
   PCNN_REQUIRE(R_cap > 0 && C > 0 && P > 0 && P <= kMaxPointsLds);
   if (workspace_bytes < pcnn_add_loss_workspace_size(R_cap, C, P)) return PCNN_ECAPACITY;
@@ -552,9 +532,9 @@ extern "C" int pcnn_add_loss_fwd(const float* pred, const float* target, const f
   int32_t* nsym = cv.take<int32_t>(1);
   int32_t* queue = cv.take<int32_t>(1);
   float* row_loss = cv.take<float>(R_cap);
-  uint32_t* done = cv.take<uint32_t>(1);
-  hipLaunchKernelGGL(k_add_prep, dim3(1), dim3(1024), 0, st, weight, symmetry, R_cap, num_rois_dev, C, rcls,
-                     sym_rows, nsym, queue, done);
+  if (!prepared)
+    hipLaunchKernelGGL(k_add_prep, dim3(1), dim3(1024), 0, st, weight, symmetry, R_cap, num_rois_dev, C, rcls,
+                       sym_rows, nsym, queue);
   // one persistent grid: symmetric (row, chunk) items of the device-side list, then the plain rows
   const long sym_items = (long)R_cap * nchunk + R_cap;  // symmetric (row, chunk) items, then plain rows
   const int sym_grid = (int)(sym_items < ADD_GRID ? sym_items : ADD_GRID);
@@ -562,9 +542,48 @@ extern "C" int pcnn_add_loss_fwd(const float* pred, const float* target, const f
                      target, weight, points, symmetry, R_cap, num_rois_dev, C, P, margin, loss_norm_rows,
                      loss_norm_rows_dev, nchunk, rcls, sym_rows, nsym, queue, partial);
   hipLaunchKernelGGL(k_add_finish_rows, dim3((R_cap + 3) / 4), dim3(256), 0, st, R_cap, num_rois_dev, C, nchunk,
-                     rcls, partial, row_loss, bottom_diff, done, loss);
+                     rcls, partial, row_loss, bottom_diff);
+  hipLaunchKernelGGL(k_add_total, dim3(1), dim3(1024), 0, st, R_cap, num_rois_dev, row_loss, loss);
   PCNN_CHECK_LAUNCH();
   return PCNN_OK;
+}
+
+extern "C" int pcnn_add_loss_fwd(const float* pred, const float* target, const float* weight, const float* points,
+                                 const float* symmetry, int R_cap, const int32_t* num_rois_dev, int C, int P,
+                                 float margin, int loss_norm_rows, const int32_t* loss_norm_rows_dev, float* loss,
+                                 float* bottom_diff, void* workspace, size_t workspace_bytes, void* stream) {
+  return add_loss_fwd(pred, target, weight, points, symmetry, R_cap, num_rois_dev, C, P, margin, loss_norm_rows,
+                      loss_norm_rows_dev, loss, bottom_diff, workspace, workspace_bytes, false, stream);
+}
+
+// The row classification of pcnn_add_loss_fwd on its own: it reads only the
+// weights (the Hough op's targets), so a caller can run it as soon as they
+// exist, on another stream, off the chain that produces the predictions.
+extern "C" int pcnn_add_loss_prep(const float* weight, const float* symmetry, int R_cap, const int32_t* num_rois_dev,
+                                  int C, int P, void* workspace, size_t workspace_bytes, void* stream) {
+  PCNN_REQUIRE(weight && symmetry && workspace && R_cap > 0 && C > 0 && P > 0 && P <= kMaxPointsLds);
+  if (workspace_bytes < pcnn_add_loss_workspace_size(R_cap, C, P)) return PCNN_ECAPACITY;
+  const int nchunk = (P + kPts - 1) / kPts;
+  pcnn::Carve cv(workspace);
+  (void)cv.take<float>((size_t)R_cap * nchunk * 5);
+  int32_t* rcls = cv.take<int32_t>(R_cap);
+  int32_t* sym_rows = cv.take<int32_t>(R_cap);
+  int32_t* nsym = cv.take<int32_t>(1);
+  int32_t* queue = cv.take<int32_t>(1);
+  hipLaunchKernelGGL(k_add_prep, dim3(1), dim3(1024), 0, (hipStream_t)stream, weight, symmetry, R_cap, num_rois_dev,
+                     C, rcls, sym_rows, nsym, queue);
+  PCNN_CHECK_LAUNCH();
+  return PCNN_OK;
+}
+
+extern "C" int pcnn_add_loss_fwd_prepared(const float* pred, const float* target, const float* weight,
+                                          const float* points, const float* symmetry, int R_cap,
+                                          const int32_t* num_rois_dev, int C, int P, float margin,
+                                          int loss_norm_rows, const int32_t* loss_norm_rows_dev, float* loss,
+                                          float* bottom_diff, void* workspace, size_t workspace_bytes,
+                                          void* stream) {
+  return add_loss_fwd(pred, target, weight, points, symmetry, R_cap, num_rois_dev, C, P, margin, loss_norm_rows,
+                      loss_norm_rows_dev, loss, bottom_diff, workspace, workspace_bytes, true, stream);
 }
 
 extern "C" int pcnn_add_loss_bwd(const float* top_diff, const float* bottom_diff, int n,

@@ -73,6 +73,7 @@ class PoseStep:
         self.t8 = torch.zeros((CAP, D), **f32)
         self.pred = torch.zeros((CAP, D), **f32)
         self.loss = torch.zeros((1,), **f32)
+        self.add_ws = None  # ADD-loss workspace (row classes written on the side stream after the vote)
         self.diff = torch.zeros((CAP, D), **f32)
         self.one = torch.ones((1,), **f32)
         self.dy8 = torch.zeros((CAP, D), **f32)
@@ -122,6 +123,21 @@ class PoseStep:
             return hv.hough_voting_gpu_capacity(label, vertex, extents, meta, gt, self.is_train, self.vthr,
                                                 self.vper, self.skip, global_batch=self.global_batch,
                                                 batch_base=self.batch_base, out=self.hough)
+
+    def add_prep(self, points, symmetry):
+        """The ADD loss's row classification (it reads only the Hough weights):
+        on the side stream right after the vote, joined before the loss."""
+        if self.add_ws is None:
+            self.add_ws = torch.empty(adl.workspace_bytes(CAP, self.C, points.shape[1]), dtype=torch.uint8,
+                                      device=self.dev)
+        h = self.hough
+        side = self.side_stream if self.timer is None else None
+        if side is not None:
+            side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side or torch.cuda.current_stream()):
+            adl.average_distance_loss_prep(h["weight"], symmetry, points.shape[1], self.add_ws,
+                                           num_rois=h["num_rois"][1:2])
+        self._prepped = True
 
     def exchange(self):
         """Global ADD-loss normaliser = max(sum of per-rank rows, 1): an
@@ -177,8 +193,14 @@ class PoseStep:
             self.norm_rows.clamp_(min=1)
         with self._t("head_add_loss_fwd"):
             ph.head_fwd(self.y8, h["weight"], self.t8, self.pred, num_rois=nr)
+            if not getattr(self, "_prepped", False):  # forward() called without step()
+                self.add_prep(points, symmetry)
+            if self.timer is None and self.side_stream is not None:
+                torch.cuda.current_stream().wait_stream(self.side_stream)  # the row classes (add_prep)
+            self._prepped = False
             adl.average_distance_loss(self.pred, h["target"], h["weight"], points, symmetry, self.margin,
-                                      num_rois=nr, loss_norm_rows_dev=self.norm_rows, out=(self.loss, self.diff))
+                                      num_rois=nr, loss_norm_rows_dev=self.norm_rows, out=(self.loss, self.diff),
+                                      workspace=self.add_ws, prepared=True)
         if self.dist is not None:  # nothing downstream reads the global loss: joined at the end of the step
             self._pending["loss"] = self.dist.all_reduce(self.loss, async_op=True)
         return self.loss
@@ -246,6 +268,7 @@ class PoseStep:
 
     def step(self, inputs):
         self.vote(inputs["label"], inputs["vertex"], inputs["extents"], inputs["meta"], inputs["gt"])
+        self.add_prep(inputs["points"], inputs["symmetry"])
         self.exchange()
         loss = self.forward(inputs["conv4"], inputs["conv5"], inputs["points"], inputs["symmetry"])
         if self.backward:

@@ -190,6 +190,25 @@ def test_add_loss(hip, orc):
     np.testing.assert_allclose(out.cpu().numpy(), 0.7 * diff.cpu().numpy(), rtol=0, atol=0)
 
 
+def test_add_loss_prepared_on_side_stream(hip, orc):
+    """pcnn_add_loss_prep on another stream + pcnn_add_loss_fwd_prepared ==
+    pcnn_add_loss_fwd, bit for bit (device row count, symmetric rows)."""
+    rng = np.random.default_rng(21)
+    pred, target, weight, pts, sym = _add_inputs(rng, 40)
+    nr = torch.tensor([31], dtype=torch.int32, device=D)
+    args = (T(pred), T(target), T(weight), T(pts), T(sym), 0.01)
+    loss0, diff0 = adl.average_distance_loss(*args, num_rois=nr)
+    ws = torch.empty(adl.workspace_bytes(40, 22, pts.shape[1]), dtype=torch.uint8, device=D)
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        adl.average_distance_loss_prep(args[2], args[4], pts.shape[1], ws, num_rois=nr)
+    torch.cuda.current_stream().wait_stream(side)
+    loss1, diff1 = adl.average_distance_loss(*args, num_rois=nr, workspace=ws, prepared=True)
+    np.testing.assert_array_equal(loss1.cpu().numpy(), loss0.cpu().numpy())
+    np.testing.assert_array_equal(diff1[:31].cpu().numpy(), diff0[:31].cpu().numpy())
+
+
 def test_add_loss_identity_zero(hip, orc):
     rng = np.random.default_rng(3)
     pred, target, weight, pts, sym = _add_inputs(rng, 8, sym_rows=False)
