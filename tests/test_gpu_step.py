@@ -1,0 +1,89 @@
+"""End-to-end parity of the fused pose step (posecnn_amd/pipeline.py) against
+an fp64 torch autograd restatement of the graph it runs
+(vgg16_convs.py:184-200 + TF's gradients):
+
+    x = pool5 + pool4 -> fc6 (relu) -> fc7 (relu) -> fc8 -> tanh * poses_weight
+      -> l2_normalize -> average_distance_loss  (network.py:393-445)
+
+The RoI pools, the Hough op and the ADD loss have their own bit-exact /
+1e-4 parity tests against the oracle; here the step's pooled rows and its ADD
+gradient (`step.diff`, d loss / d pred) are taken as given, and everything the
+step chains around them -- the split-bf16 x3 GEMMs, bias / ReLU epilogues, the
+ReLU masks of the backward, the bias column sums, the tail's tanh / l2-norm
+backward and the RoI-pool backward routing of dX -- is checked against fp64,
+on a small configuration (64 channels, 256 units)."""
+import numpy as np
+import pytest
+import torch
+
+from posecnn_amd import synth
+from posecnn_amd.pipeline import PoseStep
+
+pytestmark = pytest.mark.gpu
+D = torch.device("cuda")
+B, H, W, C, CH, UNITS = 2, 120, 160, 22, 64, 256
+
+
+def _close(a, ref, rt=1e-4):
+    """relative to the tensor's scale: |a - ref| <= rt * (|ref| + max |ref|)"""
+    np.testing.assert_allclose(a, ref, rtol=rt, atol=rt * float(np.abs(ref).max()))
+
+
+def test_pose_step_vs_fp64_autograd(hip, orc):
+    fr = synth.make_frames(B, H=H, W=W, num_classes=C, objects_per_image=4, seed=91)
+    g = torch.Generator().manual_seed(3)
+    conv4 = torch.randn((B, H // 8, W // 8, CH), generator=g)
+    conv5 = torch.randn((B, H // 16, W // 16, CH), generator=g)
+    pts, sym = synth.rescaled_points(C)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(D)
+    inputs = dict(label=t(fr["label"]), vertex=t(fr["vertex"]), extents=t(fr["extents"]), meta=t(fr["meta"]),
+                  gt=t(fr["gt"]), conv4=conv4.to(D), conv5=conv5.to(D), points=t(pts), symmetry=t(sym))
+    step = PoseStep(B, H, W, C, D, channels=CH, units=UNITS, is_train=1, skip_pixels=3)
+    # non-zero biases so the bias epilogues and column sums are exercised
+    w = step.weights
+    for b in (w.b6, w.b7, w.b8):
+        b.copy_(torch.randn(b.shape, generator=g) * 1e-3)
+    step.step(inputs)
+    torch.cuda.synchronize()
+    n = int(step.hough["num_rois"][1].item())
+    assert n > 8, "the synthetic frames should produce RoI rows"
+    f64 = lambda x: x.detach().double().cpu()
+
+    x = f64(step.pool[:n].reshape(n, -1))
+    W6, W7, W8 = (f64(v).requires_grad_() for v in (w.w6, w.w7, w.w8))
+    b6, b7, b8 = (f64(v).requires_grad_() for v in (w.b6, w.b7, w.b8))
+    x.requires_grad_()
+    y6 = torch.relu(x @ W6 + b6)
+    y7 = torch.relu(y6 @ W7 + b7)
+    y8 = y7 @ W8 + b8
+    pw = f64(step.hough["weight"][:n])
+    m = torch.tanh(y8) * pw
+    pred = m / torch.sqrt(torch.clamp((m * m).sum(1, keepdim=True), min=1e-12))
+
+    _close(step.y6[:n].cpu().numpy(), y6.detach().numpy())
+    _close(step.y7[:n].cpu().numpy(), y7.detach().numpy())
+    _close(step.pred[:n].cpu().numpy(), pred.detach().numpy())
+
+    # the ADD loss against the oracle on the step's own prediction (1e-4, its contract)
+    ol, od, _ = orc.average_distance_loss(step.pred[:n].cpu().numpy(), step.hough["target"][:n].cpu().numpy(),
+                                              step.hough["weight"][:n].cpu().numpy(), pts, sym, 0.01)
+    np.testing.assert_allclose(step.loss.cpu().numpy(), ol, rtol=1e-4)
+    np.testing.assert_allclose(step.diff[:n].cpu().numpy(), od, rtol=1e-4, atol=1e-7)
+
+    pred.backward(f64(step.diff[:n]))
+    gr = step.grads
+    for k, ref in (("w8", W8), ("b8", b8), ("w7", W7), ("b7", b7), ("w6", W6), ("b6", b6)):
+        _close(gr[k].cpu().numpy(), ref.grad.numpy())
+    dx = step.dx[:n].cpu().numpy()
+    _close(dx, x.grad.numpy())
+
+    # dX routed into both feature maps by the RoI-pool backward: the oracle's
+    # backward of the step's own dX and argmax (flat index = pixel * C + c)
+    box = step.hough["box"][:n].cpu().numpy()
+    for arg, data, dconv, s in ((step.arg5, conv5, step.dconv5, 1.0 / 16), (step.arg4, conv4, step.dconv4, 1.0 / 8)):
+        a = arg[:n].cpu().numpy().astype(np.int64)
+        if arg.dtype == torch.int16:
+            a &= 0xFFFF
+            a = np.where(a == 0xFFFF, -1, a * CH + np.arange(CH))
+        od = orc.roi_pool_bwd(dx.reshape(n, 7, 7, CH), a.astype(np.int32), tuple(data.shape), box, 7, 7, s, 0)
+        np.testing.assert_array_equal(dconv.cpu().numpy(), od)
