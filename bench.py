@@ -46,10 +46,11 @@ def parse():
     p.add_argument("--no-graph", action="store_true", help="time eager launches instead of a HIP graph")
     p.add_argument("--flat-argmax", action="store_true",
                    help="RoI-pool argmax as the reference's int32 flat index instead of uint16 pixel indices (A/B)")
-    p.add_argument("--precision", type=int, choices=[0, 1], default=1,
-                   help="FC GEMMs: 1 = split-bf16 x3 MFMA (fp32-class), 0 = fp32 MFMA")
-    p.add_argument("--no-fp32-leg", action="store_true",
-                   help="skip the extra fp32-MFMA (precision 0) timing reported beside the main line")
+    p.add_argument("--precision", type=int, choices=[0, 1, 2], default=2,
+                   help="FC GEMMs: 2 = exact 3-way split-bf16 x6 MFMA (fp32-faithful, default), "
+                        "1 = split-bf16 x3 MFMA (~2^-16 per product), 0 = fp32 MFMA")
+    p.add_argument("--no-fp32-leg", "--no-precision-legs", dest="no_legs", action="store_true",
+                   help="skip the secondary steps at the other GEMM precisions reported beside the main line")
     return p.parse_args()
 
 
@@ -180,6 +181,21 @@ def main():
             ops[k] = sum(a.elapsed_time(b) for a, b in evs) / nb
         vr_timer.clear()
 
+    # (1b) in-step GEMM times: eager steps with the stream overlap left on and
+    # HIP events around each FC GEMM on the stream it is launched on (the
+    # weight gradients run on the side stream beside the data-gradient
+    # chain), i.e. each kernel's duration as it runs in the timed step
+    gemm_in_step = {}
+    if step is not None:
+        step.gemm_timer = {}
+        nb = max(3, min(args.steps, 10))
+        for _ in range(nb):
+            run()
+        barrier()
+        for k, evs in step.gemm_timer.items():
+            gemm_in_step[k] = sum(a.elapsed_time(b) for a, b in evs) / len(evs)
+        step.gemm_timer = None
+
     # (2) timed region: K steps bracketed by a barrier + device sync on both
     # sides, max over ranks.  On one GPU the step runs both as a HIP-graph
     # replay (no host launch cost) and as eager launches on the step's two
@@ -230,20 +246,24 @@ def main():
         modes["hipgraph"] = measure(graph_replay)
     modes["eager"] = measure(run)
     mode = min(modes, key=modes.get)
-    # the same step with the FC GEMMs on exact fp32 MFMA (precision 0), eager,
-    # reported beside the line (the split-bf16 x3 GEMMs are fp32-class, not
-    # fp32-rounded; the reference runs these layers as fp32 matmuls)
-    fp32_leg = None
-    if args.workload == "full" and world == 1 and args.precision == 1 and not args.no_fp32_leg:
-        step0 = PoseStep(B, H, W, C, dev, is_train=1, skip_pixels=10, global_batch=gB, batch_base=rank * B,
-                         dist=dist, precision=0, weights=step.weights)
-        run0 = lambda: step0.step(inputs)
-        run0()
-        t0_ = measure(run0)
-        fp32_leg = {"value": round(gB * args.steps / t0_, 2), "unit": "frames/s",
-                    "ms_per_step": round(t0_ / args.steps * 1e3, 4), "fc_gemm": "fp32 MFMA (k_gemm_f32, 32x32x2f32)",
-                    "timing": "eager"}
-        del step0
+    # the same step with the FC GEMMs at the other precisions, eager, reported
+    # beside the line as labelled secondary keys: split-bf16 x3 (~2^-16 per
+    # product: fp32-class for the 1e-4 quaternion bound, not fp32-faithful) and
+    # plain fp32 MFMA
+    legs = {}
+    if args.workload == "full" and world == 1 and not args.no_legs:
+        for prec, key, desc in ((1, "bf16x3_step", "split-bf16 x3 MFMA (k_gemm_x3, hi*hi + hi*lo + lo*hi)"),
+                                (0, "fp32_mfma_step", "fp32 MFMA (k_gemm_f32, 32x32x2f32)")):
+            if prec == args.precision:
+                continue
+            step0 = PoseStep(B, H, W, C, dev, is_train=1, skip_pixels=10, global_batch=gB, batch_base=rank * B,
+                             dist=dist, precision=prec, weights=step.weights)
+            run0 = lambda: step0.step(inputs)
+            run0()
+            t0_ = measure(run0)
+            legs[key] = {"value": round(gB * args.steps / t0_, 2), "unit": "frames/s",
+                         "ms_per_step": round(t0_ / args.steps * 1e3, 4), "fc_gemm": desc, "timing": "eager"}
+            del step0
     elapsed = modes[mode]
     frames = gB * args.steps
     # per-step distribution of the reported mode (after the timed region, which
@@ -269,21 +289,26 @@ def main():
                      "kernel": "hough_voting_gpu op (label compaction + interval vote + peak + emit)",
                      "bytes_per_launch": vote_bytes, "practical_peak": practical,
                      "frac_of_practical": round(ach / practical["GB/s"], 4)}
-    if full and ops:
+    if full and gemm_in_step:
+        # dominant kernel: the slowest fc6 GEMM by its in-step HIP-event time
+        # (pass 1b: the launch as it runs in the overlapped step, on its own
+        # stream); algorithmic fp32 flops 2 R K N per launch
         R = max(nrows, 1)
         K6, U = 49 * 512, 4096
-        gem = {"gemm_fc6_fwd": 2.0 * R * K6 * U, "gemm_fc6_dx": 2.0 * R * K6 * U, "gemm_fc6_dw": 2.0 * R * K6 * U}
-        dom = max(gem, key=lambda k: ops.get(k, 0.0))
-        tf = gem[dom] / (ops[dom] / 1e3) / 1e12
-        if args.precision == 1:
-            # algorithmic fp32 flops against the rate of the 3 bf16 MFMA passes that produce them;
-            # fc6_fwd runs split-K (k_gemm_x3 + k_gemm_reduce), fc6_dw / fc6_dx one k_gemm_x3 launch
-            peak, kname = BF16_MFMA_PEAK_TFS / 3, (f"k_gemm_x3 ({dom}{' + k_gemm_reduce' if dom == 'gemm_fc6_fwd' else ''}"
-                                                   f", split-bf16 x3 MFMA 32x32x16, R={R})")
-        else:
-            peak, kname = FP32_MFMA_PEAK_TFS, f"k_gemm_f32 ({dom}, fp32 MFMA 32x32x2, R={R})"
+        gem = {"fc6_fwd": 2.0 * R * K6 * U, "fc6_dx": 2.0 * R * K6 * U, "fc6_dw": 2.0 * R * K6 * U}
+        dom = max(gem, key=lambda k: gemm_in_step.get(k, 0.0))
+        tf = gem[dom] / (gemm_in_step[dom] / 1e3) / 1e12
+        fam, peak, form = {2: ("k_gemm_x6", BF16_MFMA_PEAK_TFS / 6, "3-way split-bf16 x6 MFMA 32x32x16"),
+                           1: ("k_gemm_x3", BF16_MFMA_PEAK_TFS / 3, "split-bf16 x3 MFMA 32x32x16"),
+                           0: ("k_gemm_f32", FP32_MFMA_PEAK_TFS, "fp32 MFMA 32x32x2")}[args.precision]
+        # the split kernels' peak: the bf16 dense MFMA rate over the MFMA passes per fp32 product;
+        # fc6_fwd runs split-K (+ k_gemm_reduce, inside its time)
+        kname = f"{fam} ({dom}{' + k_gemm_reduce' if dom == 'fc6_fwd' else ''}, {form}, R={R})"
         roof = {"bound": "mfma", "achieved": round(tf, 2), "peak": round(peak, 1), "unit": "TFLOP/s",
-                "frac": round(tf / peak, 4), "traffic": None, "kernel": kname, "flops_per_launch": gem[dom]}
+                "frac": round(tf / peak, 4), "traffic": None, "kernel": kname, "flops_per_launch": gem[dom],
+                "us_per_launch_in_step": round(gemm_in_step[dom] * 1e3, 1),
+                "us_per_launch_serialised": round(ops.get(f"gemm_{dom}", 0.0) * 1e3, 1),
+                "timing": "HIP events on the launching stream, overlapped step (bench pass 1b)"}
     else:
         roof = roof_vote
     # HBM traffic of the same launches from the committed rocprofv3 FETCH_SIZE /
@@ -293,8 +318,8 @@ def main():
         try:
             pmc = json.load(open(pmc_path))
             wl = pmc.get(args.workload, {})
-            if roof is not None and full and args.precision == 1:
-                ent = wl.get(f"k_gemm_x3:{dom.replace('gemm_', '')}")
+            if roof is not None and full and args.precision in (1, 2):
+                ent = wl.get(f"{fam}:{dom}")
                 if ent:
                     roof["traffic"] = round(ent["traffic_bytes"])
                     roof["traffic_unit"] = "bytes/launch (rocprofv3 2*FETCH_SIZE + WRITE_SIZE)"
@@ -326,8 +351,13 @@ def main():
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "higher_is_better": True,
             "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "f32 (FC GEMMs split-bf16x3 MFMA, fp32 accumulate)" if args.precision == 1 else "f32",
+            # no published GPU number exists: the ratio to the
+            # measured CPU baseline of BASELINE.md §2, on this host
+            "vs_baseline": round(value / cpu["value"], 2) if cpu and cpu.get("value") else None,
+            "vs_baseline_basis": "cpu_baseline.value (reference CPU Houghvoting op, BASELINE.md §2)",
+            "dtype": {2: "f32 (FC GEMMs: exact 3-way split-bf16 x6 MFMA, products within 2^-24, fp32 accumulate: "
+                         "fp32-faithful)",
+                      1: "f32 (FC GEMMs split-bf16x3 MFMA, fp32 accumulate)", 0: "f32"}[args.precision],
             "data": "synthetic (seeded label/vertex maps per minibatch.py:517-575; random conv4_3/conv5_3; "
                     "random-init FC weights" + ("; LINEMOD box-surface model points, rendered box depth, random "
                                                 "backprojection features" if linemod else "") + ")",
@@ -339,19 +369,21 @@ def main():
                              "configs[1]: hough_voting_gpu(test) + roi_pool x2 forward"),
                 "global_batch": gB, "per_rank_batch": B, "height": H, "width": W, "num_classes": C,
                 "skip_pixels": 10, "index_size": 128 // gB, "roi_rows_rank0": nrows,
-                "fc_gemm": "split-bf16x3 MFMA, fp32 accumulate" if args.precision == 1 else "fp32 MFMA",
+                "fc_gemm": {2: "3-way split-bf16 x6 MFMA (fp32-faithful)", 1: "split-bf16x3 MFMA, fp32 accumulate",
+                            0: "fp32 MFMA"}[args.precision],
                 "parallelism": (f"image-shard x{world} (RCCL: row-count/loss all-reduce, fc weight-gradient "
                                 f"row blocks via all-to-all + all-gather)") if world > 1 else "single",
             },
             "roofline": roof,
             "roofline_vote": roof_vote,
             "ops_ms_per_step": {k: round(v, 4) for k, v in ops.items()},
+            "gemm_us_in_step": {k: round(v * 1e3, 1) for k, v in gemm_in_step.items()},
             "timing": mode,
             "timing_ms_per_step": {k: round(v / args.steps * 1e3, 4) for k, v in modes.items()},
             "step_ms_distribution": dist_steps,
             "hbm_practical_peak": practical,
             "cpu_baseline": cpu,
-            "fp32_mfma_step": fp32_leg,
+            **legs,
         }
         print(json.dumps(out), flush=True)
     if dist is not None:
@@ -393,33 +425,74 @@ def d2d_gbs(dev, nbytes=1 << 30, reps=5):
     return {"GB/s": round(gbs, 1), "method": f"torch copy_ D2D of {nbytes >> 20} MiB x{reps} (read + write bytes)"}
 
 
+def host_cpu():
+    """CPU model and core counts of this host (recorded beside the baseline)."""
+    import subprocess
+    info = {"model": None, "logical_cpus": os.cpu_count(), "physical_cores": None,
+            "affinity_cpus": len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None}
+    try:
+        cores, model = set(), None
+        phys = core = None
+        for line in open("/proc/cpuinfo"):
+            k, _, v = line.partition(":")
+            k, v = k.strip(), v.strip()
+            if k == "model name" and model is None:
+                model = v
+            elif k == "physical id":
+                phys = v
+            elif k == "core id":
+                core = v
+            elif not k and phys is not None:
+                cores.add((phys, core))
+                phys = core = None
+        info["model"] = model
+        info["physical_cores"] = len(cores) or None
+    except OSError:
+        pass
+    try:  # GNU nproc: the processing units available to this process (honours OMP_NUM_THREADS)
+        info["nproc"] = int(subprocess.run(["nproc"], capture_output=True, text=True, timeout=10).stdout)
+    except Exception:
+        info["nproc"] = info["affinity_cpus"] or os.cpu_count()
+    return info
+
+
 def cpu_baseline(fr, train, budget_s):
     """Reference CPU Houghvoting op (oracle restatement, OpenMP) on a bounded
-    sample of the same frames; frames/s on this host's cores."""
+    sample of the same frames: frames/s at nproc threads (BASELINE.md §2:
+    OMP_NUM_THREADS=$(nproc)) and at 1 thread, on this host's cores.  The
+    vertex map is given in the CPU op's raw-distance convention
+    (synth.cpu_vertex)."""
     try:
         from oracle import oracle
         oracle.build()
     except Exception as e:  # the oracle is test infrastructure; absence is reported, not fatal
         return {"value": None, "error": f"oracle unavailable: {e}"}
-    import numpy as np
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(os.cpu_count() or 1, 16)
+    from posecnn_amd import synth
+    cpu = host_cpu()
+    threads = cpu["nproc"]
+    vert = synth.cpu_vertex(fr["vertex"])
     B = fr["label"].shape[0]
-    # warm-up frame
-    oracle.ransac_hough(fr["label"][:1], fr["vertex"][:1], fr["extents"], fr["meta"][:1], int(train), threads)
-    n = 0
-    t0 = time.perf_counter()
-    while True:
-        for i in range(B):
-            oracle.ransac_hough(fr["label"][i:i + 1], fr["vertex"][i:i + 1], fr["extents"], fr["meta"][i:i + 1],
-                                int(train), threads)
-            n += 1
-        if time.perf_counter() - t0 > budget_s or n >= 400:
-            break
-    dt = time.perf_counter() - t0
-    return {"value": round(n / dt, 2), "unit": "frames/s", "cores": threads, "kind": "port",
+
+    def rate(nt, budget):
+        oracle.ransac_hough(fr["label"][:1], vert[:1], fr["extents"], fr["meta"][:1], int(train), nt)  # warm-up
+        n, t0 = 0, time.perf_counter()
+        while True:
+            for i in range(B):
+                oracle.ransac_hough(fr["label"][i:i + 1], vert[i:i + 1], fr["extents"], fr["meta"][i:i + 1],
+                                    int(train), nt)
+                n += 1
+            if time.perf_counter() - t0 > budget or n >= 400:
+                break
+        return n, n / (time.perf_counter() - t0)
+
+    n, fps = rate(threads, budget_s)
+    n1, fps1 = rate(1, budget_s / 2)
+    return {"value": round(fps, 2), "unit": "frames/s", "cores": threads, "kind": "port",
+            "single_thread": {"value": round(fps1, 2), "unit": "frames/s", "cores": 1, "frames": n1},
+            "host": cpu,
             "sample": f"{n} frames ({B} distinct synthetic 640x480 frames cycled), "
                       f"reference Houghvoting op (preemptive RANSAC, {'train' if train else 'test'} mode) "
-                      f"restated in oracle/orc_ransac.cpp, OpenMP {threads} threads"}
+                      f"restated in oracle/orc_ransac.cpp, OpenMP {threads} threads (nproc on this host)"}
 
 
 if __name__ == "__main__":

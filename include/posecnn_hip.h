@@ -227,7 +227,10 @@ int pcnn_backproject_bwd(const float* top_diff, const float* depth, const float*
  *  epilogue: bias (N) added if non-NULL; act 0 none, 1 relu;
  *            mask (optional, ldm) -> C *= (mask > 0)  (relu backward)
  *  precision: 0 = exact fp32 MFMA (v_mfma_f32_32x32x2_f32),
- *             1 = split-bf16 x3 MFMA (fp32-class accuracy, ~5x the fp32 rate)
+ *             1 = split-bf16 x3 MFMA (hi*hi + hi*lo + lo*hi: ~2^-16 per product),
+ *             2 = exact three-way split-bf16 x6 MFMA (hi/mid/lo planes, six
+ *                 products: within 2^-24 |a||b| per product, fp32
+ *                 accumulation -- fp32-faithful; the pose step's default)
  *  Deterministic (split-K partials are reduced in fixed order).
  *  workspace: >= pcnn_gemm_workspace_size() bytes, one per stream.
  * ------------------------------------------------------------------------- */

@@ -204,6 +204,18 @@ def ransac_hough(label, vertex, extents, meta, is_train=0, num_threads=0):
     return rows[:min(n, cap)]
 
 
+def ransac_hough_op(label, vertex, extents, meta, is_train=0, num_threads=0):
+    """The reference CPU op's outputs (hough_voting_op.cc:161-225): top_box
+    (R, 6) [b, cls, x1, y1, x2, y2] and top_pose (R, 7); with no detection in
+    the batch, the one dummy row box [0, -1, 0, 0, 1, 1], pose [1, 0, ...]
+    (:163-177; cv::Vec zero-initialises the rest)."""
+    rows = ransac_hough(label, vertex, extents, meta, is_train, num_threads)
+    if rows.shape[0] == 0:
+        rows = np.zeros((1, 13), np.float32)
+        rows[0, [1, 4, 5, 6]] = (-1, 1, 1, 1)
+    return np.ascontiguousarray(rows[:, :6]), np.ascontiguousarray(rows[:, 6:])
+
+
 def box_nms(dets, thresh):
     """lib/utils/nms.py:3-32 (canonical tie order): kept row indices, score descending."""
     d, dp = _f(dets)

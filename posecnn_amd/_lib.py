@@ -140,11 +140,13 @@ def stream_ptr(stream=None):
 _ws = {}
 
 
-def workspace(nbytes, device, tag="default"):
-    """Per-(device, tag, current stream) grow-only byte workspace (no
-    allocation on the hot path once sized; ops on different streams never
-    share scratch)."""
-    key = (str(device), tag, torch.cuda.current_stream(device).cuda_stream)
+def workspace(nbytes, device, tag="default", stream=None):
+    """Per-(device, tag, stream) grow-only byte workspace (no allocation on
+    the hot path once sized).  `stream` is the stream the op launches on
+    (default: the current stream): ops on different streams never share
+    scratch, so concurrent calls stay reentrant."""
+    s = stream if stream is not None else torch.cuda.current_stream(device)
+    key = (str(device), tag, s.cuda_stream)
     buf = _ws.get(key)
     if buf is None or buf.numel() < nbytes:
         buf = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)

@@ -15,47 +15,17 @@
 // host sync.  Small-tile-count shapes split K; partial slabs are reduced in
 // fixed order by a second kernel that also applies the epilogue (bit-stable
 // across runs).  The pool5 + pool4 addition is fused into the A-tile load.
-#include "pcnn_common.h"
+#include "gemm_common.h"
 #include <math.h>
 #include <stdlib.h>
-#include <type_traits>
+
+using namespace pcnn_gk;
 
 namespace {
 
 constexpr int BM = 128, BN = 128, BK = 16;
 constexpr int kGemmThreads = 256;
 constexpr int kMaxSplit = 8;   // fp32 kernel
-
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-
-struct GemmArgs {
-  int M, N, K;
-  const float* A;
-  const float* A2;
-  int lda;
-  const float* B;
-  int ldb;
-  float* C;
-  int ldc;
-  const float* bias;
-  int act;
-  const float* mask;
-  int ldm;
-  const int32_t* M_dev;
-  const int32_t* K_dev;
-  float* slab;  // split-K partials [kMaxSplit][M][N] (fp32 path); x3: stream-K segment slabs
-  int prec;     // 0 fp32 MFMA, 1 split-bf16 x3 (selects the split rule)
-  int tile;     // x3 tile edge (256 or 128), chosen on the host
-  int xgrid;    // x3 launch grid (the plan depends on it; k_gemm_reduce re-derives the plan)
-  int c_stream; // x3: store C non-temporally (outputs far beyond the caches, e.g. the fc6 weight gradient)
-};
-
-__device__ __forceinline__ int eff_dim(int full, const int32_t* dev) {
-  if (!dev) return full;
-  int v = *dev;
-  return v < full ? (v < 0 ? 0 : v) : full;
-}
 
 // split-K factor for the effective shape (shared by GEMM and reducer)
 __host__ __device__ __forceinline__ int split_for(int M, int N, int K) {
@@ -269,8 +239,6 @@ __global__ void __launch_bounds__(kGemmThreads) k_gemm_f32(GemmArgs g) {
 // CU): 4x the workgroups of an output- or latency-bound shape.  Measured
 // (scripts/gemm_bench.py): fc8 23-26 us vs 33-40 us at 256; 128 everywhere
 // loses 20-25% on fc6 and is even on fc7.
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 constexpr int XBK = 32;
 // Tile geometry: T = 256 (the large shapes) or 128 (shapes with an edge of
 // <= 128 or too few 256-tiles to fill the chip: 256 threads as 2 x 2 waves of
@@ -294,92 +262,6 @@ struct XTile {
 __device__ __forceinline__ int x_off(int row, int c) {
   const int g = ((row >> 2) & 1) | ((((row >> 1) ^ (row >> 3)) & 1) << 1);
   return row * 64 + 16 * (c ^ g);
-}
-
-// tile edge of the x3 kernel for a (capacity) shape
-__host__ __device__ __forceinline__ int tile_x3(int M, int N, int K) {
-#ifdef PCNN_FORCE_TILE
-  return PCNN_FORCE_TILE;
-#endif
-  return (M <= 128 || N <= 128 || K <= 128) ? 128 : 256;
-}
-
-// Plan of the x3 kernel for an effective shape (M and K may live on the
-// device; the host evaluates the same plan for workspace sizing).
-//  - M tiles are balanced: mt = ceil(M / T) tiles of Tm rows each, Tm the
-//    smallest multiple of 32 >= M / mt (M = 405: 224 + 181 rows, not
-//    256 + 149), so the tiles of one N column carry about the same number of
-//    live 32-row accumulator blocks; rows past a tile's end are padding whose
-//    MFMAs the K loop skips.  The tiles of a column run side by side on one
-//    XCD, share their B panel through L2 and finish together (fc6 dX, 196
-//    tiles in one round: 318 -> 295 us).
-//  - Tile mode: whole tiles dealt round-robin.
-//  - Split-K (fewer than G/2 tiles, long K): S K slices per tile, partial
-//    slabs reduced in slice order by k_gemm_reduce (the forward shapes).
-//  Measured and dropped: stream-K over the tiles of a column (K ranges cut
-//  evenly over workgroup pairs, partial tiles fixed up in fixed order by the
-//  last segment to finish): fc6 dX 295 -> 343 us — the slab round trip and
-//  the per-segment fix-up cost more than the balance gains.
-constexpr int kMaxSplitX = 16;   // split-K slices
-struct XPlan {
-  int mt, nt, ns, Tm, tiles, mode, S;
-  bool m_fast;  // tile order: the dimension with fewer tiles runs fastest (its
-                // neighbours share the other operand's tile in L2)
-  __host__ __device__ int mi_of(int t) const { return m_fast ? t % mt : t / nt; }
-  __host__ __device__ int ni_of(int t) const { return m_fast ? t / mt : t % nt; }
-};
-
-__host__ __device__ __forceinline__ XPlan x_plan(int Meff, int N, int Keff, int T, int G) {
-  XPlan p;
-  p.mt = (Meff + T - 1) / T;
-  p.nt = (N + T - 1) / T;
-  p.ns = (Keff + XBK - 1) / XBK;
-  p.tiles = p.mt * p.nt;
-  p.m_fast = p.mt <= p.nt;
-  const int rows = p.mt ? (Meff + p.mt - 1) / p.mt : 0;
-  p.Tm = (rows + 31) / 32 * 32;
-  p.mode = 0;
-  p.S = 1;
-#ifdef PCNN_NOSPLIT
-  if (false) {
-#else
-  if (p.tiles > 0 && p.tiles < G / 2) {
-#endif
-    int s = G / p.tiles;
-    if (s > p.ns / 4) s = p.ns / 4;
-    if (s > kMaxSplitX) s = kMaxSplitX;
-    if (s > 1) {
-      p.mode = 1;
-      p.S = s;
-    }
-  }
-  return p;
-}
-
-// Operand view for buffer loads: SGPR descriptor + the extent in bytes.  All
-// per-lane address math is one 32-bit voffset; uniform parts go to soffset.
-// Masked lanes use voffset kXOob (>= every extent, < 2^31): the hardware
-// range check returns 0 whether or not soffset takes part in it.
-constexpr unsigned kXOob = 0x80000000u;
-struct XOp {
-  __amdgpu_buffer_rsrc_t rs;
-  int ld;
-  bool valid;
-};
-__device__ __forceinline__ XOp x_op(const float* P, int ld, long elems) {
-  XOp o;
-  o.valid = P != nullptr;
-  o.rs = __builtin_amdgcn_make_buffer_rsrc((void*)P, (short)0, (int)(elems * 4), 0x00020000);
-  o.ld = ld;
-  return o;
-}
-__device__ __forceinline__ float x_ld1(const XOp& o, unsigned voff, int soff) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(o.rs, voff, soff, 0));
-}
-typedef float xf4 __attribute__((ext_vector_type(4)));
-constexpr int kXNonTemporal = 2;  // buffer cache-policy bit: nt
-__device__ __forceinline__ xf4 x_ld4(const XOp& o, unsigned voff, int soff) {
-  return __builtin_bit_cast(xf4, __builtin_amdgcn_raw_buffer_load_b128(o.rs, voff, soff, 0));
 }
 
 // Staging of one 256-row x 32-k operand tile into 16 fp32 registers.
@@ -454,8 +336,6 @@ __device__ __forceinline__ void x_load(const XOp& P, const XOp& P2, int r0, int 
 // (RNE), lo = bf16(x - hi) (the subtraction is exact).  One pack-convert for
 // both hi halves, the fp32 value of each hi half by a shift / mask of that
 // pack, one pack-convert for both lo halves.
-typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
-typedef float f32x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ void x_split2(float a, float b, unsigned& hi, unsigned& lo) {
 #ifdef PCNN_OLDSPLIT
   const __bf16 ha = (__bf16)a, hb = (__bf16)b;
@@ -502,10 +382,6 @@ __device__ __forceinline__ void x_store(const float (&v)[16], char* hi, char* lo
   for (int q = 0; q < 4; q++) x_store_part<T, KC>(v, hi, lo, q);
 }
 
-template <int N>
-using IC = std::integral_constant<int, N>;
-
-
 // GEN: the general form (split-K and stream-K plans, for device-side M);
 // without it the kernel runs whole tiles only (a static-M shape whose plan
 // is tile mode, e.g. the weight gradients) and carries none of the partial-
@@ -518,7 +394,7 @@ __global__ void __launch_bounds__(XTile<T>::threads, T == 256 ? 1 : 2) k_gemm_x3
   constexpr bool A_KC = !A_T, B_KC = B_T;
   const int Meff = eff_dim(g.M, g.M_dev);
   const int Keff = eff_dim(g.K, g.K_dev);
-  XPlan pl = x_plan(Meff, g.N, Keff, T, g.xgrid);
+  XPlan pl = x_plan(Meff, g.N, Keff, T, g.xgrid, XBK);
   if constexpr (!GEN) {
     pl.mode = 0;
     pl.S = 1;
@@ -671,82 +547,7 @@ __global__ void __launch_bounds__(XTile<T>::threads, T == 256 ? 1 : 2) k_gemm_x3
 #endif
     }
 
-    // epilogue (one uniform branch: slab or C), otherwise branch-free: bias /
-    // mask come in through buffer loads and results leave through buffer
-    // stores, out-of-range lanes masked by an out-of-extent offset (loads
-    // return 0, stores are dropped).  The 16 mask values of group (j, i) are
-    // issued one group ahead of their use, so the tile pays one mask latency,
-    // not 8.
-    // Accumulator blocks: EJ (N) x EI (M) blocks of EB x EB, EQ values per
-    // lane.  Value q of block (i, j) sits at row m0 + rlane + qrow(i, q),
-    // column n0 + clane + 32 j.  Every per-value term is uniform (a scalar
-    // add / compare against the lane's one base): left to itself the
-    // compiler precomputes a lane's 64 row indices once per kernel, spills
-    // them, and reloads one per store behind a full vmcnt drain.
-    constexpr int EJ = 2, EI = AM, EQ = 16, EB = 32;
-    const int rlane = wm * (T / 2) + 4 * hsel, clane = wn * 64 + r;
-    auto qrow = [](int i, int q) { return i * EB + (q & 3) + 8 * (q >> 2); };
-    const int rlim = rl - m0, clim = g.N - n0;  // rows / columns of the tile that exist
-    if (pl.mode == 1) {  // split-K slice: raw partial sums to slab z
-      const XOp oslab = x_op(g.slab, g.N, (long)pl.S * g.M * g.N);
-      const unsigned sb = (unsigned)(((z * g.M + m0 + rlane) * g.N + n0 + clane) * 4);
-#pragma unroll
-      for (int j = 0; j < EJ; j++)
-#pragma unroll
-        for (int i = 0; i < EI; i++)
-#pragma unroll
-          for (int q = 0; q < EQ; q++) {
-            const bool ok = clane < clim - j * EB && rlane < rlim - qrow(i, q);
-            // (a scalar copy first: __builtin_bit_cast of an ext-vector
-            // element subscript reads element 0 with this compiler)
-            const float v = acc[i][j][q];
-            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), oslab.rs,
-                                                  ok ? sb + (unsigned)((qrow(i, q) * g.N + j * EB) * 4) : kXOob,
-                                                  0, 0);
-          }
-      return;
-    }
-    const bool msk = g.mask != nullptr;
-    const XOp oc = x_op(g.C, g.ldc, (long)(g.M - 1) * g.ldc + g.N);
-    const XOp obias = x_op(g.bias, 0, g.N);
-    const XOp omask = x_op(g.mask, g.ldm, g.mask ? (long)(g.M - 1) * g.ldm + g.N : 0);
-    const unsigned cbase = (unsigned)(((m0 + rlane) * g.ldc + n0 + clane) * 4);
-    const unsigned mbase = (unsigned)(((m0 + rlane) * g.ldm + n0 + clane) * 4);
-    float mv[2][EQ];
-    auto load_mask = [&](int gi, float (&d)[EQ]) {
-      const int j = gi / EI, i = gi % EI;
-#pragma unroll
-      for (int q = 0; q < EQ; q++) {
-        const bool ok = clane < clim - j * EB && rlane < rlim - qrow(i, q);
-        d[q] = x_ld1(omask, ok ? mbase + (unsigned)((qrow(i, q) * g.ldm + j * EB) * 4) : kXOob, 0);
-      }
-    };
-    if (msk) load_mask(0, mv[0]);
-#pragma unroll
-    for (int j = 0; j < EJ; j++) {
-      const bool nok = clane < clim - j * EB;
-      const float bv = g.bias ? x_ld1(obias, nok ? (unsigned)((n0 + clane + j * EB) * 4) : kXOob, 0) : 0.f;
-#pragma unroll
-      for (int i = 0; i < EI; i++) {
-        const int gi = EI * j + i;
-        if (msk && gi + 1 < EJ * EI) load_mask(gi + 1, mv[(gi + 1) & 1]);
-#pragma unroll
-        for (int q = 0; q < EQ; q++) {
-          const bool ok = nok && rlane < rlim - qrow(i, q);
-          float v = acc[i][j][q] + bv;
-          if (g.act == 1) v = v > 0.f ? v : 0.f;
-          if (msk && !(mv[gi & 1][q] > 0.f)) v = 0.f;
-#ifdef PCNN_ABL_NOEPI
-          if (v != 1.2345e-30f) continue;
-#endif
-          const unsigned co = ok ? cbase + (unsigned)((qrow(i, q) * g.ldc + j * EB) * 4) : kXOob;
-          if (g.c_stream)  // non-temporal: the output is far larger than L2 + MALL
-            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), oc.rs, co, 0, kXNonTemporal);
-          else
-            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), oc.rs, co, 0, 0);
-        }
-      }
-    }
+    x_epilogue<T, AM>(g, pl, acc, m0, n0, rl, z, wm, wn, r, hsel);
   };
 
   // this workgroup's items: every active-th (tile, K slice); one call site,
@@ -762,7 +563,7 @@ __global__ void __launch_bounds__(XTile<T>::threads, T == 256 ? 1 : 2) k_gemm_x3
 __global__ void __launch_bounds__(256) k_gemm_reduce(GemmArgs g) {
   const int Meff = eff_dim(g.M, g.M_dev);
   const int Keff = eff_dim(g.K, g.K_dev);
-  const int S = g.prec ? x_plan(Meff, g.N, Keff, g.tile, g.xgrid).S : split_for(Meff, g.N, Keff);
+  const int S = g.prec ? x_plan(Meff, g.N, Keff, g.tile, g.xgrid, split_bk(g.prec)).S : split_for(Meff, g.N, Keff);
   if (S == 1) return;
   // slab sums in slice order z = 0, 1, ... (0 + s0 == s0, so starting from
   // s0 is the same fp32 sum); float4 along N when rows stay 16-B aligned
@@ -891,10 +692,10 @@ static int x3_max_grid(int T) { return T == 256 ? XTile<256>::grid : XTile<128>:
 
 extern "C" size_t pcnn_gemm_workspace_size(int M, int N, int K, int m_dynamic, int precision) {
   if (M <= 0 || N <= 0) return 256;
-  if (precision == 1) {
+  if (precision == 1 || precision == 2) {
     // split-K slabs [S][M][N] at the largest split any effective M <= M can take (fewest tiles)
     const int T = tile_x3(M, N, K);
-    const XPlan lo = x_plan(m_dynamic ? 1 : M, N, K, T, x3_max_grid(T));
+    const XPlan lo = x_plan(m_dynamic ? 1 : M, N, K, T, x3_max_grid(T), split_bk(precision));
     return lo.mode == 1 ? pcnn::align_up((size_t)lo.S * M * N * sizeof(float), 256) + 256 : 256;
   }
   // fp32 path: split-K partial slabs; the split only grows when the device-side M shrinks
@@ -907,7 +708,7 @@ extern "C" int pcnn_gemm(int M, int N, int K, const float* A, const float* A2, i
                          int ldm, const int32_t* M_dev, const int32_t* K_dev, int precision, void* workspace,
                          size_t workspace_bytes, void* stream) {
   PCNN_REQUIRE(M >= 0 && N > 0 && K >= 0 && A && B && Cm);
-  PCNN_REQUIRE(precision == 0 || precision == 1);
+  PCNN_REQUIRE(precision >= 0 && precision <= 2);
   PCNN_REQUIRE(lda >= (a_trans ? M : K) && ldb >= (b_trans ? K : N) && ldc >= N);
   PCNN_REQUIRE(!mask || ldm >= N);
   PCNN_REQUIRE(act == 0 || act == 1);
@@ -922,7 +723,7 @@ extern "C" int pcnn_gemm(int M, int N, int K, const float* A, const float* A2, i
   GemmArgs g{M, N, K, A, A2, lda, B, ldb, Cm, ldc, bias, act, mask, ldm, M_dev, K_dev, (float*)workspace, precision,
              tile_x3(M, N, K), 0, 0};
   hipStream_t st = (hipStream_t)stream;
-  if (precision == 1) {
+  if (precision == 1 || precision == 2) {
     // ragged edges: a KC operand whose K (or device-side K) is not a multiple of
     // 4, or an NC operand whose row count is not -> element-wise edge loads
     const bool a_kc = !a_trans, b_kc = b_trans;
@@ -937,7 +738,7 @@ extern "C" int pcnn_gemm(int M, int N, int K, const float* A, const float* A2, i
       // the split), use the fewest workgroups that keep the same number of
       // rounds (fc6 dW: 1568 tiles -> 224 workgroups x 7): the makespan is
       // unchanged and the spare CUs run the other stream's kernels
-      const XPlan pl = x_plan(M, N, K, T, max_grid);
+      const XPlan pl = x_plan(M, N, K, T, max_grid, split_bk(precision));
       may_split = pl.mode == 1;
       if (pl.mode == 0) {
         gen = T != 256;  // the lean whole-tile kernel (instantiated for T = 256)
@@ -977,7 +778,8 @@ extern "C" int pcnn_gemm(int M, int N, int K, const float* A, const float* A2, i
     else if (a_trans && !b_trans) PCNN_X3_LAUNCH(true, false, RG, S2); \
     else PCNN_X3_LAUNCH(true, true, RG, S2);                       \
   } while (0)
-    if (!ragged && !A2) PCNN_X3_LAYOUT(false, false);
+    if (precision == 2) launch_gemm_x6(g, (int)grid, a_trans, b_trans, ragged, A2 != nullptr, gen, st);
+    else if (!ragged && !A2) PCNN_X3_LAYOUT(false, false);
     else if (!ragged) PCNN_X3_LAYOUT(false, true);
     else if (!A2) PCNN_X3_LAYOUT(true, false);
     else PCNN_X3_LAYOUT(true, true);

@@ -81,7 +81,7 @@ def hough_voting_gpu_capacity(label, vertex, extents, meta_data, gt, is_train, t
     if prob is not None and out.get("label") is None:
         out["label"] = torch.empty((B, H, W), dtype=torch.int32, device=dev)
     nbytes = lib.pcnn_hough_voting_workspace_size(B, H, W, C, int(skip_pixels), float(threshold_vote))
-    ws = _lib.workspace(nbytes, dev, "hough")
+    ws = _lib.workspace(nbytes, dev, "hough", stream)
     if prob is not None:
         head = (lib.pcnn_hough_voting_prob, _lib.ptr(prob), _lib.ptr(out["label"]))
     elif vertex_compact:

@@ -36,7 +36,7 @@ CAP = hv.CAPACITY
 class PoseStep:
     def __init__(self, B, H, W, num_classes, device, conv4_hw=None, conv5_hw=None, channels=512, units=4096,
                  is_train=1, skip_pixels=10, vote_threshold=-1.0, vote_percentage=0.02, margin=0.01,
-                 global_batch=None, batch_base=0, weights=None, dist=None, backward=True, precision=1,
+                 global_batch=None, batch_base=0, weights=None, dist=None, backward=True, precision=2,
                  overlap_weight_grads=True, pixel_argmax=True):
         self.B, self.H, self.W, self.C = B, H, W, num_classes
         self.dev = device
@@ -46,7 +46,9 @@ class PoseStep:
         self.batch_base = batch_base
         self.dist = dist  # torch.distributed module (initialised) or None
         self.backward = backward
-        self.prec = precision  # FC GEMMs: 1 = split-bf16 x3 MFMA (fp32-class), 0 = exact fp32 MFMA
+        # FC GEMMs: 2 = exact three-way split-bf16 x6 MFMA (fp32-faithful, the default), 1 = split-bf16 x3
+        # MFMA (fp32-class, ~2^-16 per product), 0 = fp32 MFMA
+        self.prec = precision
         self.h4, self.w4 = conv4_hw or (H // 8, W // 8)
         self.h5, self.w5 = conv5_hw or (H // 16, W // 16)
         self.Ch = channels
@@ -95,6 +97,9 @@ class PoseStep:
         self.dconv5 = torch.zeros((B, self.h5, self.w5, channels), **f32)
         self.norm_rows = torch.zeros((1,), **i32)
         self.timer = None  # optional {name: [(start_event, end_event), ...]} (bench.py)
+        # optional {gemm name: [(start_event, end_event), ...]}: HIP events around each FC GEMM on the
+        # stream it runs on, with the step's stream overlap left on (the in-step kernel times, bench.py)
+        self.gemm_timer = None
         self.xchg = None  # RoiExchange, built on the first gather_detections()
         self._pending = {}  # async collectives of the current step
         # weight-gradient branch of the backward (None: everything on the caller's stream)
@@ -180,14 +185,14 @@ class PoseStep:
         if gs is not None:  # fc6 input column blocks to their owners (overlaps the forward)
             gs.send_input("w6", x)
         with self._t("gemm_fc6_fwd"):
-            ph.gemm(x, w.w6, self.y6, bias=w.b6, act=1, M_dev=nr, precision=self.prec)
+            self._g("fc6_fwd", x, w.w6, self.y6, bias=w.b6, act=1, M_dev=nr)
         if gs is not None:
             gs.send_input("w7", self.y6)
         with self._t("gemm_fc7_fc8_fwd"):
-            ph.gemm(self.y6, w.w7, self.y7, bias=w.b7, act=1, M_dev=nr, precision=self.prec)
+            self._g("fc7_fwd", self.y6, w.w7, self.y7, bias=w.b7, act=1, M_dev=nr)
             if gs is not None:
                 gs.send_input("w8", self.y7)
-            ph.gemm(self.y7, w.w8, self.y8, bias=w.b8, act=0, M_dev=nr, precision=self.prec)
+            self._g("fc8_fwd", self.y7, w.w8, self.y8, bias=w.b8, act=0, M_dev=nr)
         if self.dist is not None:
             self._wait("rows")
             self.norm_rows.clamp_(min=1)
@@ -236,7 +241,7 @@ class PoseStep:
                     # the bias sum first: a short launch ahead of the long dW GEMM, not
                     # a tail after it (fc6: it ran 44 us behind the dW, beside the pool bwd)
                     ph.colsum(dY, g["b" + name[1:]], M_dev=nr)
-                    ph.gemm(X, dY, g[name], a_trans=1, K_dev=nr, M=M, N=N, K=K_loc, precision=self.prec)
+                    self._g(f"fc{name[1:]}_dw", X, dY, g[name], a_trans=1, K_dev=nr, M=M, N=N, K=K_loc)
 
         with self._t("add_loss_head_bwd"):
             # average_distance_loss_grad (top_diff[0] * bottom_diff) folded into
@@ -245,15 +250,15 @@ class PoseStep:
         with self._t("gemm_fc8_fc7_dw_bias"):  # fc8 weight / bias gradients
             weight_grads("w8", self.y7, self.dy8, CAP, w.units, self.D)
         with self._t("gemm_fc8_fc7_dx"):
-            ph.gemm(self.dy8, w.w8, self.dy7, b_trans=1, mask=self.y7, M_dev=nr, precision=self.prec)
+            self._g("fc8_dx", self.dy8, w.w8, self.dy7, b_trans=1, mask=self.y7, M_dev=nr)
         with self._t("gemm_fc8_fc7_dw_bias"):  # fc7 weight / bias gradients
             weight_grads("w7", self.y6, self.dy7, CAP, w.units, w.units)
         with self._t("gemm_fc8_fc7_dx"):
-            ph.gemm(self.dy7, w.w7, self.dy6, b_trans=1, mask=self.y6, M_dev=nr, precision=self.prec)
+            self._g("fc7_dx", self.dy7, w.w7, self.dy6, b_trans=1, mask=self.y6, M_dev=nr)
         with self._t("gemm_fc6_dw"):  # fc6 weight / bias gradients (A = pool5 + pool4)
             weight_grads("w6", x, self.dy6, CAP, K6, w.units)
         with self._t("gemm_fc6_dx"):
-            ph.gemm(self.dy6, w.w6, self.dx, b_trans=1, M_dev=nr, precision=self.prec)
+            self._g("fc6_dx", self.dy6, w.w6, self.dx, b_trans=1, M_dev=nr)
         dxp = self.dx.view(CAP, 7, 7, self.Ch)
         with self._t("roi_pool_bwd"):  # both pools receive d(pool5 + pool4) = dx
             rp.roi_pool_grad(conv5, h["box"], self.arg5, dxp, 7, 7, 1.0 / 16.0, 0, num_rois=nr, out=self.dconv5,
@@ -265,6 +270,18 @@ class PoseStep:
 
     def _gemm(self, A, B, C, **kw):
         return ph.gemm(A, B, C, precision=self.prec, **kw)
+
+    def _g(self, name, A, B, C, **kw):
+        """One FC GEMM at the step's precision, bracketed by HIP events on the
+        stream it is launched on when gemm_timer is set."""
+        if self.gemm_timer is None:
+            return ph.gemm(A, B, C, precision=self.prec, **kw)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        ph.gemm(A, B, C, precision=self.prec, **kw)
+        e1.record()
+        self.gemm_timer.setdefault(name, []).append((e0, e1))
+        return C
 
     def step(self, inputs):
         self.vote(inputs["label"], inputs["vertex"], inputs["extents"], inputs["meta"], inputs["gt"])

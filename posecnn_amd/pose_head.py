@@ -14,7 +14,7 @@ from . import _lib
 
 
 def gemm(A, B, C, a_trans=0, b_trans=0, A2=None, bias=None, act=0, mask=None, M_dev=None, K_dev=None, M=None,
-         N=None, K=None, precision=0, stream=None):
+         N=None, K=None, precision=2, stream=None):
     """C[M,N] = epilogue(op(A) (+ op(A2)) @ op(B)); see pcnn_gemm in include/posecnn_hip.h."""
     _lib.require_gpu(A, B, C)
     for t in (A, B, C, A2, bias, mask):
@@ -27,7 +27,8 @@ def gemm(A, B, C, a_trans=0, b_trans=0, A2=None, bias=None, act=0, mask=None, M_
     if N is None:
         N = B.shape[0] if b_trans else B.shape[1]
     lib = _lib.load()
-    ws = _lib.workspace(lib.pcnn_gemm_workspace_size(M, N, K, int(M_dev is not None), precision), C.device, "gemm")
+    ws = _lib.workspace(lib.pcnn_gemm_workspace_size(M, N, K, int(M_dev is not None), precision), C.device, "gemm",
+                        stream)
     rc = lib.pcnn_gemm(M, N, K, _lib.ptr(A), _lib.ptr(A2), A.stride(0), int(a_trans), _lib.ptr(B), B.stride(0),
                        int(b_trans), _lib.ptr(C), C.stride(0), _lib.ptr(bias), int(act), _lib.ptr(mask),
                        mask.stride(0) if mask is not None else 0, _lib.ptr(M_dev), _lib.ptr(K_dev), int(precision),

@@ -153,6 +153,18 @@ def make_frames(B, H=480, W=640, num_classes=22, objects_per_image=6, seed=0, im
     return out
 
 
+def cpu_vertex(vertex):
+    """The vertex map in the convention of the reference CPU op `Houghvoting`:
+    channel 3c+2 is the raw distance (TransHyp::compute_distance,
+    ransac.h:108-119; hypotheses with a negative one are skipped,
+    hough_voting_op.cc:583-599), where the GPU op reads log-depth and takes
+    exp (hough_voting_gpu_op.cu.cc:280).  The CPU baseline is timed on this
+    form of the same frames."""
+    v = vertex.copy()
+    v[..., 2::3] = np.exp(v[..., 2::3])
+    return v
+
+
 def rescaled_points(num_classes=22, symmetric=True):
     """Model points rescaled as minibatch.py:50-60 does, plus the symmetry vector."""
     mdl = models()

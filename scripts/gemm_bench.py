@@ -1,6 +1,6 @@
 """Time the pose step's nine FC GEMMs (R RoI rows, fp32 in HBM) one by one
 with HIP events; prints us and achieved TFLOP/s per shape.
-    python scripts/gemm_bench.py [--rows 405] [--precision 1] [--iters 20]"""
+    python scripts/gemm_bench.py [--rows 405] [--precision 2[,1,0]] [--iters 20]"""
 import argparse
 import sys
 
@@ -11,7 +11,7 @@ from posecnn_amd import pose_head as ph  # noqa: E402
 
 p = argparse.ArgumentParser()
 p.add_argument("--rows", type=int, default=405)
-p.add_argument("--precision", type=int, default=1)
+p.add_argument("--precision", default="2")
 p.add_argument("--iters", type=int, default=20)
 p.add_argument("--only", default="")
 a = p.parse_args()
@@ -24,34 +24,40 @@ y6, y7, y8 = r(CAP, U), r(CAP, U), torch.empty(CAP, O, device=D)
 dy8, dy7, dy6, dx = r(CAP, O), r(CAP, U), r(CAP, U), torch.empty(CAP, K6, device=D)
 gw6, gw7, gw8 = torch.empty(K6, U, device=D), torch.empty(U, U, device=D), torch.empty(U, O, device=D)
 nr = torch.tensor([a.rows], dtype=torch.int32, device=D)
-P = a.precision
 R = a.rows
-cases = [
-    ("fc6_fwd", 2 * R * K6 * U, lambda: ph.gemm(x5, w6, y6, act=1, M_dev=nr, precision=P)),
-    ("fc7_fwd", 2 * R * U * U, lambda: ph.gemm(y6, w7, y7, act=1, M_dev=nr, precision=P)),
-    ("fc8_fwd", 2 * R * U * O, lambda: ph.gemm(y7, w8, y8, M_dev=nr, precision=P)),
-    ("fc8_dw", 2 * R * U * O, lambda: ph.gemm(y7, dy8, gw8, a_trans=1, K_dev=nr, M=U, N=O, K=CAP, precision=P)),
-    ("fc8_dx", 2 * R * U * O, lambda: ph.gemm(dy8, w8, dy7, b_trans=1, mask=y7, M_dev=nr, precision=P)),
-    ("fc7_dw", 2 * R * U * U, lambda: ph.gemm(y6, dy7, gw7, a_trans=1, K_dev=nr, M=U, N=U, K=CAP, precision=P)),
-    ("fc7_dx", 2 * R * U * U, lambda: ph.gemm(dy7, w7, dy6, b_trans=1, mask=y6, M_dev=nr, precision=P)),
-    ("fc6_dw", 2 * R * K6 * U, lambda: ph.gemm(x5, dy6, gw6, a_trans=1, K_dev=nr, M=K6, N=U, K=CAP,
-                                               precision=P)),
-    ("fc6_dx", 2 * R * K6 * U, lambda: ph.gemm(dy6, w6, dx, b_trans=1, M_dev=nr, precision=P)),
-]
-tot = 0.0
-for name, flops, fn in cases:
-    if a.only and name not in a.only.split(","):
-        continue
-    for _ in range(3):
-        fn()
-    torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(a.iters):
-        fn()
-    e1.record()
-    torch.cuda.synchronize()
-    us = e0.elapsed_time(e1) / a.iters * 1e3
-    tot += us
-    print(f"{name:8s} {us:9.1f} us  {flops / us / 1e6:8.1f} TFLOP/s", flush=True)
-print(f"total    {tot:9.1f} us", flush=True)
+
+
+def cases_for(P):
+    return [
+        ("fc6_fwd", 2 * R * K6 * U, lambda: ph.gemm(x5, w6, y6, act=1, M_dev=nr, precision=P)),
+        ("fc7_fwd", 2 * R * U * U, lambda: ph.gemm(y6, w7, y7, act=1, M_dev=nr, precision=P)),
+        ("fc8_fwd", 2 * R * U * O, lambda: ph.gemm(y7, w8, y8, M_dev=nr, precision=P)),
+        ("fc8_dw", 2 * R * U * O, lambda: ph.gemm(y7, dy8, gw8, a_trans=1, K_dev=nr, M=U, N=O, K=CAP, precision=P)),
+        ("fc8_dx", 2 * R * U * O, lambda: ph.gemm(dy8, w8, dy7, b_trans=1, mask=y7, M_dev=nr, precision=P)),
+        ("fc7_dw", 2 * R * U * U, lambda: ph.gemm(y6, dy7, gw7, a_trans=1, K_dev=nr, M=U, N=U, K=CAP, precision=P)),
+        ("fc7_dx", 2 * R * U * U, lambda: ph.gemm(dy7, w7, dy6, b_trans=1, mask=y6, M_dev=nr, precision=P)),
+        ("fc6_dw", 2 * R * K6 * U, lambda: ph.gemm(x5, dy6, gw6, a_trans=1, K_dev=nr, M=K6, N=U, K=CAP,
+                                                   precision=P)),
+        ("fc6_dx", 2 * R * K6 * U, lambda: ph.gemm(dy6, w6, dx, b_trans=1, M_dev=nr, precision=P)),
+    ]
+
+
+for P in [int(v) for v in a.precision.split(",")]:
+    print(f"precision {P}", flush=True)
+    tot = 0.0
+    for name, flops, fn in cases_for(P):
+        if a.only and name not in a.only.split(","):
+            continue
+        for _ in range(3):
+            fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(a.iters):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        us = e0.elapsed_time(e1) / a.iters * 1e3
+        tot += us
+        print(f"{name:8s} {us:9.1f} us  {flops / us / 1e6:8.1f} TFLOP/s", flush=True)
+    print(f"total    {tot:9.1f} us", flush=True)

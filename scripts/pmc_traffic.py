@@ -13,14 +13,16 @@ import re
 import sys
 from collections import defaultdict
 
-# k_gemm_x3 dispatches of one pose step in enqueue order (pipeline.py), over
-# every tile / layout instantiation
+# split-GEMM dispatches (k_gemm_x6 at the step's default precision, k_gemm_x3
+# at precision 1) of one pose step in enqueue order (pipeline.py), over every
+# tile / layout instantiation
 STEP_ORDER = ["fc6_fwd", "fc7_fwd", "fc8_fwd", "fc8_dw", "fc8_dx", "fc7_dw", "fc7_dx", "fc6_dw", "fc6_dx"]
+GEMM_FAMILIES = ("k_gemm_x6", "k_gemm_x3")
 
 
-def gemm_roles(per):
+def gemm_roles(per, fam):
     """{role: [values]} from {kernel: [(dispatch_id, value)]}; roles by position in the step order."""
-    seq = sorted(x for k, v in per.items() if k.startswith("k_gemm_x3") for x in v)
+    seq = sorted(x for k, v in per.items() if k.startswith(fam) for x in v)
     out = defaultdict(list)
     for i, (_, val) in enumerate(seq):
         out[STEP_ORDER[i % len(STEP_ORDER)]].append(val)
@@ -48,10 +50,11 @@ def load(path, counter):
 def summarize(fetch_csv, write_csv):
     f, w = load(fetch_csv, "FETCH_SIZE"), load(write_csv, "WRITE_SIZE")
     out = {}
-    fr_all, wr_all = gemm_roles(f), gemm_roles(w)
-    for role, fr in fr_all.items():
-        wr = wr_all.get(role, [])
-        out[f"k_gemm_x3:{role}"] = {"read_bytes": 2 * sum(fr) / len(fr), "write_bytes": sum(wr) / max(len(wr), 1),
+    for fam in GEMM_FAMILIES:
+        fr_all, wr_all = gemm_roles(f, fam), gemm_roles(w, fam)
+        for role, fr in fr_all.items():
+            wr = wr_all.get(role, [])
+            out[f"{fam}:{role}"] = {"read_bytes": 2 * sum(fr) / len(fr), "write_bytes": sum(wr) / max(len(wr), 1),
                                     "dispatches": len(fr)}
     for k in f:
         fv = [v for _, v in f[k]]

@@ -78,7 +78,9 @@ def test_workspace_sizing(lib):
     # the weight-gradient shapes run whole tiles
     assert lib.pcnn_gemm_workspace_size(1152, 4096, 25088, 1, 0) >= 2 * 1152 * 4096 * 4
     assert lib.pcnn_gemm_workspace_size(1152, 4096, 25088, 1, 1) >= 8 * 1152 * 4096 * 4
+    assert lib.pcnn_gemm_workspace_size(1152, 4096, 25088, 1, 2) >= 8 * 1152 * 4096 * 4
     assert lib.pcnn_gemm_workspace_size(25088, 4096, 1152, 0, 1) == 256
+    assert lib.pcnn_gemm_workspace_size(25088, 4096, 1152, 0, 2) == 256
     assert lib.pcnn_gemm_workspace_size(0, 4096, 25088, 0, 0) == 256
 
 

@@ -91,3 +91,47 @@ def test_hough_no_detection_dummy_row(hip, orc):
     fr["label"][:] = 0
     (box, pose, tgt, wgt, dom), n, _ = _run(fr, 1)
     assert n == 0 and box.shape == (1, 7) and not box.any() and not pose.any()
+
+
+def test_hough_grad_zeros(hip):
+    """HoughvotinggpuGrad (hough_voting_gpu_op.cc:440-484, set_gradients
+    cu.cc:608-612): float zeros shaped like label (B,H,W) and vertex
+    (B,H,W,3C), written over recycled non-zero memory."""
+    d = torch.device("cuda")
+    fr = synth.make_frames(2, 120, 160, num_classes=22, objects_per_image=4, seed=7)
+    label = torch.from_numpy(fr["label"]).to(d)
+    vertex = torch.from_numpy(fr["vertex"]).to(d)
+    junk = torch.full((vertex.numel() + label.numel() + 4096,), 3.5, device=d)  # the allocator re-hands this out
+    del junk
+    gl, gv = hv.hough_voting_gpu_grad(label, vertex, torch.ones(1, device=d))
+    torch.cuda.synchronize()
+    assert gl.shape == label.shape and gl.dtype == torch.float32
+    assert gv.shape == vertex.shape and gv.dtype == torch.float32
+    assert not gl.any() and not gv.any()
+
+
+def test_hough_two_streams_concurrent(hip, orc):
+    """Reentrancy: two calls on two explicit streams, issued
+    back to back from a third current stream, each with its own frames, get
+    separate scratch (the workspace is keyed on the launch stream) and both
+    match the oracle bit for bit."""
+    d = torch.device("cuda")
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(d)
+    frs = [synth.make_frames(2, 240, 320, num_classes=22, objects_per_image=5, seed=s) for s in (61, 62)]
+    ins = [tuple(t(f[k]) for k in ("label", "vertex", "extents", "meta", "gt")) for f in frs]
+    torch.cuda.synchronize()
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    keep = []  # every call's outputs stay alive until the sync (the allocator must not recycle them across streams)
+    for _ in range(3):  # repeated, so the second stream's launch overlaps the first's
+        outs = [hv.hough_voting_gpu_capacity(*ins[i], 1, -1.0, 0.02, 5, stream=streams[i]) for i in range(2)]
+        keep.append(outs)
+    torch.cuda.synchronize()
+    assert outs[0]["_ws"].data_ptr() != outs[1]["_ws"].data_ptr()
+    for fr, o in zip(frs, outs):
+        n = int(o["num_rois"][1].item())
+        ob, op, ot, ow, od, on = orc.hough_voting(fr["label"], fr["vertex"], fr["extents"], fr["meta"], fr["gt"], 1,
+                                                  -1.0, 0.02, 5)
+        assert n == on > 0
+        np.testing.assert_array_equal(o["box"][:n].cpu().numpy(), ob)
+        np.testing.assert_array_equal(o["pose"][:n].cpu().numpy(), op)
+        np.testing.assert_array_equal(o["target"][:n].cpu().numpy(), ot)

@@ -328,15 +328,17 @@ def test_backproject_linemod_config(hip, orc):
 
 
 # Tolerances: precision 0 is fp32 MFMA (fp32 products, fp32 accumulation);
+# precision 2 is the exact three-way split-bf16 x6 MFMA (products to within
+# 2^-24 |a||b|, fp32 accumulation) and is held to the same fp32 bound;
 # precision 1 is the split-bf16 x3 MFMA (hi*hi + hi*lo + lo*hi, fp32
 # accumulation): per-product relative error <= ~2^-16, so the error of a
-# K-term dot product of O(1) values is ~2^-16 * sqrt(K).  Both are held to
-# the north-star 1e-4 relative bound, with atol scaled by sqrt(K).
+# K-term dot product of O(1) values is ~2^-16 * sqrt(K) -- held to the
+# north-star 1e-4 relative bound, with atol scaled by sqrt(K).
 def _gemm_tol(prec, K):
-    return dict(rtol=2e-5, atol=2e-4) if prec == 0 else dict(rtol=1e-4, atol=1e-4 * np.sqrt(K))
+    return dict(rtol=2e-5, atol=2e-4) if prec != 1 else dict(rtol=1e-4, atol=1e-4 * np.sqrt(K))
 
 
-@pytest.mark.parametrize("prec", [0, 1])
+@pytest.mark.parametrize("prec", [0, 1, 2])
 @pytest.mark.parametrize("at,bt", [(0, 0), (0, 1), (1, 0), (1, 1)])
 def test_gemm_layouts(hip, at, bt, prec):
     rng = np.random.default_rng(5)
@@ -354,7 +356,7 @@ def test_gemm_layouts(hip, at, bt, prec):
     np.testing.assert_allclose(C.cpu().numpy(), ref, **_gemm_tol(prec, 2 * K))
 
 
-@pytest.mark.parametrize("prec", [0, 1])
+@pytest.mark.parametrize("prec", [0, 1, 2])
 def test_gemm_device_dims_split(hip, prec):
     rng = np.random.default_rng(6)
     M, N, K = 1152, 256, 8192
@@ -365,18 +367,19 @@ def test_gemm_device_dims_split(hip, prec):
     C = torch.zeros((M, N), dtype=torch.float32, device=D)
     ph.gemm(T(A), T(B), C, mask=T(mask), M_dev=Mdev, precision=prec)
     ref = (A[:333].astype(np.float64) @ B) * (mask[:333] > 0)
-    np.testing.assert_allclose(C[:333].cpu().numpy(), ref, **(dict(rtol=2e-5, atol=5e-4) if prec == 0 else _gemm_tol(1, K)))
+    np.testing.assert_allclose(C[:333].cpu().numpy(), ref, **(dict(rtol=2e-5, atol=5e-4) if prec != 1 else _gemm_tol(1, K)))
     assert not C[333:].cpu().numpy().any()
     # K on device (weight-gradient form: C = A^T B over the first 77 rows)
     Kdev = torch.tensor([77], dtype=torch.int32, device=D)
     C2 = torch.empty((K, N), dtype=torch.float32, device=D)
     ph.gemm(T(A), T(B[:M].copy()), C2, a_trans=1, K_dev=Kdev, M=K, N=N, K=M, precision=prec)
     ref2 = A[:77].T.astype(np.float64) @ B[:77]
-    np.testing.assert_allclose(C2.cpu().numpy(), ref2, **(dict(rtol=2e-5, atol=5e-4) if prec == 0 else _gemm_tol(1, 77)))
+    np.testing.assert_allclose(C2.cpu().numpy(), ref2, **(dict(rtol=2e-5, atol=5e-4) if prec != 1 else _gemm_tol(1, 77)))
 
 
-def test_gemm_weight_grad_unsplit(hip):
-    """Unsplit x3 persistent grid in the fc6 / fc7 dW form: C = A^T B over a
+@pytest.mark.parametrize("prec", [1, 2])
+def test_gemm_weight_grad_unsplit(hip, prec):
+    """Unsplit persistent grid in the fc6 / fc7 dW form: C = A^T B over a
     device-side row count, 16 x 8 tiles of 256, K = 405 rows of 1152."""
     rng = np.random.default_rng(9)
     R, M, N = 1152, 4096, 2048
@@ -384,13 +387,14 @@ def test_gemm_weight_grad_unsplit(hip):
     B = rng.normal(size=(R, N)).astype(np.float32)
     Kdev = torch.tensor([405], dtype=torch.int32, device=D)
     C = torch.empty((M, N), dtype=torch.float32, device=D)
-    ph.gemm(T(A), T(B), C, a_trans=1, K_dev=Kdev, M=M, N=N, K=R, precision=1)
+    ph.gemm(T(A), T(B), C, a_trans=1, K_dev=Kdev, M=M, N=N, K=R, precision=prec)
     ref = A[:405].T.astype(np.float64) @ B[:405]
-    np.testing.assert_allclose(C.cpu().numpy(), ref, **_gemm_tol(1, 405))
+    np.testing.assert_allclose(C.cpu().numpy(), ref, **_gemm_tol(prec, 405))
 
 
+@pytest.mark.parametrize("prec", [1, 2])
 @pytest.mark.parametrize("bt", [0, 1])
-def test_gemm_live_row_blocks(hip, bt):
+def test_gemm_live_row_blocks(hip, bt, prec):
     """Device-side row counts that leave every number (0-4) of live 32-row
     accumulator blocks in a wave's half of a 256-row tile (the K loop is
     specialised on that count): fc7-like capacity shape, bias + relu + mask."""
@@ -404,13 +408,13 @@ def test_gemm_live_row_blocks(hip, bt):
     for live in (1, 31, 33, 70, 100, 128, 129, 200, 257, 290, 333, 405, 449, 511, 512, 700, 1152):
         Mdev = torch.tensor([live], dtype=torch.int32, device=D)
         C = torch.zeros((M, N), dtype=torch.float32, device=D)
-        ph.gemm(tA, tB, C, b_trans=bt, bias=T(bias), act=1, mask=T(mask), M_dev=Mdev, precision=1)
+        ph.gemm(tA, tB, C, b_trans=bt, bias=T(bias), act=1, mask=T(mask), M_dev=Mdev, precision=prec)
         ref = np.maximum(A[:live].astype(np.float64) @ B + bias, 0) * (mask[:live] > 0)
-        np.testing.assert_allclose(C[:live].cpu().numpy(), ref, err_msg=f"live={live}", **_gemm_tol(1, K))
+        np.testing.assert_allclose(C[:live].cpu().numpy(), ref, err_msg=f"live={live}", **_gemm_tol(prec, K))
         assert not C[live:].cpu().numpy().any(), live
 
 
-@pytest.mark.parametrize("prec", [0, 1])
+@pytest.mark.parametrize("prec", [0, 1, 2])
 @pytest.mark.parametrize("at,bt", [(0, 0), (0, 1), (1, 0), (1, 1)])
 def test_gemm_ragged_padded(hip, at, bt, prec):
     """Ragged M/N/K (no multiple of 4 or of the tile) through padded leading dims."""
@@ -430,9 +434,10 @@ def test_gemm_ragged_padded(hip, at, bt, prec):
     np.testing.assert_allclose(C.cpu().numpy(), ref, **_gemm_tol(prec, K))
 
 
+@pytest.mark.parametrize("prec", [1, 2])
 @pytest.mark.parametrize("shape", [(332, 88, 1000), (204, 300, 100), (88, 500, 404), (1152, 4096, 88)])
 @pytest.mark.parametrize("at,bt", [(0, 0), (0, 1), (1, 0), (1, 1)])
-def test_gemm_small_tile(hip, shape, at, bt):
+def test_gemm_small_tile(hip, shape, at, bt, prec):
     """Shapes with an edge <= 128 (the fc8 GEMMs) run the 128 x 128 x3 tile:
     A + A2, bias, relu, mask and a device-side M (333 live rows)."""
     rng = np.random.default_rng(10)
@@ -446,9 +451,9 @@ def test_gemm_small_tile(hip, shape, at, bt):
     Mdev = torch.tensor([live], dtype=torch.int32, device=D)
     C = torch.zeros((M, N), dtype=torch.float32, device=D)
     ph.gemm(T(A.T.copy() if at else A), T(B.T.copy() if bt else B), C, a_trans=at, b_trans=bt,
-            A2=T(A2.T.copy() if at else A2), bias=T(bias), act=1, mask=T(mask), M_dev=Mdev, precision=1)
+            A2=T(A2.T.copy() if at else A2), bias=T(bias), act=1, mask=T(mask), M_dev=Mdev, precision=prec)
     ref = np.maximum((A[:live].astype(np.float64) + A2[:live]) @ B + bias, 0) * (mask[:live] > 0)
-    np.testing.assert_allclose(C[:live].cpu().numpy(), ref, **_gemm_tol(1, 2 * K))
+    np.testing.assert_allclose(C[:live].cpu().numpy(), ref, **_gemm_tol(prec, 2 * K))
     assert not C[live:].cpu().numpy().any()
 
 
