@@ -200,6 +200,12 @@ int pcnn_add_loss_fwd_prepared(const float* pred, const float* target, const flo
 int pcnn_add_loss_bwd(const float* top_diff, const float* bottom_diff, int n, const int32_t* num_rois_dev,
                       int row_len, float* out, void* stream);
 
+/* Self-check of the ADD loss's per-launch division (average_distance.hip
+ * div_rn): out[i] = x[i] / b correctly rounded, through the kernels' reciprocal
+ * + two fma-correction form, in fp32 (dbl = 0) or in double rounded to fp32
+ * (dbl = 1, the loss-sum form of cu.cc:181).  Test infrastructure only. */
+int pcnn_div_rn_check(const float* x, float b, int n, int dbl, float* out, void* stream);
+
 /* ---------------------------------------------------------------------------
  * Depth backprojection (Backproject / BackprojectGrad).
  * Replaces BackprojectForwardLaucher / BackprojectBackwardLaucher

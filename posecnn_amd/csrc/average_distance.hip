@@ -57,19 +57,37 @@ __device__ __forceinline__ void quat2rot(float s, float u, float v, float w, flo
   r[8] = s * s - u * u - v * v + w * w;
 }
 
-// x / b correctly rounded, for a b fixed per launch (the loss normaliser):
-// y = RN(x * r) with r = RN(1 / b) is a faithful quotient, its remainder
-// x - b y is exact in one fma, and RN(y + r (x - b y)) is the correctly
-// rounded x / b (Markstein's theorem; no underflow at these magnitudes) -- the
-// reference's IEEE division (cu.cc:181,196-202) in three instructions instead
-// of the ten of the generic division sequence.  Same for the double form.
+// x / b correctly rounded, for a b fixed per launch (the loss normaliser),
+// from r = RN(1 / b): y0 = RN(x r) is within ~2 ulp of x / b; one fma
+// correction y1 = RN(y0 + r (x - b y0)) leaves a relative error of ~2u^2 on
+// top of its own rounding, so y1 is a faithful quotient; then its remainder
+// x - b y1 is exact in one fma and RN(y1 + r (x - b y1)) is the correctly
+// rounded x / b (Markstein's theorem: faithful y, r = RN(1/b), no underflow
+// at these magnitudes) -- the reference's IEEE division (cu.cc:181,196-202)
+// in five instructions instead of the ten of the generic division sequence.
+// (One correction from y0 alone is not enough: y0 need not be faithful when
+// x / b has its mantissa near 2.)  pcnn_div_rn_check exposes it to the tests.
+// Same for the double form.
 __device__ __forceinline__ float div_rn(float x, float b, float r) {
-  const float y = x * r;
-  return fmaf(fmaf(-y, b, x), r, y);
+  const float y0 = x * r;
+  const float y1 = fmaf(fmaf(-y0, b, x), r, y0);
+  return fmaf(fmaf(-y1, b, x), r, y1);
 }
 __device__ __forceinline__ double div_rn(double x, double b, double r) {
-  const double y = x * r;
-  return fma(fma(-y, b, x), r, y);
+  const double y0 = x * r;
+  const double y1 = fma(fma(-y0, b, x), r, y0);
+  return fma(fma(-y1, b, x), r, y1);
+}
+
+__global__ void k_div_rn_check(const float* __restrict__ x, float b, int n, int dbl, float* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  if (dbl) {
+    const double bd = (double)b, rd = 1.0 / bd;
+    out[i] = (float)div_rn((double)x[i], bd, rd);
+  } else {
+    out[i] = div_rn(x[i], b, 1.f / b);
+  }
 }
 
 __device__ __forceinline__ int row_class(const float* __restrict__ weight, int n, int C) {
@@ -507,6 +525,14 @@ __global__ void k_add_bwd_rows(const float* __restrict__ top_diff, const float* 
 }
 
 }  // namespace
+
+extern "C" int pcnn_div_rn_check(const float* x, float b, int n, int dbl, float* out, void* stream) {
+  PCNN_REQUIRE(x && out && n >= 0 && b != 0.f);
+  if (n == 0) return PCNN_OK;
+  hipLaunchKernelGGL(k_div_rn_check, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, x, b, n, dbl, out);
+  PCNN_CHECK_LAUNCH();
+  return PCNN_OK;
+}
 
 extern "C" size_t pcnn_add_loss_workspace_size(int R_cap, int C, int P) {
   (void)C;

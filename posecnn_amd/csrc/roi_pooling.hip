@@ -668,7 +668,9 @@ static int roi_pool_bwd(const float* top_diff, const void* argmax, bool px, int 
   const int tbh = narrow ? 1 : 2, tbw = 4;
   const bool vec = layout == 0 && !pool_channel && C % 2 == 0 && pooled_h * tbh <= 32 && pooled_w * tbw <= 32 &&
                    (long)H * W * C < (1l << 30) && (long)R_cap * pooled_h * pooled_w * C < (1l << 29) &&
-                   (((uintptr_t)top_diff | (uintptr_t)argmax | (uintptr_t)bottom_diff) & (px ? 3 : 7)) == 0;
+                   // top_diff is read as b64 and bottom_diff written as float2 in both forms;
+                   // only the argmax (uint16 pixel indices in the px form) may be 4-byte aligned
+                   (((uintptr_t)top_diff | (uintptr_t)bottom_diff) & 7) == 0 && ((uintptr_t)argmax & (px ? 3 : 7)) == 0;
   PCNN_REQUIRE(!px || (vec && (long)H * W < 0xFFFF));  // pixel-index argmax: the entry-list kernel only
   if (vec) {
     const int tiles = ((H + tbh - 1) / tbh) * ((W + tbw - 1) / tbw);

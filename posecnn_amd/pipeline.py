@@ -102,6 +102,7 @@ class PoseStep:
         self.gemm_timer = None
         self.xchg = None  # RoiExchange, built on the first gather_detections()
         self._pending = {}  # async collectives of the current step
+        self._in_step = False  # forward() inside step(): the loss all-reduce is joined at the step's end
         # weight-gradient branch of the backward (None: everything on the caller's stream)
         self.side_stream = torch.cuda.Stream(device=device) if overlap_weight_grads else None
 
@@ -203,11 +204,16 @@ class PoseStep:
             if self.timer is None and self.side_stream is not None:
                 torch.cuda.current_stream().wait_stream(self.side_stream)  # the row classes (add_prep)
             self._prepped = False
+            # the previous step's in-place loss all-reduce must be done before
+            # the loss kernel rewrites self.loss (its handle orders it on this stream)
+            self._wait("loss")
             adl.average_distance_loss(self.pred, h["target"], h["weight"], points, symmetry, self.margin,
                                       num_rois=nr, loss_norm_rows_dev=self.norm_rows, out=(self.loss, self.diff),
                                       workspace=self.add_ws, prepared=True)
         if self.dist is not None:  # nothing downstream reads the global loss: joined at the end of the step
             self._pending["loss"] = self.dist.all_reduce(self.loss, async_op=True)
+            if not self._in_step:  # called on its own: the returned loss is the reduced one
+                self._wait("loss")
         return self.loss
 
     def backward_pass(self, conv4, conv5):
@@ -287,8 +293,12 @@ class PoseStep:
         self.vote(inputs["label"], inputs["vertex"], inputs["extents"], inputs["meta"], inputs["gt"])
         self.add_prep(inputs["points"], inputs["symmetry"])
         self.exchange()
-        loss = self.forward(inputs["conv4"], inputs["conv5"], inputs["points"], inputs["symmetry"])
-        if self.backward:
-            self.backward_pass(inputs["conv4"], inputs["conv5"])
+        self._in_step = True
+        try:
+            loss = self.forward(inputs["conv4"], inputs["conv5"], inputs["points"], inputs["symmetry"])
+            if self.backward:
+                self.backward_pass(inputs["conv4"], inputs["conv5"])
+        finally:
+            self._in_step = False
         self._wait("loss")
         return loss

@@ -474,3 +474,30 @@ def test_roi_pool_accumulate(hip, orc):
     np.testing.assert_array_equal(top.cpu().numpy(), o5 + o4)
     np.testing.assert_array_equal(a5.cpu().numpy(), oa5)
     np.testing.assert_array_equal(a4.cpu().numpy(), oa4)
+
+
+@pytest.mark.parametrize("dbl", [0, 1])
+def test_add_loss_division_correctly_rounded(hip, dbl):
+    """The ADD loss divides every per-point term by the launch's normaliser
+    b = (2) R P (cu.cc:181,196-202) through r = RN(1/b) and two fma
+    corrections (average_distance.hip div_rn).  Against IEEE division over
+    random x in many binades and quotients with their mantissa near 1 and
+    near 2 (where one correction alone is not enough), for the normalisers
+    of R = 1..1152 rows of P = 2620 points: bit-exact."""
+    import ctypes
+    rng = np.random.default_rng(21 + dbl)
+    lib = hip
+    for R in (1, 3, 9, 405, 1152, 777):
+        b = np.float32((2 if dbl else 1) * R * 2620)
+        x = (rng.uniform(-1, 1, 200000) * np.exp2(rng.integers(-30, 10, 200000))).astype(np.float32)
+        # quotients with mantissa just above 1 and just below 2 (x = b * q)
+        q = np.concatenate([1 + rng.uniform(0, 1e-3, 20000), 2 - rng.uniform(0, 1e-3, 20000)])
+        q = q * np.exp2(rng.integers(-20, 5, q.size))
+        x = np.concatenate([x, (b * q).astype(np.float32), np.nextafter((b * q).astype(np.float32), np.float32(3))])
+        xd = torch.from_numpy(x).to(D)
+        out = torch.empty_like(xd)
+        rc = lib.pcnn_div_rn_check(ctypes.c_void_p(xd.data_ptr()), ctypes.c_float(b), x.size, dbl,
+                                   ctypes.c_void_p(out.data_ptr()), None)
+        assert rc == 0
+        ref = (x.astype(np.float64) / np.float64(b)).astype(np.float32) if dbl else x / b
+        np.testing.assert_array_equal(out.cpu().numpy(), ref, err_msg=f"R={R}")
