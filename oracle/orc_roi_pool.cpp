@@ -72,6 +72,8 @@ ORC_API int orc_roi_pool_bwd(const float* top_diff, const int* argmax, int B, in
   const int Cout = pool_channel ? 1 : C;
   std::vector<RoiGeom> geo(R);
   for (int n = 0; n < R; n++) geo[n] = roi_geom(rois + (size_t)n * roi_stride, scale, PH, PW);
+  // every bottom element is independent (its own ordered sum): rows in parallel
+#pragma omp parallel for collapse(2) schedule(static)
   for (int n = 0; n < B; n++)
     for (int h = 0; h < H; h++)
       for (int w = 0; w < W; w++)
