@@ -7,15 +7,16 @@ import sys
 from collections import defaultdict
 
 sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.abspath(__file__)))
-from pmc_traffic import STEP_ORDER, gemm_roles  # noqa: E402
+from pmc_traffic import GEMM_FAMILIES, STEP_ORDER, gemm_roles  # noqa: E402
 
 per = defaultdict(list)
 for row in csv.DictReader(open(sys.argv[1])):
     m = re.search(r"(k_\w+(?:<[^>]*>)?)", row["Kernel_Name"])
     if m:
         per[m.group(1)].append((int(row["Dispatch_Id"]), (int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) / 1e3))
-roles = gemm_roles(per)
-for role in STEP_ORDER:
-    x = roles.get(role, [])
-    if x:
-        print(f"k_gemm_x3:{role:8s} n={len(x):4d} avg={sum(x) / len(x):8.1f} us")
+for fam in GEMM_FAMILIES:
+    roles = gemm_roles(per, fam)
+    for role in STEP_ORDER:
+        x = roles.get(role, [])
+        if x:
+            print(f"{fam}:{role:8s} n={len(x):4d} avg={sum(x) / len(x):8.1f} us")

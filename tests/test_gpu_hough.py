@@ -135,4 +135,3 @@ def test_hough_two_streams_concurrent(hip, orc):
         np.testing.assert_array_equal(o["box"][:n].cpu().numpy(), ob)
         np.testing.assert_array_equal(o["pose"][:n].cpu().numpy(), op)
         np.testing.assert_array_equal(o["target"][:n].cpu().numpy(), ot)
-
