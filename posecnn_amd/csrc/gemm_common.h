@@ -138,9 +138,9 @@ __device__ __forceinline__ xf4 x_ld4(const XOp& o, unsigned voff, int soff) {
   return __builtin_bit_cast(xf4, __builtin_amdgcn_raw_buffer_load_b128(o.rs, voff, soff, 0));
 }
 
-// Epilogue of one tile (or split-K slice) of a split kernel: AM x 2
+// Epilogue of one tile (or split-K slice) of a split kernel: AM x AN
 // accumulator blocks of 32 x 32 per wave, the wave at rows wm * (T / 2),
-// columns wn * 64 of the tile.  One uniform branch (slab or C), otherwise
+// columns wn * 32 AN of the tile.  One uniform branch (slab or C), otherwise
 // branch-free: bias / mask come in through buffer loads and results leave
 // through buffer stores, out-of-range lanes masked by an out-of-extent offset
 // (loads return 0, stores are dropped).  The 16 mask values of group (j, i)
@@ -150,11 +150,11 @@ __device__ __forceinline__ xf4 x_ld4(const XOp& o, unsigned voff, int soff) {
 // against the lane's one base): left to itself the compiler precomputes a
 // lane's 64 row indices once per kernel, spills them, and reloads one per
 // store behind a full vmcnt drain.
-template <int T, int AM>
-__device__ __forceinline__ void x_epilogue(const GemmArgs& g, const XPlan& pl, const f32x16 (&acc)[AM][2], int m0,
+template <int T, int AM, int AN = 2>
+__device__ __forceinline__ void x_epilogue(const GemmArgs& g, const XPlan& pl, const f32x16 (&acc)[AM][AN], int m0,
                                            int n0, int rl, int z, int wm, int wn, int r, int hsel) {
-  constexpr int EJ = 2, EI = AM, EQ = 16, EB = 32;
-  const int rlane = wm * (T / 2) + 4 * hsel, clane = wn * 64 + r;
+  constexpr int EJ = AN, EI = AM, EQ = 16, EB = 32;
+  const int rlane = wm * (T / 2) + 4 * hsel, clane = wn * (32 * AN) + r;
   auto qrow = [](int i, int q) { return i * EB + (q & 3) + 8 * (q >> 2); };
   const int rlim = rl - m0, clim = g.N - n0;  // rows / columns of the tile that exist
   if (pl.mode == 1) {  // split-K slice: raw partial sums to slab z
