@@ -1,0 +1,64 @@
+"""Backprojection microbench at the configs[4] bench size (B = 8, 640x480,
+G = 64, Ch = 64, NC = 16, kernel size 1, threshold 0.02): forward and
+backward op time by HIP events, the algorithmic bytes of each (forward:
+top_data + top_flag + top_label written, label_3d read where a voxel has no
+hit; backward: bottom_diff written + the top_diff rows of in-grid pixels
+read), the forward's hit fraction and the backward's in-grid fraction.  POSECNN_HIP_LIB selects a variant library."""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from posecnn_amd import synth
+from posecnn_amd.backprojecting_layer import backprojecting_op as bpo
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--iters", type=int, default=50)
+ap.add_argument("--batch", type=int, default=8)
+a = ap.parse_args()
+B, H, W, C, G, CH = a.batch, 480, 640, 16, 64, 64
+dev = torch.device("cuda")
+voxel = ([2.0 / G, 1.5 / G, 1.7 / G], [-1.0, -0.75, 0.4])  # as bench.py --workload linemod
+fr = synth.make_frames(B, H, W, num_classes=C, objects_per_image=4, seed=5, extents=synth.models()["linemod_extents"],
+                       with_depth=True, voxel=voxel)
+g = torch.Generator(device=dev)
+g.manual_seed(7)
+to = lambda x: torch.from_numpy(np.ascontiguousarray(x)).to(dev)
+data = torch.randn((B, H, W, CH), generator=g, device=dev)
+label = torch.rand((B, H, W, C), generator=g, device=dev)
+depth, meta = to(fr["depth"]), to(fr["meta"])
+label3d = torch.rand((B, G, G, G, C), generator=g, device=dev)
+grad = torch.randn((B, G, G, G, CH), generator=g, device=dev)
+
+
+def timeit(fn):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(a.iters):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) * 1e3 / a.iters
+
+
+out = bpo.backproject(data, label, depth, meta, label3d, G, 1, 0.02)
+top_flag = out[2] if isinstance(out, (tuple, list)) else None
+hit = float((top_flag[..., 0] > 0).float().mean()) if top_flag is not None else float("nan")
+fwd = timeit(lambda: bpo.backproject(data, label, depth, meta, label3d, G, 1, 0.02))
+gd = bpo.backproject_grad(data, depth, meta, grad, G, 1, 0.02)
+ingrid = float((gd[..., 0] != 0).float().mean())  # pixels whose top_diff row is read
+bwd = timeit(lambda: bpo.backproject_grad(data, depth, meta, grad, G, 1, 0.02))
+nvox = B * G ** 3
+fwd_bytes = nvox * (2 * CH + C) * 4 + (1 - hit) * nvox * C * 4
+bwd_bytes = B * H * W * CH * 4 * (1 + ingrid)
+print(json.dumps({"fwd_us": round(fwd, 1), "fwd_TBps_written+label3d": round(fwd_bytes / fwd / 1e6, 3),
+                  "bwd_us": round(bwd, 1), "bwd_TBps_rw": round(bwd_bytes / bwd / 1e6, 3), "hit_fraction": round(hit, 4),
+                  "bwd_ingrid_fraction": round(ingrid, 4),
+                  "B": B, "G": G, "Ch": CH, "NC": C}))
