@@ -307,6 +307,66 @@ int pcnn_hard_label_bwd(float* grad_prob, float* grad_gt, int B, int H, int W, i
 int pcnn_vertex_pred_compact(const float* feat, const float* weights, const float* bias, const int32_t* label, int B,
                              int H, int W, int K, int C, float* vertex3, void* stream);
 
+/* ---------------------------------------------------------------------------
+ * Test-time pose refinement: the numerical core of
+ * Synthesizer::solveICP (lib/synthesize/synthesize.cpp:2052-2395, reached from
+ * lib/fcn/test.py:1316-1351 via synthesizer.icp_python, synthesizer.pyx:60-75).
+ * Maps are row-major (H,W,ch) f32; the rendered maps (the reference's OpenGL
+ * pass, synthesize.cpp:2106-2137) are inputs: pred_vertices / pred_normals
+ * (H,W,4) per problem (renderer_vn_ textures), vertmap (H,W,3) canonical model
+ * coordinates with the class id in the integer part of x (renderer_ texture).
+ * Poses are (qw,qx,qy,qz,tx,ty,tz); input quaternions are normalised as
+ * Sophus' SE3(quaternion, translation) constructor does.
+ *
+ * pcnn_icp_live_vertices: live (L,H,W,3) = df::backproject of the masked depth
+ *   (synthesize.cpp:2140-2160; backprojection.cu:10-27, Poly3 camera at zero
+ *   distortion): d = depth / factor where label == obj_ids[l], else 0;
+ *   vertex = ((x-px)/fx*d, (y-py)/fy*d, d). depth (H,W) uint16, H*W % 4 == 0.
+ * pcnn_icp: df::icp (lib/kinect_fusion/src/optimization/icp.cpp:20-106 +
+ *   icp.cu:22-245) for N problems: `iterations` Gauss-Newton steps of the
+ *   projective point-to-plane residual (border 2 px, ray/normal test 0.1,
+ *   |error| <= max_error, weight 1/live depth), each solving JTJ x = JTr
+ *   (Eigen LDLT) and left-multiplying SE3::exp(x) into the accumulated update.
+ *   live (L,H,W,3) with live_index (N) selecting problem n's map (NULL: n);
+ *   update (N,7); pose_in / pose_out (N,7) optional: pose_out = update * pose_in
+ *   (refinePose, synthesize.cpp:2023-2025); systems (N,iterations,28) optional:
+ *   per iteration the 21 upper-triangle JTJ entries, 6 JTr and the pixel count.
+ * pcnn_icp_center: the translation re-centring of solveICP
+ *   (synthesize.cpp:2163-2219) for L objects: out (L,4) = mean(live - model) over
+ *   the object's pixels with depth > 0, finite vertmap and |n.(live - pred)| <
+ *   max_error, and the count; pose_out = pose_in with t = (rx Tz, ry Tz, Tz),
+ *   rx = tx / tz of pose_in, when the count is > 0.
+ * pcnn_pose_energy: optEnergy (synthesize.cpp:2474-2526) of K poses: mean
+ *   |T p - v| over the object's pixels with finite T p and both depths inside
+ *   (znear, zfar); energy (K).
+ * ------------------------------------------------------------------------- */
+int pcnn_icp_live_vertices(const uint16_t* depth, const int32_t* label, int H, int W, const int32_t* obj_ids, int L,
+                           float factor, float fx, float fy, float px, float py, float* live, void* stream);
+size_t pcnn_icp_workspace_size(int N, int H, int W);
+int pcnn_icp(const float* live, const int32_t* live_index, const float* pred_vertices, const float* pred_normals,
+             int N, int H, int W, float fx, float fy, float px, float py, float znear, float zfar, float max_error,
+             int iterations, const float* pose_in, float* update, float* pose_out, float* systems, void* workspace,
+             size_t workspace_bytes, void* stream);
+size_t pcnn_icp_reduce_workspace_size(int L, int H, int W);
+int pcnn_icp_center(const float* live, const int32_t* label, const int32_t* obj_ids, int L, const float* vertmap,
+                    const float* pred_vertices, const float* pred_normals, int H, int W, float max_error,
+                    const float* pose_in, float* out, float* pose_out, void* workspace, size_t workspace_bytes,
+                    void* stream);
+/* pcnn_icp_score: the SegICP hypothesis score of solveICP (synthesize.cpp:2288-2330):
+ *   over the object's pixels with depth > 0 and a finite vertmap, each model
+ *   point (vertmap, class offset dropped) moved by hypothesis j takes its
+ *   nearest live point within `radius` (squared distance < radius^2; ties ->
+ *   lowest raster index); score (J) = distinct live points taken / model points;
+ *   choose (1) = first best hypothesis (0 when the object has no such pixel).
+ *   J <= 64. */
+size_t pcnn_icp_score_workspace_size(int J, int H, int W);
+int pcnn_icp_score(const float* live, const int32_t* label, int obj, const float* vertmap, int H, int W,
+                   const float* hyps, int J, float radius, float* score, int32_t* choose, void* workspace,
+                   size_t workspace_bytes, void* stream);
+int pcnn_pose_energy(const float* live, const int32_t* label, int obj, const float* pred_vertices, int H, int W,
+                     float znear, float zfar, const float* poses, int K, float* energy, void* workspace,
+                     size_t workspace_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -283,3 +283,84 @@ def vertex_pred_compact(feat, weights, biases, label):
     acc = acc + b[cols]
     acc[~ok] = 0.0
     return acc.reshape(B, H, W, 3)
+
+
+# --- test-time pose refinement (orc_icp.cpp) --------------------------------
+def icp_live_vertices(depth_u16, label, obj, factor, camera):
+    H, W = label.shape
+    d = np.ascontiguousarray(depth_u16, dtype=np.uint16)
+    lab, lp = _i(label)
+    out = np.empty((H, W, 3), np.float32)
+    fx, fy, px, py = (float(c) for c in camera)
+    lib().orc_icp_live_vertices(d.ctypes.data_as(ctypes.POINTER(ctypes.c_uint16)), lp, H, W, int(obj),
+                                ctypes.c_float(factor), ctypes.c_float(fx), ctypes.c_float(fy), ctypes.c_float(px),
+                                ctypes.c_float(py), out.ctypes.data_as(F32P))
+    return out
+
+
+def icp(live, pred_v, pred_n, camera, depth_range=(0.25, 6.0), max_error=0.01, iterations=8):
+    """df::icp restated: returns (update (7,), systems (iterations, 28))."""
+    H, W = live.shape[:2]
+    lv, lp = _f(live)
+    pv, pvp = _f(pred_v)
+    pn, pnp = _f(pred_n)
+    upd = np.empty(7, np.float32)
+    sysm = np.empty((max(iterations, 1), 28), np.float32)
+    fx, fy, px, py = (float(c) for c in camera)
+    c = ctypes.c_float
+    lib().orc_icp(lp, pvp, pnp, H, W, c(fx), c(fy), c(px), c(py), c(depth_range[0]), c(depth_range[1]),
+                  c(max_error), int(iterations), upd.ctypes.data_as(F32P), sysm.ctypes.data_as(F32P))
+    return upd, sysm[:iterations]
+
+
+def icp_center(live, label, obj, vertmap, pred_v, pred_n, max_error=0.01):
+    H, W = label.shape
+    lv, lp = _f(live)
+    lab, labp = _i(label)
+    vm, vmp = _f(vertmap)
+    pv, pvp = _f(pred_v)
+    pn, pnp = _f(pred_n)
+    out = np.empty(4, np.float32)
+    lib().orc_icp_center(lp, labp, int(obj), vmp, pvp, pnp, H, W, ctypes.c_float(max_error), out.ctypes.data_as(F32P))
+    return out
+
+
+def pose_energy(live, label, obj, pred_v, poses, depth_range=(0.25, 6.0)):
+    H, W = label.shape
+    lv, lp = _f(live)
+    lab, labp = _i(label)
+    pv, pvp = _f(pred_v)
+    P, Pp = _f(np.asarray(poses).reshape(-1, 7))
+    e = np.empty(P.shape[0], np.float32)
+    lib().orc_pose_energy(lp, labp, int(obj), pvp, H, W, ctypes.c_float(depth_range[0]),
+                          ctypes.c_float(depth_range[1]), Pp, P.shape[0], e.ctypes.data_as(F32P))
+    return e
+
+
+def se3_mul(a, b):
+    A, ap = _f(a)
+    B, bp = _f(b)
+    c = np.empty(7, np.float32)
+    lib().orc_se3_mul(ap, bp, c.ctypes.data_as(F32P))
+    return c
+
+
+def ldlt_solve6(A, b):
+    A_, ap = _f(A)
+    b_, bp = _f(b)
+    x = np.empty(6, np.float32)
+    lib().orc_ldlt_solve6(ap, bp, x.ctypes.data_as(F32P))
+    return x
+
+
+def icp_score(live, label, obj, vertmap, hyps, radius=0.01):
+    H, W = label.shape
+    lv, lp = _f(live)
+    lab, labp = _i(label)
+    vm, vmp = _f(vertmap)
+    P, Pp = _f(np.asarray(hyps).reshape(-1, 7))
+    sc = np.empty(P.shape[0], np.float32)
+    ch = np.zeros(1, np.int32)
+    lib().orc_icp_score(lp, labp, int(obj), vmp, H, W, Pp, P.shape[0], ctypes.c_float(radius),
+                        sc.ctypes.data_as(F32P), ch.ctypes.data_as(I32P))
+    return sc, int(ch[0])

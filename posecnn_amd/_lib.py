@@ -83,6 +83,20 @@ _SIGS = {
     "pcnn_pose_head_fwd": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p]),
     "pcnn_pose_head_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p,
                                    c_void_p]),
+    "pcnn_icp_live_vertices": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_float, c_float, c_float,
+                                       c_float, c_float, c_void_p, c_void_p]),
+    "pcnn_icp_workspace_size": (c_size_t, [c_int, c_int, c_int]),
+    "pcnn_icp": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_float, c_float,
+                         c_float, c_float, c_float, c_float, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                         c_size_t, c_void_p]),
+    "pcnn_icp_reduce_workspace_size": (c_size_t, [c_int, c_int, c_int]),
+    "pcnn_icp_center": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int,
+                                c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "pcnn_icp_score_workspace_size": (c_size_t, [c_int, c_int, c_int]),
+    "pcnn_icp_score": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_float, c_void_p,
+                               c_void_p, c_void_p, c_size_t, c_void_p]),
+    "pcnn_pose_energy": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_float, c_float, c_void_p, c_int,
+                                 c_void_p, c_void_p, c_size_t, c_void_p]),
 }
 
 

@@ -1,0 +1,811 @@
+// Test-time pose refinement on MI355X: the numerical
+// core of Synthesizer::solveICP (lib/synthesize/synthesize.cpp:2052-2395),
+// called from lib/fcn/test.py:1316-1351 through synthesizer.icp_python.
+//
+//   pcnn_icp_live_vertices   masked depth -> live vertex map per object
+//                            (synthesize.cpp:2140-2160 + df::backproject,
+//                            lib/kinect_fusion/src/image/backprojection.cu:10-27)
+//   pcnn_icp_center          translation re-centring (synthesize.cpp:2163-2233)
+//   pcnn_pose_energy         optEnergy of K candidate poses (synthesize.cpp:2474-2526)
+//   pcnn_icp                 df::icp (lib/kinect_fusion/src/optimization/icp.cpp:20-106,
+//                            icp.cu:22-245), batched over N (RoI, hypothesis) problems
+//
+// The reference runs each ICP iteration as a per-pixel kernel over the whole
+// H x W frame that writes a Jacobian row per pixel to HBM, a thrust
+// transform_reduce of those rows, a device sync and a host-side 6x6 LDLT solve
+// (icp.cpp:51-103).  Here the pixels whose rendered depth lies in the depth
+// range (the only ones icpKernel can use: icp.cu:56-63) are compacted once per
+// problem, in raster order, into dense (vertex, normal) records; one 1024-lane
+// workgroup per problem then runs every Gauss-Newton iteration: J^T J and J^T r
+// accumulate in registers, reduce through the wave and LDS in a fixed order,
+// and one lane solves the 6x6 system (Eigen LDLT with diagonal pivoting),
+// exponentiates the twist (Sophus SE3::exp) and left-multiplies it into the
+// accumulated update, which the next iteration reads from LDS.  No per-pixel
+// Jacobian ever reaches HBM and the host is never involved.
+//
+// Rendering (the OpenGL vertex / normal / canonical-coordinate maps of the
+// model at a pose, synthesize.cpp:2106-2137) and the NLopt Nelder-Mead pose
+// search (poseWithOpt, :2529-2573) are outside the path: the maps are inputs.
+#include "pcnn_common.h"
+
+namespace pcnn_refine {
+
+constexpr int kSeg = 2048;       // pixels per compaction / reduction block
+constexpr int kBlk = 256;        // threads of the per-pixel kernels
+constexpr int kIterThreads = 1024;
+constexpr int kSys = 28;         // 21 upper-triangle JTJ + 6 JTr + pixel count
+
+struct Quat { float w, x, y, z; };
+struct SE3 { Quat q; float t[3]; };
+
+// Eigen Quaternion::_transformVector (the point action of Sophus SO3)
+__device__ __forceinline__ void rotate(const Quat& q, float v0, float v1, float v2, float& o0, float& o1,
+                                       float& o2) {
+  float uv0 = q.y * v2 - q.z * v1;
+  float uv1 = q.z * v0 - q.x * v2;
+  float uv2 = q.x * v1 - q.y * v0;
+  uv0 = uv0 + uv0;
+  uv1 = uv1 + uv1;
+  uv2 = uv2 + uv2;
+  const float c0 = q.y * uv2 - q.z * uv1;
+  const float c1 = q.z * uv0 - q.x * uv2;
+  const float c2 = q.x * uv1 - q.y * uv0;
+  o0 = v0 + q.w * uv0 + c0;
+  o1 = v1 + q.w * uv1 + c1;
+  o2 = v2 + q.w * uv2 + c2;
+}
+
+// Sophus SE3 product a * b (quaternion renormalised by 2 / (1 + |q|^2))
+__device__ SE3 se3_mul(const SE3& a, const SE3& b) {
+  SE3 r;
+  float t0, t1, t2;
+  rotate(a.q, b.t[0], b.t[1], b.t[2], t0, t1, t2);
+  r.t[0] = a.t[0] + t0;
+  r.t[1] = a.t[1] + t1;
+  r.t[2] = a.t[2] + t2;
+  r.q.w = a.q.w * b.q.w - a.q.x * b.q.x - a.q.y * b.q.y - a.q.z * b.q.z;
+  r.q.x = a.q.w * b.q.x + a.q.x * b.q.w + a.q.y * b.q.z - a.q.z * b.q.y;
+  r.q.y = a.q.w * b.q.y + a.q.y * b.q.w + a.q.z * b.q.x - a.q.x * b.q.z;
+  r.q.z = a.q.w * b.q.z + a.q.z * b.q.w + a.q.x * b.q.y - a.q.y * b.q.x;
+  const float n2 = r.q.w * r.q.w + r.q.x * r.q.x + r.q.y * r.q.y + r.q.z * r.q.z;
+  if (n2 != 1.0f) {
+    const float s = 2.0f / (1.0f + n2);
+    r.q.w *= s;
+    r.q.x *= s;
+    r.q.y *= s;
+    r.q.z *= s;
+  }
+  return r;
+}
+
+// Sophus SE3<float>::exp of the twist (upsilon, omega)
+__device__ SE3 se3_exp(const float a[6]) {
+  const float w0 = a[3], w1 = a[4], w2 = a[5];
+  const float theta_sq = w0 * w0 + w1 * w1 + w2 * w2;
+  const float theta = sqrtf(theta_sq);
+  const float eps = 1e-5f;
+  float imag, real;
+  if (theta < eps) {
+    const float t4 = theta_sq * theta_sq;
+    imag = 0.5f - (float)(1.0 / 48.0) * theta_sq + (float)(1.0 / 3840.0) * t4;
+    real = 1.0f - 0.5f * theta_sq + (float)(1.0 / 384.0) * t4;
+  } else {
+    imag = sinf(0.5f * theta) / theta;
+    real = cosf(0.5f * theta);
+  }
+  SE3 r;
+  r.q = {real, imag * w0, imag * w1, imag * w2};
+  float V[9];
+  if (theta < eps) {  // V = so3.matrix()
+    const Quat& q = r.q;
+    const float tx = 2.f * q.x, ty = 2.f * q.y, tz = 2.f * q.z;
+    const float twx = tx * q.w, twy = ty * q.w, twz = tz * q.w;
+    const float txx = tx * q.x, txy = ty * q.x, txz = tz * q.x;
+    const float tyy = ty * q.y, tyz = tz * q.y, tzz = tz * q.z;
+    V[0] = 1.f - (tyy + tzz); V[1] = txy - twz; V[2] = txz + twy;
+    V[3] = txy + twz; V[4] = 1.f - (txx + tzz); V[5] = tyz - twx;
+    V[6] = txz - twy; V[7] = tyz + twx; V[8] = 1.f - (txx + tyy);
+  } else {
+    const float O[9] = {0.f, -w2, w1, w2, 0.f, -w0, -w1, w0, 0.f};
+    const float c1 = (1.0f - cosf(theta)) / theta_sq;
+    const float c2 = (theta - sinf(theta)) / (theta_sq * theta);
+#pragma unroll
+    for (int i = 0; i < 3; i++)
+#pragma unroll
+      for (int j = 0; j < 3; j++) {
+        const float o2 = O[i * 3 + 0] * O[0 * 3 + j] + O[i * 3 + 1] * O[1 * 3 + j] + O[i * 3 + 2] * O[2 * 3 + j];
+        V[i * 3 + j] = (i == j ? 1.f : 0.f) + c1 * O[i * 3 + j] + c2 * o2;
+      }
+  }
+#pragma unroll
+  for (int i = 0; i < 3; i++) r.t[i] = V[i * 3 + 0] * a[0] + V[i * 3 + 1] * a[1] + V[i * 3 + 2] * a[2];
+  return r;
+}
+
+// Eigen 3.3 LDLT<Upper> of the symmetric 6x6 system and its solve
+// (diagonal pivoting; zero pivots -> 0 in the pseudo-inverse of D)
+__device__ void ldlt_solve6(float m[36], const float b[6], float x[6]) {
+  int tr[6];
+  float temp[6];
+  for (int k = 0; k < 6; k++) {
+    int big = k;
+    float bv = fabsf(m[k * 6 + k]);
+    for (int i = k + 1; i < 6; i++)
+      if (fabsf(m[i * 6 + i]) > bv) {
+        bv = fabsf(m[i * 6 + i]);
+        big = i;
+      }
+    tr[k] = big;
+    if (big != k) {
+      for (int j = 0; j < k; j++) { const float t = m[k * 6 + j]; m[k * 6 + j] = m[big * 6 + j]; m[big * 6 + j] = t; }
+      for (int i = big + 1; i < 6; i++) { const float t = m[i * 6 + k]; m[i * 6 + k] = m[i * 6 + big]; m[i * 6 + big] = t; }
+      { const float t = m[k * 6 + k]; m[k * 6 + k] = m[big * 6 + big]; m[big * 6 + big] = t; }
+      for (int i = k + 1; i < big; i++) { const float t = m[i * 6 + k]; m[i * 6 + k] = m[big * 6 + i]; m[big * 6 + i] = t; }
+    }
+    if (k > 0) {
+      for (int j = 0; j < k; j++) temp[j] = m[j * 6 + j] * m[k * 6 + j];
+      float s = 0.f;
+      for (int j = 0; j < k; j++) s = s + m[k * 6 + j] * temp[j];
+      m[k * 6 + k] -= s;
+      for (int i = k + 1; i < 6; i++) {
+        float si = 0.f;
+        for (int j = 0; j < k; j++) si = si + m[i * 6 + j] * temp[j];
+        m[i * 6 + k] -= si;
+      }
+    }
+    const float akk = m[k * 6 + k];
+    const bool valid = fabsf(akk) > 0.f;
+    if (k == 0 && !valid) {  // all-zero diagonal: nothing to solve
+      for (int i = 0; i < 6; i++) x[i] = 0.f;
+      return;
+    }
+    if (k < 5 && valid)
+      for (int i = k + 1; i < 6; i++) m[i * 6 + k] /= akk;
+  }
+  for (int i = 0; i < 6; i++) x[i] = b[i];
+  for (int k = 0; k < 6; k++) { const float t = x[k]; x[k] = x[tr[k]]; x[tr[k]] = t; }
+  for (int i = 0; i < 6; i++)
+    for (int j = 0; j < i; j++) x[i] -= m[i * 6 + j] * x[j];
+  for (int i = 0; i < 6; i++) {
+    const float d = m[i * 6 + i];
+    x[i] = fabsf(d) > 1.17549435e-38f ? x[i] / d : 0.f;
+  }
+  for (int i = 5; i >= 0; i--)
+    for (int j = i + 1; j < 6; j++) x[i] -= m[j * 6 + i] * x[j];
+  for (int k = 5; k >= 0; k--) { const float t = x[k]; x[k] = x[tr[k]]; x[tr[k]] = t; }
+}
+
+__device__ __forceinline__ bool in_range(float z, float znear, float zfar) { return !(z < znear || z > zfar); }
+
+// Block-wide sum of an int (all threads call; result in every thread).
+template <int T>
+__device__ __forceinline__ int block_sum_int(int v, int* sh) {
+  v = pcnn::wave_sum(v);
+  if (pcnn::lane_id() == 0) sh[threadIdx.x >> 6] = v;
+  __syncthreads();
+  int s = 0;
+#pragma unroll
+  for (int w = 0; w < T / 64; w++) s += sh[w];
+  __syncthreads();
+  return s;
+}
+
+// ---------------------------------------------------------------------------
+// live vertices: one thread per 4 pixels of one object's map (float4 stores)
+__global__ void __launch_bounds__(kBlk) k_icp_live(const uint16_t* __restrict__ depth,
+                                                   const int32_t* __restrict__ label, int HW, int W,
+                                                   const int32_t* __restrict__ obj_ids, float factor, float fx,
+                                                   float fy, float px, float py, float* __restrict__ out) {
+  const int l = blockIdx.y;
+  const int obj = obj_ids[l];
+  const int p0 = 4 * (blockIdx.x * kBlk + threadIdx.x);
+  if (p0 >= HW) return;
+  float v[12];
+#pragma unroll
+  for (int e = 0; e < 4; e++) {
+    const int p = p0 + e;
+    float d = 0.f;
+    int x = 0, y = 0;
+    if (p < HW) {
+      d = label[p] == obj ? (float)depth[p] / factor : 0.f;
+      x = p % W;
+      y = p / W;
+    }
+    v[3 * e + 0] = (((float)x - px) / fx) * d;
+    v[3 * e + 1] = (((float)y - py) / fy) * d;
+    v[3 * e + 2] = d;
+  }
+  float* o = out + ((size_t)l * HW + p0) * 3;
+  if (p0 + 4 <= HW) {
+    float4* o4 = (float4*)o;  // HW % 4 == 0 is required by the launcher
+    o4[0] = make_float4(v[0], v[1], v[2], v[3]);
+    o4[1] = make_float4(v[4], v[5], v[6], v[7]);
+    o4[2] = make_float4(v[8], v[9], v[10], v[11]);
+  }
+}
+
+// compaction pass 1: per (segment, problem) the count of pixels whose rendered
+// depth is in range
+__global__ void __launch_bounds__(kBlk) k_icp_count(const float* __restrict__ pred_v, int HW, float znear,
+                                                    float zfar, int nseg, int32_t* __restrict__ cnt) {
+  __shared__ int sh[kBlk / 64];
+  const int n = blockIdx.y, seg = blockIdx.x;
+  const float* pv = pred_v + (size_t)n * HW * 4;
+  int c = 0;
+  for (int i = threadIdx.x; i < kSeg; i += kBlk) {
+    const int p = seg * kSeg + i;
+    if (p < HW && in_range(pv[(size_t)p * 4 + 2], znear, zfar)) c++;
+  }
+  c = block_sum_int<kBlk>(c, sh);
+  if (threadIdx.x == 0) cnt[(size_t)n * nseg + seg] = c;
+}
+
+// compaction pass 2: the segment's in-range pixels in raster order ->
+// records [offset, offset + count) of problem n (rec[2i] = vertex, rec[2i+1] =
+// normal)
+__global__ void __launch_bounds__(kBlk) k_icp_scatter(const float* __restrict__ pred_v,
+                                                      const float* __restrict__ pred_n, int HW, float znear,
+                                                      float zfar, int nseg, const int32_t* __restrict__ cnt,
+                                                      float4* __restrict__ rec) {
+  __shared__ int sh[kBlk / 64];
+  __shared__ int wc[kBlk / 64];
+  const int n = blockIdx.y, seg = blockIdx.x;
+  const int32_t* cn = cnt + (size_t)n * nseg;
+  int o = 0;
+  for (int s = threadIdx.x; s < seg; s += kBlk) o += cn[s];
+  int off = block_sum_int<kBlk>(o, sh);
+  const float4* pv = (const float4*)(pred_v + (size_t)n * HW * 4);
+  const float4* pn = (const float4*)(pred_n + (size_t)n * HW * 4);
+  float4* rn = rec + (size_t)n * HW * 2;
+  const int wave = threadIdx.x >> 6;
+  for (int i0 = 0; i0 < kSeg; i0 += kBlk) {
+    const int p = seg * kSeg + i0 + threadIdx.x;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    bool ok = false;
+    if (p < HW) {
+      v = pv[p];
+      ok = in_range(v.z, znear, zfar);
+    }
+    const uint64_t m = __ballot(ok);
+    if (pcnn::lane_id() == 0) wc[wave] = __popcll(m);
+    __syncthreads();
+    int base = off;
+    for (int w = 0; w < wave; w++) base += wc[w];
+    if (ok) {
+      const int r = base + __popcll(m & pcnn::lanemask_lt());
+      rn[2 * (size_t)r] = v;
+      rn[2 * (size_t)r + 1] = pn[p];
+    }
+    for (int w = 0; w < kBlk / 64; w++) off += wc[w];
+    __syncthreads();
+  }
+}
+
+// The Gauss-Newton loop of df::icp for one problem per workgroup.
+__global__ void __launch_bounds__(kIterThreads) k_icp_iterate(
+    const float4* __restrict__ rec, const int32_t* __restrict__ cnt, int nseg, const float* __restrict__ live,
+    const int32_t* __restrict__ live_index, int H, int W, float fx, float fy, float px, float py, float znear,
+    float zfar, float max_error, int iterations, const float* __restrict__ pose_in, float* __restrict__ update,
+    float* __restrict__ pose_out, float* __restrict__ systems) {
+  __shared__ float part[kIterThreads / 64][kSys];
+  __shared__ float sys[kSys];
+  __shared__ SE3 acc_sh;
+  __shared__ int ish[kIterThreads / 64];
+  const int n = blockIdx.x;
+  const int HW = H * W;
+  int c = 0;
+  for (int s = threadIdx.x; s < nseg; s += kIterThreads) c += cnt[(size_t)n * nseg + s];
+  const int total = block_sum_int<kIterThreads>(c, ish);
+  const float4* rn = rec + (size_t)n * HW * 2;
+  const float* lv = live + (size_t)(live_index ? live_index[n] : n) * HW * 3;
+  if (threadIdx.x == 0) {
+    acc_sh.q = {1.f, 0.f, 0.f, 0.f};
+    acc_sh.t[0] = acc_sh.t[1] = acc_sh.t[2] = 0.f;
+  }
+  __syncthreads();
+  const float border = 2.f;
+  const float umax = (float)(W - 1) - border, vmax = (float)(H - 1) - border;
+  const int wave = threadIdx.x >> 6, lane = pcnn::lane_id();
+  for (int it = 0; it < iterations; it++) {
+    const SE3 T = acc_sh;
+    float a[kSys];
+#pragma unroll
+    for (int e = 0; e < kSys; e++) a[e] = 0.f;
+    for (int i = threadIdx.x; i < total; i += kIterThreads) {
+      const float4 v = rn[2 * (size_t)i];
+      const float4 nm = rn[2 * (size_t)i + 1];
+      float p0, p1, p2;
+      rotate(T.q, v.x, v.y, v.z, p0, p1, p2);
+      p0 = p0 + T.t[0];
+      p1 = p1 + T.t[1];
+      p2 = p2 + T.t[2];
+      const int u = (int)((p0 / p2) * fx + px + 0.5f);  // v_cvt_i32_f32: NaN -> 0
+      const int vv = (int)((p1 / p2) * fy + py + 0.5f);
+      if ((float)u <= border || (float)u >= umax || (float)vv <= border || (float)vv >= vmax) continue;
+      const float* l3 = lv + ((size_t)vv * W + u) * 3;
+      const float l0 = l3[0], l1 = l3[1], l2 = l3[2];
+      if (l2 < znear || l2 > zfar) continue;
+      const float nr = sqrtf(p0 * p0 + p1 * p1 + p2 * p2);
+      if (-((p0 / nr) * nm.x + (p1 / nr) * nm.y + (p2 / nr) * nm.z) < 0.1f) continue;
+      const float e = nm.x * (l0 - p0) + nm.y * (l1 - p1) + nm.z * (l2 - p2);
+      if (fabsf(e) > max_error) continue;
+      const float w = 1.0f / l2;
+      float J[6];
+      J[0] = w * nm.x;
+      J[1] = w * nm.y;
+      J[2] = w * nm.z;
+      J[3] = w * (nm.z * p1 - nm.y * p2);
+      J[4] = w * (nm.x * p2 - nm.z * p0);
+      J[5] = w * (nm.y * p0 - nm.x * p1);
+      const float r = w * e;
+      int k = 0;
+#pragma unroll
+      for (int ii = 0; ii < 6; ii++)
+#pragma unroll
+        for (int jj = ii; jj < 6; jj++) a[k++] += J[ii] * J[jj];
+#pragma unroll
+      for (int ii = 0; ii < 6; ii++) a[21 + ii] += J[ii] * r;
+      a[27] += 1.f;
+    }
+    // fixed-order reduction: wave butterfly, then the waves in order
+#pragma unroll
+    for (int e = 0; e < kSys; e++) {
+      const float s = pcnn::wave_sum(a[e]);
+      if (lane == 0) part[wave][e] = s;
+    }
+    __syncthreads();
+    if (threadIdx.x < kSys) {
+      float s = 0.f;
+      for (int w = 0; w < kIterThreads / 64; w++) s += part[w][threadIdx.x];
+      sys[threadIdx.x] = s;
+      if (systems) systems[((size_t)n * iterations + it) * kSys + threadIdx.x] = s;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      float m[36], b[6], x[6];
+      int k = 0;
+      for (int i = 0; i < 6; i++)
+        for (int j = i; j < 6; j++) {
+          m[i * 6 + j] = sys[k];
+          m[j * 6 + i] = sys[k];
+          k++;
+        }
+      for (int i = 0; i < 6; i++) b[i] = sys[21 + i];
+      ldlt_solve6(m, b, x);
+      acc_sh = se3_mul(se3_exp(x), T);
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const SE3 A = acc_sh;
+    float* u = update + (size_t)n * 7;
+    u[0] = A.q.w; u[1] = A.q.x; u[2] = A.q.y; u[3] = A.q.z;
+    u[4] = A.t[0]; u[5] = A.t[1]; u[6] = A.t[2];
+    if (pose_in && pose_out) {  // refinePose: T_co = update * T_co (synthesize.cpp:2023-2025)
+      const float* P = pose_in + (size_t)n * 7;
+      const float qn = sqrtf(P[0] * P[0] + P[1] * P[1] + P[2] * P[2] + P[3] * P[3]);
+      SE3 B;
+      B.q = {P[0] / qn, P[1] / qn, P[2] / qn, P[3] / qn};
+      B.t[0] = P[4]; B.t[1] = P[5]; B.t[2] = P[6];
+      const SE3 R = se3_mul(A, B);
+      float* o = pose_out + (size_t)n * 7;
+      o[0] = R.q.w; o[1] = R.q.x; o[2] = R.q.y; o[3] = R.q.z;
+      o[4] = R.t[0]; o[5] = R.t[1]; o[6] = R.t[2];
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Segmented sums with a fixed-order finish: every block writes its partial,
+// the last block to arrive (ticket) adds the partials in block order.
+template <int NV>
+__device__ __forceinline__ bool finish_partials(const float (&v)[NV], float* partial, int nblk, int blk,
+                                                unsigned* ticket, float* sh, int* flag) {
+#pragma unroll
+  for (int e = 0; e < NV; e++) {
+    const float s = pcnn::wave_sum(v[e]);
+    if (pcnn::lane_id() == 0) sh[(threadIdx.x >> 6) * NV + e] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x < NV) {
+    float s = 0.f;
+    for (int w = 0; w < kBlk / 64; w++) s += sh[w * NV + threadIdx.x];
+    partial[(size_t)blk * NV + threadIdx.x] = s;
+  }
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0) *flag = atomicAdd(ticket, 1u) == (unsigned)(nblk - 1);
+  __syncthreads();
+  if (!*flag) return false;
+  __threadfence();
+  if (threadIdx.x < NV) {  // totals -> sh[0, NV)
+    float s = 0.f;
+    for (int b = 0; b < nblk; b++) s += __builtin_nontemporal_load(partial + (size_t)b * NV + threadIdx.x);
+    sh[threadIdx.x] = s;
+  }
+  if (threadIdx.x == 0) *ticket = 0u;
+  __syncthreads();
+  return true;
+}
+
+// translation re-centring of solveICP for L objects (grid: segments x objects)
+__global__ void __launch_bounds__(kBlk) k_icp_center(const float* __restrict__ live, const int32_t* __restrict__ label,
+                                                     const int32_t* __restrict__ obj_ids,
+                                                     const float* __restrict__ vertmap, const float* __restrict__ pred_v,
+                                                     const float* __restrict__ pred_n, int HW, float max_error,
+                                                     const float* __restrict__ pose_in, float* __restrict__ partial,
+                                                     unsigned* __restrict__ tickets, float* __restrict__ out,
+                                                     float* __restrict__ pose_out) {
+  __shared__ float sh[(kBlk / 64) * 4];
+  __shared__ int flag;
+  const int l = blockIdx.y, seg = blockIdx.x, nblk = gridDim.x;
+  const int obj = obj_ids[l];
+  const float* lv = live + (size_t)l * HW * 3;
+  const float* vm = vertmap + (size_t)l * HW * 3;
+  const float* pv = pred_v + (size_t)l * HW * 4;
+  const float* pn = pred_n + (size_t)l * HW * 4;
+  float v[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int i = threadIdx.x; i < kSeg; i += kBlk) {
+    const int j = seg * kSeg + i;
+    if (j >= HW || label[j] != obj) continue;
+    const float d2 = lv[(size_t)j * 3 + 2];
+    if (!(d2 > 0.f)) continue;
+    const float mx = vm[(size_t)j * 3 + 0];
+    const float mxr = mx - roundf(mx);  // the class offset dropped; std::round = half away from zero
+    const float vy = vm[(size_t)j * 3 + 1], vz = vm[(size_t)j * 3 + 2];
+    if (isnan(mxr) || isnan(vy) || isnan(vz)) continue;
+    const float d0 = lv[(size_t)j * 3 + 0], d1 = lv[(size_t)j * 3 + 1];
+    const float* n = pn + (size_t)j * 4;
+    const float* p = pv + (size_t)j * 4;
+    const float e = n[0] * (d0 - p[0]) + n[1] * (d1 - p[1]) + n[2] * (d2 - p[2]);
+    if (fabsf(e) < max_error) {
+      v[0] += d0 - mxr;
+      v[1] += d1 - vy;
+      v[2] += d2 - vz;
+      v[3] += 1.f;
+    }
+  }
+  if (!finish_partials<4>(v, partial + (size_t)l * nblk * 4, nblk, seg, tickets + l, sh, &flag)) return;
+  if (threadIdx.x == 0) {
+    const float c = sh[3];
+    const float Tx = c > 0.f ? sh[0] / c : 0.f, Ty = c > 0.f ? sh[1] / c : 0.f, Tz = c > 0.f ? sh[2] / c : 0.f;
+    float* o = out + (size_t)l * 4;
+    o[0] = Tx; o[1] = Ty; o[2] = Tz; o[3] = c;
+    if (pose_in && pose_out) {  // T_co.translation = (rx Tz, ry Tz, Tz) when c > 0 (:2207-2219)
+      const float* P = pose_in + (size_t)l * 7;
+      float* Q = pose_out + (size_t)l * 7;
+      float rx = 0.f, ry = 0.f;
+      if (P[6] != 0.f) {
+        rx = P[4] / P[6];
+        ry = P[5] / P[6];
+      }
+      for (int e = 0; e < 4; e++) Q[e] = P[e];
+      Q[4] = c > 0.f ? rx * Tz : P[4];
+      Q[5] = c > 0.f ? ry * Tz : P[5];
+      Q[6] = c > 0.f ? Tz : P[6];
+    }
+  }
+}
+
+// optEnergy for K poses over the object's pixels (grid: segments x poses)
+__global__ void __launch_bounds__(kBlk) k_pose_energy(const float* __restrict__ live, const int32_t* __restrict__ label,
+                                                      int obj, const float* __restrict__ pred_v, int HW, float znear,
+                                                      float zfar, const float* __restrict__ poses,
+                                                      float* __restrict__ partial, unsigned* __restrict__ tickets,
+                                                      float* __restrict__ energy) {
+  __shared__ float sh[(kBlk / 64) * 2];
+  __shared__ int flag;
+  const int k = blockIdx.y, seg = blockIdx.x, nblk = gridDim.x;
+  const float* P = poses + (size_t)k * 7;
+  const float qn = sqrtf(P[0] * P[0] + P[1] * P[1] + P[2] * P[2] + P[3] * P[3]);
+  const Quat q = {P[0] / qn, P[1] / qn, P[2] / qn, P[3] / qn};
+  float v[2] = {0.f, 0.f};
+  for (int i = threadIdx.x; i < kSeg; i += kBlk) {
+    const int j = seg * kSeg + i;
+    if (j >= HW || label[j] != obj) continue;
+    float p0, p1, p2;
+    rotate(q, pred_v[(size_t)j * 4 + 0], pred_v[(size_t)j * 4 + 1], pred_v[(size_t)j * 4 + 2], p0, p1, p2);
+    p0 = p0 + P[4];
+    p1 = p1 + P[5];
+    p2 = p2 + P[6];
+    const float l0 = live[(size_t)j * 3 + 0], l1 = live[(size_t)j * 3 + 1], l2 = live[(size_t)j * 3 + 2];
+    if (!isnan(p0) && !isnan(p1) && !isnan(p2) && l2 > znear && l2 < zfar && p2 > znear && p2 < zfar) {
+      const float dx = p0 - l0, dy = p1 - l1, dz = p2 - l2;
+      v[0] += sqrtf(dx * dx + dy * dy + dz * dz);
+      v[1] += 1.f;
+    }
+  }
+  if (!finish_partials<2>(v, partial + (size_t)k * nblk * 2, nblk, seg, tickets + k, sh, &flag)) return;
+  if (threadIdx.x == 0) energy[k] = sh[1] > 0.f ? sh[0] / sh[1] : 0.f;
+}
+
+
+// ---------------------------------------------------------------------------
+// SegICP hypothesis score (synthesize.cpp:2288-2330).  The object's pixels
+// with depth > 0 and a finite rendered vertmap give, in raster order, the
+// model points (canonical vertmap, class offset dropped) and the depth points
+// (live vertices).  For hypothesis j every transformed model point takes its
+// nearest depth point within 1 cm (squared distance < 1e-4: FLANN's radius
+// test; ties -> the lowest index) and flags it; score_j = distinct flagged
+// depth points / model points.  The reference's order of flagging (an OpenMP
+// race) does not change the count.
+__device__ __forceinline__ bool score_pick(const float* __restrict__ live, const int32_t* __restrict__ label, int obj,
+                                           const float* __restrict__ vertmap, int j) {
+  if (label[j] != obj || !(live[(size_t)j * 3 + 2] > 0.f)) return false;
+  const float mx = vertmap[(size_t)j * 3 + 0];
+  return !isnan(mx - roundf(mx)) && !isnan(vertmap[(size_t)j * 3 + 1]) && !isnan(vertmap[(size_t)j * 3 + 2]);
+}
+
+__global__ void __launch_bounds__(kBlk) k_score_count(const float* __restrict__ live, const int32_t* __restrict__ label,
+                                                      int obj, const float* __restrict__ vertmap, int HW, int nseg,
+                                                      int32_t* __restrict__ cnt) {
+  __shared__ int sh[kBlk / 64];
+  int c = 0;
+  for (int i = threadIdx.x; i < kSeg; i += kBlk) {
+    const int j = blockIdx.x * kSeg + i;
+    if (j < HW && score_pick(live, label, obj, vertmap, j)) c++;
+  }
+  c = block_sum_int<kBlk>(c, sh);
+  if (threadIdx.x == 0) cnt[blockIdx.x] = c;
+}
+
+__global__ void __launch_bounds__(kBlk) k_score_scatter(const float* __restrict__ live,
+                                                        const int32_t* __restrict__ label, int obj,
+                                                        const float* __restrict__ vertmap, int HW, int nseg,
+                                                        const int32_t* __restrict__ cnt, float4* __restrict__ model,
+                                                        float4* __restrict__ dpts) {
+  __shared__ int sh[kBlk / 64];
+  __shared__ int wc[kBlk / 64];
+  int o = 0;
+  for (int s = threadIdx.x; s < (int)blockIdx.x; s += kBlk) o += cnt[s];
+  int off = block_sum_int<kBlk>(o, sh);
+  const int wave = threadIdx.x >> 6;
+  for (int i0 = 0; i0 < kSeg; i0 += kBlk) {
+    const int j = blockIdx.x * kSeg + i0 + threadIdx.x;
+    const bool ok = j < HW && score_pick(live, label, obj, vertmap, j);
+    const uint64_t m = __ballot(ok);
+    if (pcnn::lane_id() == 0) wc[wave] = __popcll(m);
+    __syncthreads();
+    int base = off;
+    for (int w = 0; w < wave; w++) base += wc[w];
+    if (ok) {
+      const int r = base + __popcll(m & pcnn::lanemask_lt());
+      const float mx = vertmap[(size_t)j * 3 + 0];
+      model[r] = make_float4(mx - roundf(mx), vertmap[(size_t)j * 3 + 1], vertmap[(size_t)j * 3 + 2], 0.f);
+      dpts[r] = make_float4(live[(size_t)j * 3 + 0], live[(size_t)j * 3 + 1], live[(size_t)j * 3 + 2], 0.f);
+    }
+    for (int w = 0; w < kBlk / 64; w++) off += wc[w];
+    __syncthreads();
+  }
+}
+
+constexpr int kScoreTile = 2048;  // depth points per LDS tile
+
+// grid (query blocks, hypotheses): nearest depth point of each transformed
+// model point, flagged when within the radius
+__global__ void __launch_bounds__(kBlk) k_score_nn(const float4* __restrict__ model, const float4* __restrict__ dpts,
+                                                   const int32_t* __restrict__ cnt, int nseg,
+                                                   const float* __restrict__ hyps, float r2,
+                                                   uint8_t* __restrict__ flags, int cap) {
+  __shared__ float4 tile[kScoreTile];
+  __shared__ int ish[kBlk / 64];
+  int c = 0;
+  for (int s = threadIdx.x; s < nseg; s += kBlk) c += cnt[s];
+  const int M = block_sum_int<kBlk>(c, ish);
+  const int h = blockIdx.y;
+  const int q = blockIdx.x * kBlk + threadIdx.x;
+  if ((int)blockIdx.x * kBlk >= M) return;  // block-uniform
+  const float* P = hyps + (size_t)h * 7;
+  const float qn = sqrtf(P[0] * P[0] + P[1] * P[1] + P[2] * P[2] + P[3] * P[3]);
+  const Quat qq = {P[0] / qn, P[1] / qn, P[2] / qn, P[3] / qn};
+  float x = 0.f, y = 0.f, z = 0.f;
+  if (q < M) {
+    const float4 m = model[q];
+    rotate(qq, m.x, m.y, m.z, x, y, z);
+    x = x + P[4];
+    y = y + P[5];
+    z = z + P[6];
+  }
+  float best = r2;  // strict: only squared distances < r2 qualify
+  int bi = -1;
+  for (int t0 = 0; t0 < M; t0 += kScoreTile) {
+    const int tn = min(kScoreTile, M - t0);
+    __syncthreads();
+    for (int i = threadIdx.x; i < tn; i += kBlk) tile[i] = dpts[t0 + i];
+    __syncthreads();
+    for (int i = 0; i < tn; i++) {
+      const float4 d = tile[i];
+      const float dx = x - d.x, dy = y - d.y, dz = z - d.z;
+      const float d2 = dx * dx + dy * dy + dz * dz;
+      if (d2 < best) {  // ties keep the lower index
+        best = d2;
+        bi = t0 + i;
+      }
+    }
+  }
+  if (q < M && bi >= 0) flags[(size_t)h * cap + bi] = 1;
+}
+
+// score per hypothesis and the first best one (one workgroup)
+__global__ void __launch_bounds__(kBlk) k_score_select(const uint8_t* __restrict__ flags, const int32_t* __restrict__ cnt,
+                                                       int nseg, int J, int cap, float* __restrict__ score,
+                                                       int32_t* __restrict__ choose) {
+  __shared__ int ish[kBlk / 64];
+  __shared__ float sc[64];
+  int c = 0;
+  for (int s = threadIdx.x; s < nseg; s += kBlk) c += cnt[s];
+  const int M = block_sum_int<kBlk>(c, ish);
+  for (int h = 0; h < J; h++) {
+    int f = 0;
+    for (int i = threadIdx.x; i < M; i += kBlk) f += flags[(size_t)h * cap + i];
+    f = block_sum_int<kBlk>(f, ish);
+    if (threadIdx.x == 0) {
+      const float v = M > 0 ? (float)f / (float)M : 0.f;
+      score[h] = v;
+      if (h < 64) sc[h] = v;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float mx = -3.402823466e38f;
+    int ch = -1;
+    for (int h = 0; h < J && h < 64; h++)
+      if (sc[h] > mx) {
+        mx = sc[h];
+        ch = h;
+      }
+    *choose = M > 0 ? ch : 0;  // no depth point: hyps[0] (synthesize.cpp:2333-2334)
+  }
+}
+
+struct IcpWs {
+  int32_t* cnt;
+  float4* rec;
+};
+
+inline IcpWs carve_icp(void* base, int N, int HW, size_t* bytes) {
+  pcnn::Carve cv(base);
+  IcpWs ws;
+  const int nseg = (HW + kSeg - 1) / kSeg;
+  ws.cnt = cv.take<int32_t>((size_t)N * nseg);
+  ws.rec = cv.take<float4>((size_t)N * HW * 2);
+  if (bytes) *bytes = cv.off;
+  return ws;
+}
+
+// partial sums + tickets of the segmented reductions
+inline void carve_red(void* base, int L, int HW, int NV, float** partial, unsigned** tickets, size_t* bytes) {
+  pcnn::Carve cv(base);
+  const int nseg = (HW + kSeg - 1) / kSeg;
+  *tickets = cv.take<unsigned>((size_t)L);
+  *partial = cv.take<float>((size_t)L * nseg * NV);
+  if (bytes) *bytes = cv.off;
+}
+
+}  // namespace pcnn_refine
+
+using namespace pcnn_refine;
+
+extern "C" int pcnn_icp_live_vertices(const uint16_t* depth, const int32_t* label, int H, int W,
+                                      const int32_t* obj_ids, int L, float factor, float fx, float fy, float px,
+                                      float py, float* out, void* stream) {
+  PCNN_REQUIRE(depth && label && obj_ids && out && H > 0 && W > 0 && L > 0 && (H * W) % 4 == 0);
+  const int HW = H * W;
+  const int nb = (HW / 4 + kBlk - 1) / kBlk;
+  hipLaunchKernelGGL(k_icp_live, dim3(nb, L), dim3(kBlk), 0, (hipStream_t)stream, depth, label, HW, W, obj_ids,
+                     factor, fx, fy, px, py, out);
+  PCNN_CHECK_LAUNCH();
+  return PCNN_OK;
+}
+
+extern "C" size_t pcnn_icp_workspace_size(int N, int H, int W) {
+  if (N <= 0 || H <= 0 || W <= 0) return 0;
+  size_t b = 0;
+  carve_icp(nullptr, N, H * W, &b);
+  return b + 256;
+}
+
+extern "C" int pcnn_icp(const float* live, const int32_t* live_index, const float* pred_vertices,
+                        const float* pred_normals, int N, int H, int W, float fx, float fy, float px, float py,
+                        float znear, float zfar, float max_error, int iterations, const float* pose_in, float* update,
+                        float* pose_out, float* systems, void* workspace, size_t workspace_bytes, void* stream) {
+  PCNN_REQUIRE(live && pred_vertices && pred_normals && update && workspace && N > 0 && H > 0 && W > 0 &&
+               iterations >= 0 && (long)H * W * 2 * N < (1l << 31));
+  size_t need = 0;
+  carve_icp(nullptr, N, H * W, &need);
+  if (workspace_bytes < need) return PCNN_ECAPACITY;
+  IcpWs ws = carve_icp(workspace, N, H * W, nullptr);
+  const int HW = H * W, nseg = (HW + kSeg - 1) / kSeg;
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(k_icp_count, dim3(nseg, N), dim3(kBlk), 0, st, pred_vertices, HW, znear, zfar, nseg, ws.cnt);
+  hipLaunchKernelGGL(k_icp_scatter, dim3(nseg, N), dim3(kBlk), 0, st, pred_vertices, pred_normals, HW, znear, zfar,
+                     nseg, ws.cnt, ws.rec);
+  hipLaunchKernelGGL(k_icp_iterate, dim3(N), dim3(kIterThreads), 0, st, ws.rec, ws.cnt, nseg, live, live_index, H, W,
+                     fx, fy, px, py, znear, zfar, max_error, iterations, pose_in, update, pose_out, systems);
+  PCNN_CHECK_LAUNCH();
+  return PCNN_OK;
+}
+
+extern "C" size_t pcnn_icp_reduce_workspace_size(int L, int H, int W) {
+  if (L <= 0 || H <= 0 || W <= 0) return 0;
+  size_t b = 0;
+  float* p;
+  unsigned* t;
+  carve_red(nullptr, L, H * W, 4, &p, &t, &b);
+  return b + 256;
+}
+
+extern "C" int pcnn_icp_center(const float* live, const int32_t* label, const int32_t* obj_ids, int L,
+                               const float* vertmap, const float* pred_vertices, const float* pred_normals, int H,
+                               int W, float max_error, const float* pose_in, float* out, float* pose_out,
+                               void* workspace, size_t workspace_bytes, void* stream) {
+  PCNN_REQUIRE(live && label && obj_ids && vertmap && pred_vertices && pred_normals && out && workspace && L > 0 &&
+               H > 0 && W > 0);
+  size_t need = 0;
+  float* partial;
+  unsigned* tickets;
+  carve_red(nullptr, L, H * W, 4, &partial, &tickets, &need);
+  if (workspace_bytes < need) return PCNN_ECAPACITY;
+  carve_red(workspace, L, H * W, 4, &partial, &tickets, nullptr);
+  hipStream_t st = (hipStream_t)stream;
+  if (hipMemsetAsync(tickets, 0, (size_t)L * sizeof(unsigned), st) != hipSuccess) return PCNN_EHIP;
+  const int HW = H * W, nseg = (HW + kSeg - 1) / kSeg;
+  hipLaunchKernelGGL(k_icp_center, dim3(nseg, L), dim3(kBlk), 0, st, live, label, obj_ids, vertmap, pred_vertices,
+                     pred_normals, HW, max_error, pose_in, partial, tickets, out, pose_out);
+  PCNN_CHECK_LAUNCH();
+  return PCNN_OK;
+}
+
+extern "C" int pcnn_pose_energy(const float* live, const int32_t* label, int obj, const float* pred_vertices, int H,
+                                int W, float znear, float zfar, const float* poses, int K, float* energy,
+                                void* workspace, size_t workspace_bytes, void* stream) {
+  PCNN_REQUIRE(live && label && pred_vertices && poses && energy && workspace && K > 0 && H > 0 && W > 0);
+  size_t need = 0;
+  float* partial;
+  unsigned* tickets;
+  carve_red(nullptr, K, H * W, 4, &partial, &tickets, &need);
+  if (workspace_bytes < need) return PCNN_ECAPACITY;
+  carve_red(workspace, K, H * W, 4, &partial, &tickets, nullptr);
+  hipStream_t st = (hipStream_t)stream;
+  if (hipMemsetAsync(tickets, 0, (size_t)K * sizeof(unsigned), st) != hipSuccess) return PCNN_EHIP;
+  const int HW = H * W, nseg = (HW + kSeg - 1) / kSeg;
+  hipLaunchKernelGGL(k_pose_energy, dim3(nseg, K), dim3(kBlk), 0, st, live, label, obj, pred_vertices, HW, znear,
+                     zfar, poses, partial, tickets, energy);
+  PCNN_CHECK_LAUNCH();
+  return PCNN_OK;
+}
+
+extern "C" size_t pcnn_icp_score_workspace_size(int J, int H, int W) {
+  if (J <= 0 || H <= 0 || W <= 0) return 0;
+  pcnn::Carve cv(nullptr);
+  const int HW = H * W, nseg = (HW + kSeg - 1) / kSeg;
+  cv.take<int32_t>(nseg);
+  cv.take<float4>((size_t)HW);
+  cv.take<float4>((size_t)HW);
+  cv.take<uint8_t>((size_t)J * HW);
+  return cv.off + 256;
+}
+
+extern "C" int pcnn_icp_score(const float* live, const int32_t* label, int obj, const float* vertmap, int H, int W,
+                              const float* hyps, int J, float radius, float* score, int32_t* choose, void* workspace,
+                              size_t workspace_bytes, void* stream) {
+  PCNN_REQUIRE(live && label && vertmap && hyps && score && choose && workspace && J > 0 && J <= 64 && H > 0 &&
+               W > 0);
+  const int HW = H * W, nseg = (HW + kSeg - 1) / kSeg;
+  pcnn::Carve cv(workspace);
+  int32_t* cnt = cv.take<int32_t>(nseg);
+  float4* model = cv.take<float4>((size_t)HW);
+  float4* dpts = cv.take<float4>((size_t)HW);
+  uint8_t* flags = cv.take<uint8_t>((size_t)J * HW);
+  if (workspace_bytes < cv.off) return PCNN_ECAPACITY;
+  hipStream_t st = (hipStream_t)stream;
+  if (hipMemsetAsync(flags, 0, (size_t)J * HW, st) != hipSuccess) return PCNN_EHIP;
+  hipLaunchKernelGGL(k_score_count, dim3(nseg), dim3(kBlk), 0, st, live, label, obj, vertmap, HW, nseg, cnt);
+  hipLaunchKernelGGL(k_score_scatter, dim3(nseg), dim3(kBlk), 0, st, live, label, obj, vertmap, HW, nseg, cnt, model,
+                     dpts);
+  hipLaunchKernelGGL(k_score_nn, dim3((HW + kBlk - 1) / kBlk, J), dim3(kBlk), 0, st, model, dpts, cnt, nseg, hyps,
+                     radius * radius, flags, HW);
+  hipLaunchKernelGGL(k_score_select, dim3(1), dim3(kBlk), 0, st, flags, cnt, nseg, J, HW, score, choose);
+  PCNN_CHECK_LAUNCH();
+  return PCNN_OK;
+}

@@ -1,0 +1,145 @@
+"""Pose refinement on the GPU (csrc/icp.hip through the C-ABI) against the
+oracle restatement (oracle/orc_icp.cpp) of df::icp and solveICP's pieces
+ on the synthetic box scene of refine_scene.py.
+
+Bars: the live vertex map is bit-exact (same float operations); the ICP
+systems, updates, centres and energies are float reductions whose order
+differs (GPU: fixed per-lane / wave / workgroup tree; oracle: double in raster
+order), so they are compared with tolerances written below."""
+import numpy as np
+import pytest
+import torch
+
+from refine_scene import CAMERA, pose_mul, scene
+
+pytestmark = pytest.mark.gpu
+D = torch.device("cuda")
+t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(D)
+
+
+def _live(sc, orc):
+    from posecnn_amd.synthesize import icp as R
+    lv = R.live_vertices(t(sc["live"]["depth"].astype(np.int32)).to(torch.uint16), t(sc["live"]["label"]),
+                         torch.tensor([sc["cls"]], dtype=torch.int32), 10000.0, CAMERA)
+    ref = orc.icp_live_vertices(sc["live"]["depth"], sc["live"]["label"], sc["cls"], 10000.0, CAMERA)
+    return lv, ref
+
+
+def test_live_vertices_bit_exact(hip, orc):
+    sc = scene(0)
+    lv, ref = _live(sc, orc)
+    np.testing.assert_array_equal(lv[0].cpu().numpy(), ref)
+
+
+@pytest.mark.parametrize("iters", [1, 8, 20])
+def test_icp_matches_oracle(hip, orc, iters):
+    from posecnn_amd.synthesize import icp as R
+    sc = scene(1)
+    lv, ref_lv = _live(sc, orc)
+    pv, pn = t(sc["pred"]["pred_v"])[None], t(sc["pred"]["pred_n"])[None]
+    upd, pout, systems = R.icp(lv, pv, pn, CAMERA, max_error=0.05, iterations=iters,
+                               pose_in=t(sc["init"].astype(np.float32))[None], return_systems=True)
+    oupd, osys = orc.icp(ref_lv, sc["pred"]["pred_v"], sc["pred"]["pred_n"], CAMERA, max_error=0.05,
+                         iterations=iters)
+    s = systems[0].cpu().numpy()
+    # iteration 0 sees identical inputs: same pixel set, sums within float
+    # accumulation error (|sum| scale 1e-5 relative)
+    assert s[0, 27] == osys[0, 27]
+    scale = np.abs(osys[0, :27]).max()
+    np.testing.assert_allclose(s[0, :27], osys[0, :27], rtol=1e-4, atol=1e-5 * scale)
+    u = upd[0].cpu().numpy()
+    np.testing.assert_allclose(u, oupd, atol=2e-5 * max(1, iters))
+    np.testing.assert_allclose(pout[0].cpu().numpy(), pose_mul(u.astype(np.float64), sc["init"]), atol=1e-5)
+    if iters == 20:  # converged onto the truth
+        refined = pose_mul(u.astype(np.float64), sc["init"])
+        assert np.linalg.norm(refined[4:] - sc["true"][4:]) < 1.5e-3
+
+
+def test_icp_batched_problems_and_live_index(hip, orc):
+    """N = 3 problems sharing one live map (the 8-hypothesis batch of
+    solveICP:2255-2286 in miniature), one of them with no usable pixel."""
+    from posecnn_amd.synthesize import icp as R
+    scs = [scene(s) for s in (0, 2)]
+    lv, ref_lv = _live(scs[0], orc)
+    far = scs[0]["pred"]["pred_v"].copy()
+    far[..., 2] = 100.0  # every rendered depth outside (znear, zfar): no pixel contributes
+    pv = t(np.stack([scs[0]["pred"]["pred_v"], scs[1]["pred"]["pred_v"], far]))
+    pn = t(np.stack([scs[0]["pred"]["pred_n"], scs[1]["pred"]["pred_n"], scs[0]["pred"]["pred_n"]]))
+    upd, _ = R.icp(lv, pv, pn, CAMERA, max_error=0.05, iterations=8, live_index=torch.zeros(3, dtype=torch.int32))
+    u = upd.cpu().numpy()
+    for k, sc in enumerate(scs):
+        o, _ = orc.icp(ref_lv, sc["pred"]["pred_v"], sc["pred"]["pred_n"], CAMERA, max_error=0.05, iterations=8)
+        np.testing.assert_allclose(u[k], o, atol=2e-4)
+    np.testing.assert_array_equal(u[2], np.array([1, 0, 0, 0, 0, 0, 0], np.float32))
+
+
+def test_icp_center_and_energy(hip, orc):
+    from posecnn_amd.synthesize import icp as R
+    sc = scene(3, perturb_deg=1.0, perturb_t=0.004)
+    lv, ref_lv = _live(sc, orc)
+    p = sc["pred"]
+    lab = t(sc["live"]["label"])
+    init = sc["init"].astype(np.float32)
+    out, pout = R.icp_center(lv, lab, torch.tensor([sc["cls"]]), t(p["vertmap"])[None], t(p["pred_v"])[None],
+                             t(p["pred_n"])[None], max_error=0.02, pose_in=t(init)[None])
+    ref = orc.icp_center(ref_lv, sc["live"]["label"], sc["cls"], p["vertmap"], p["pred_v"], p["pred_n"],
+                         max_error=0.02)
+    o = out[0].cpu().numpy()
+    assert o[3] == ref[3] and ref[3] > 500
+    np.testing.assert_allclose(o[:3], ref[:3], rtol=1e-5, atol=1e-6)
+    po = pout[0].cpu().numpy()
+    np.testing.assert_array_equal(po[:4], init[:4])
+    np.testing.assert_allclose(po[4:], [init[4] / init[6] * o[2], init[5] / init[6] * o[2], o[2]], rtol=1e-6)
+    poses = np.stack([init, sc["true"].astype(np.float32), np.array([1, 0, 0, 0, 0, 0, 0.5], np.float32)])
+    e = R.pose_energy(lv[0], lab, sc["cls"], t(p["pred_v"]), t(poses)).cpu().numpy()
+    eo = orc.pose_energy(ref_lv, sc["live"]["label"], sc["cls"], p["pred_v"], poses)
+    np.testing.assert_allclose(e, eo, rtol=2e-5)
+
+
+def test_icp_score_matches_oracle(hip, orc):
+    """SegICP hypothesis scores: same candidate sets, same float distance
+    arithmetic and tie rule -> identical scores and choice."""
+    from posecnn_amd.synthesize import icp as R
+    sc = scene(4, perturb_deg=2.0, perturb_t=0.006, half=(0.03, 0.025, 0.02))
+    lv, ref_lv = _live(sc, orc)
+    hyps = np.repeat(sc["init"].astype(np.float32)[None], 8, 0)
+    hyps[1:, 6] += np.array([-0.02, -0.01, 0.01, 0.02, 0.03, 0.04, 0.05], np.float32)
+    hyps[3] = sc["true"].astype(np.float32)
+    s, ch = R.icp_score(lv[0], t(sc["live"]["label"]), sc["cls"], t(sc["pred"]["vertmap"]), t(hyps))
+    so, cho = orc.icp_score(ref_lv, sc["live"]["label"], sc["cls"], sc["pred"]["vertmap"], hyps)
+    np.testing.assert_array_equal(s.cpu().numpy(), so)
+    assert int(ch[0]) == cho
+
+
+def test_solve_icp_end_to_end(hip, orc):
+    """The solveICP flow (synthesize.cpp:2052-2395) with the box ray-caster as
+    the renderer: poses_new is the re-centred pose (no Nelder-Mead stage here),
+    poses_icp the SegICP-chosen ICP hypothesis, closer to the truth than the
+    initial pose; a RoI of class 0 and one without enough pixels stay zero."""
+    from posecnn_amd.synthesize import icp as R
+    from refine_scene import render_box
+    sc = scene(5, perturb_deg=2.0, perturb_t=0.01)
+
+    def render(obj, pose):
+        m = render_box(np.asarray(pose, np.float64), sc["half"], obj)
+        return t(m["vertmap"]), t(m["pred_v"]), t(m["pred_n"])
+
+    params = list(CAMERA) + [0.25, 6.0, 10000.0]
+    rois = np.array([[0, sc["cls"], 0, 0, 1, 1], [0, 0, 0, 0, 1, 1], [0, 7, 0, 0, 1, 1]], np.float32)
+    poses = np.stack([sc["init"], sc["init"], sc["init"]]).astype(np.float32)
+    depth = t(sc["live"]["depth"].astype(np.int32)).to(torch.uint16)
+    pnew, picp = R.solve_icp(t(sc["live"]["label"]), depth, params, rois, poses, render, max_error=0.02, nm_evals=0)
+    assert np.all(pnew[1:] == 0) and np.all(picp[1:] == 0)
+    # re-centring step against the oracle
+    ref_lv = orc.icp_live_vertices(sc["live"]["depth"], sc["live"]["label"], sc["cls"], 10000.0, CAMERA)
+    c = orc.icp_center(ref_lv, sc["live"]["label"], sc["cls"], sc["pred"]["vertmap"], sc["pred"]["pred_v"],
+                       sc["pred"]["pred_n"], max_error=0.02)
+    init = sc["init"].astype(np.float32)
+    np.testing.assert_allclose(pnew[0, 4:], [init[4] / init[6] * c[2], init[5] / init[6] * c[2], c[2]], rtol=1e-5)
+    e_icp = np.linalg.norm(picp[0, 4:] - sc["true"][4:])
+    assert e_icp < np.linalg.norm(init[4:] - sc["true"][4:]) and e_icp < 3e-3
+    # with the Nelder-Mead stage the result stays a unit-quaternion pose near the truth
+    pnew2, picp2 = R.solve_icp(t(sc["live"]["label"]), depth, params, rois[:1], poses[:1], render, max_error=0.02,
+                               nm_evals=50)
+    assert abs(np.linalg.norm(picp2[0, :4]) - 1) < 1e-4
+    assert np.linalg.norm(picp2[0, 4:] - sc["true"][4:]) < 5e-3
