@@ -15,13 +15,14 @@
 // transform_reduce of those rows, a device sync and a host-side 6x6 LDLT solve
 // (icp.cpp:51-103).  Here the pixels whose rendered depth lies in the depth
 // range (the only ones icpKernel can use: icp.cu:56-63) are compacted once per
-// problem, in raster order, into dense (vertex, normal) records; one 1024-lane
-// workgroup per problem then runs every Gauss-Newton iteration: J^T J and J^T r
-// accumulate in registers, reduce through the wave and LDS in a fixed order,
-// and one lane solves the 6x6 system (Eigen LDLT with diagonal pivoting),
-// exponentiates the twist (Sophus SE3::exp) and left-multiplies it into the
-// accumulated update, which the next iteration reads from LDS.  No per-pixel
-// Jacobian ever reaches HBM and the host is never involved.
+// problem, in raster order, into dense (vertex, normal) records; then each
+// Gauss-Newton iteration is two launches over all N problems: 8-64
+// workgroups per problem accumulate J^T J and J^T r in registers and reduce
+// them through the wave and the workgroup, and one wave per problem adds the
+// slices in order, solves the 6x6 system (Eigen LDLT with diagonal
+// pivoting), exponentiates the twist (Sophus SE3::exp) and left-multiplies it
+// into the accumulated update that the next iteration reads.  No per-pixel Jacobian ever
+// reaches HBM and the host is never involved.
 //
 // Rendering (the OpenGL vertex / normal / canonical-coordinate maps of the
 // model at a pose, synthesize.cpp:2106-2137) and the NLopt Nelder-Mead pose
@@ -32,7 +33,6 @@ namespace pcnn_refine {
 
 constexpr int kSeg = 2048;       // pixels per compaction / reduction block
 constexpr int kBlk = 256;        // threads of the per-pixel kernels
-constexpr int kIterThreads = 1024;
 constexpr int kSys = 28;         // 21 upper-triangle JTJ + 6 JTr + pixel count
 
 struct Quat { float w, x, y, z; };
@@ -123,56 +123,123 @@ __device__ SE3 se3_exp(const float a[6]) {
 }
 
 // Eigen 3.3 LDLT<Upper> of the symmetric 6x6 system and its solve
-// (diagonal pivoting; zero pivots -> 0 in the pseudo-inverse of D)
-__device__ void ldlt_solve6(float m[36], const float b[6], float x[6]) {
-  int tr[6];
-  float temp[6];
-  for (int k = 0; k < 6; k++) {
-    int big = k;
-    float bv = fabsf(m[k * 6 + k]);
-    for (int i = k + 1; i < 6; i++)
-      if (fabsf(m[i * 6 + i]) > bv) {
-        bv = fabsf(m[i * 6 + i]);
-        big = i;
-      }
-    tr[k] = big;
-    if (big != k) {
-      for (int j = 0; j < k; j++) { const float t = m[k * 6 + j]; m[k * 6 + j] = m[big * 6 + j]; m[big * 6 + j] = t; }
-      for (int i = big + 1; i < 6; i++) { const float t = m[i * 6 + k]; m[i * 6 + k] = m[i * 6 + big]; m[i * 6 + big] = t; }
-      { const float t = m[k * 6 + k]; m[k * 6 + k] = m[big * 6 + big]; m[big * 6 + big] = t; }
-      for (int i = k + 1; i < big; i++) { const float t = m[i * 6 + k]; m[i * 6 + k] = m[big * 6 + i]; m[big * 6 + i] = t; }
+// (diagonal pivoting; zero pivots -> 0 in the pseudo-inverse of D).  Every
+// loop is unrolled so that each matrix index is a compile-time constant and m
+// stays in registers; the data-dependent pivot swaps become selects over the
+// candidate rows.
+template <int K, int BI>
+__device__ __forceinline__ void ldlt_swap(float (&m)[36]) {
+#pragma unroll
+  for (int j = 0; j < K; j++) { const float t = m[K * 6 + j]; m[K * 6 + j] = m[BI * 6 + j]; m[BI * 6 + j] = t; }
+#pragma unroll
+  for (int i = BI + 1; i < 6; i++) { const float t = m[i * 6 + K]; m[i * 6 + K] = m[i * 6 + BI]; m[i * 6 + BI] = t; }
+  { const float t = m[K * 6 + K]; m[K * 6 + K] = m[BI * 6 + BI]; m[BI * 6 + BI] = t; }
+#pragma unroll
+  for (int i = K + 1; i < BI; i++) { const float t = m[i * 6 + K]; m[i * 6 + K] = m[BI * 6 + i]; m[BI * 6 + i] = t; }
+}
+
+template <int K>
+__device__ __forceinline__ void ldlt_pivot(float (&m)[36], int big) {
+  if constexpr (K + 1 < 6) { if (big == K + 1) ldlt_swap<K, K + 1>(m); }
+  if constexpr (K + 2 < 6) { if (big == K + 2) ldlt_swap<K, K + 2>(m); }
+  if constexpr (K + 3 < 6) { if (big == K + 3) ldlt_swap<K, K + 3>(m); }
+  if constexpr (K + 4 < 6) { if (big == K + 4) ldlt_swap<K, K + 4>(m); }
+  if constexpr (K + 5 < 6) { if (big == K + 5) ldlt_swap<K, K + 5>(m); }
+}
+
+// x[k] <-> x[t] for a runtime t >= k
+template <int K>
+__device__ __forceinline__ void swap_x(float (&x)[6], int t) {
+#pragma unroll
+  for (int i = K + 1; i < 6; i++)
+    if (t == i) { const float v = x[K]; x[K] = x[i]; x[i] = v; }
+}
+
+template <int K>
+__device__ __forceinline__ bool ldlt_step(float (&m)[36], int (&tr)[6]) {
+  int big = K;
+  float bv = fabsf(m[K * 6 + K]);
+#pragma unroll
+  for (int i = K + 1; i < 6; i++)
+    if (fabsf(m[i * 6 + i]) > bv) {
+      bv = fabsf(m[i * 6 + i]);
+      big = i;
     }
-    if (k > 0) {
-      for (int j = 0; j < k; j++) temp[j] = m[j * 6 + j] * m[k * 6 + j];
-      float s = 0.f;
-      for (int j = 0; j < k; j++) s = s + m[k * 6 + j] * temp[j];
-      m[k * 6 + k] -= s;
-      for (int i = k + 1; i < 6; i++) {
-        float si = 0.f;
-        for (int j = 0; j < k; j++) si = si + m[i * 6 + j] * temp[j];
-        m[i * 6 + k] -= si;
-      }
+  tr[K] = big;
+  ldlt_pivot<K>(m, big);
+  if constexpr (K > 0) {
+    float temp[K > 0 ? K : 1];
+#pragma unroll
+    for (int j = 0; j < K; j++) temp[j] = m[j * 6 + j] * m[K * 6 + j];
+    float sum = 0.f;
+#pragma unroll
+    for (int j = 0; j < K; j++) sum = sum + m[K * 6 + j] * temp[j];
+    m[K * 6 + K] -= sum;
+#pragma unroll
+    for (int i = K + 1; i < 6; i++) {
+      float si = 0.f;
+#pragma unroll
+      for (int j = 0; j < K; j++) si = si + m[i * 6 + j] * temp[j];
+      m[i * 6 + K] -= si;
     }
-    const float akk = m[k * 6 + k];
-    const bool valid = fabsf(akk) > 0.f;
-    if (k == 0 && !valid) {  // all-zero diagonal: nothing to solve
-      for (int i = 0; i < 6; i++) x[i] = 0.f;
-      return;
-    }
-    if (k < 5 && valid)
-      for (int i = k + 1; i < 6; i++) m[i * 6 + k] /= akk;
   }
+  const float akk = m[K * 6 + K];
+  const bool valid = fabsf(akk) > 0.f;
+  if (K == 0 && !valid) return false;  // all-zero diagonal: nothing to solve
+  if (K < 5 && valid) {
+#pragma unroll
+    for (int i = K + 1; i < 6; i++) m[i * 6 + K] /= akk;
+  }
+  return true;
+}
+
+__device__ void ldlt_solve6(float (&m)[36], const float (&b)[6], float (&x)[6]) {
+  int tr[6];
+  if (!ldlt_step<0>(m, tr)) {
+#pragma unroll
+    for (int i = 0; i < 6; i++) x[i] = 0.f;
+    return;
+  }
+  ldlt_step<1>(m, tr);
+  ldlt_step<2>(m, tr);
+  ldlt_step<3>(m, tr);
+  ldlt_step<4>(m, tr);
+  ldlt_step<5>(m, tr);
+#pragma unroll
   for (int i = 0; i < 6; i++) x[i] = b[i];
-  for (int k = 0; k < 6; k++) { const float t = x[k]; x[k] = x[tr[k]]; x[tr[k]] = t; }
+  swap_x<0>(x, tr[0]); swap_x<1>(x, tr[1]); swap_x<2>(x, tr[2]);
+  swap_x<3>(x, tr[3]); swap_x<4>(x, tr[4]); swap_x<5>(x, tr[5]);
+#pragma unroll
   for (int i = 0; i < 6; i++)
+#pragma unroll
     for (int j = 0; j < i; j++) x[i] -= m[i * 6 + j] * x[j];
+#pragma unroll
   for (int i = 0; i < 6; i++) {
     const float d = m[i * 6 + i];
     x[i] = fabsf(d) > 1.17549435e-38f ? x[i] / d : 0.f;
   }
+#pragma unroll
   for (int i = 5; i >= 0; i--)
+#pragma unroll
     for (int j = i + 1; j < 6; j++) x[i] -= m[j * 6 + i] * x[j];
-  for (int k = 5; k >= 0; k--) { const float t = x[k]; x[k] = x[tr[k]]; x[tr[k]] = t; }
+  swap_x<5>(x, tr[5]); swap_x<4>(x, tr[4]); swap_x<3>(x, tr[3]);
+  swap_x<2>(x, tr[2]); swap_x<1>(x, tr[1]); swap_x<0>(x, tr[0]);
+}
+
+
+// sum of n strided floats in index order, loads issued 8 ahead of the adds
+// (a plain loop waits out one memory latency per term)
+__device__ __forceinline__ float ordered_sum_strided(const float* __restrict__ p, int n, size_t stride) {
+  float sum = 0.f;
+  for (int q0 = 0; q0 < n; q0 += 8) {
+    float v[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) v[k] = q0 + k < n ? p[(size_t)(q0 + k) * stride] : 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+      if (q0 + k < n) sum += v[k];
+  }
+  return sum;
 }
 
 __device__ __forceinline__ bool in_range(float z, float znear, float zfar) { return !(z < znear || z > zfar); }
@@ -281,117 +348,165 @@ __global__ void __launch_bounds__(kBlk) k_icp_scatter(const float* __restrict__ 
   }
 }
 
-// The Gauss-Newton loop of df::icp for one problem per workgroup.
-__global__ void __launch_bounds__(kIterThreads) k_icp_iterate(
+// One Gauss-Newton iteration of df::icp for N problems: grid (split, N),
+// each workgroup accumulates J^T J / J^T r over a strided slice of its
+// problem's records into its slot of `partial`; k_icp_solve then adds the
+// slices in slice order.  The order of every sum is fixed (lane, wave tree,
+// waves, slices): results are run-to-run identical.  (A last-arriver ticket
+// in place of the second launch measured 28 us per iteration at 16 slices
+// and 65 us at 64: each workgroup's device-scope release fence costs more
+// than the launch it saves.)
+constexpr int kIcpSplitMax = 64;  // workgroups per problem (the launcher picks 8..64 by N)
+
+__device__ __forceinline__ SE3 load_se3(const float* p) {
+  SE3 T;
+  T.q = {p[0], p[1], p[2], p[3]};
+  T.t[0] = p[4]; T.t[1] = p[5]; T.t[2] = p[6];
+  return T;
+}
+__device__ __forceinline__ void store_se3(float* p, const SE3& T) {
+  p[0] = T.q.w; p[1] = T.q.x; p[2] = T.q.y; p[3] = T.q.z;
+  p[4] = T.t[0]; p[5] = T.t[1]; p[6] = T.t[2];
+}
+
+__global__ void __launch_bounds__(kBlk) k_icp_step(
     const float4* __restrict__ rec, const int32_t* __restrict__ cnt, int nseg, const float* __restrict__ live,
     const int32_t* __restrict__ live_index, int H, int W, float fx, float fy, float px, float py, float znear,
-    float zfar, float max_error, int iterations, const float* __restrict__ pose_in, float* __restrict__ update,
-    float* __restrict__ pose_out, float* __restrict__ systems) {
-  __shared__ float part[kIterThreads / 64][kSys];
-  __shared__ float sys[kSys];
-  __shared__ SE3 acc_sh;
-  __shared__ int ish[kIterThreads / 64];
-  const int n = blockIdx.x;
+    float zfar, float max_error, int it, int split, const float* __restrict__ acc_pose,
+    float* __restrict__ partial) {
+  __shared__ float part[kBlk / 64][kSys];
+  __shared__ int ish[kBlk / 64];
+  const int n = blockIdx.y, g = blockIdx.x;
   const int HW = H * W;
   int c = 0;
-  for (int s = threadIdx.x; s < nseg; s += kIterThreads) c += cnt[(size_t)n * nseg + s];
-  const int total = block_sum_int<kIterThreads>(c, ish);
+  for (int s = threadIdx.x; s < nseg; s += kBlk) c += cnt[(size_t)n * nseg + s];
+  const int total = block_sum_int<kBlk>(c, ish);
   const float4* rn = rec + (size_t)n * HW * 2;
   const float* lv = live + (size_t)(live_index ? live_index[n] : n) * HW * 3;
-  if (threadIdx.x == 0) {
-    acc_sh.q = {1.f, 0.f, 0.f, 0.f};
-    acc_sh.t[0] = acc_sh.t[1] = acc_sh.t[2] = 0.f;
-  }
-  __syncthreads();
+  const SE3 T = it == 0 ? SE3{{1.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}} : load_se3(acc_pose + (size_t)n * 8);
   const float border = 2.f;
   const float umax = (float)(W - 1) - border, vmax = (float)(H - 1) - border;
   const int wave = threadIdx.x >> 6, lane = pcnn::lane_id();
-  for (int it = 0; it < iterations; it++) {
-    const SE3 T = acc_sh;
-    float a[kSys];
+  float a[kSys];
 #pragma unroll
-    for (int e = 0; e < kSys; e++) a[e] = 0.f;
-    for (int i = threadIdx.x; i < total; i += kIterThreads) {
-      const float4 v = rn[2 * (size_t)i];
-      const float4 nm = rn[2 * (size_t)i + 1];
-      float p0, p1, p2;
-      rotate(T.q, v.x, v.y, v.z, p0, p1, p2);
-      p0 = p0 + T.t[0];
-      p1 = p1 + T.t[1];
-      p2 = p2 + T.t[2];
-      const int u = (int)((p0 / p2) * fx + px + 0.5f);  // v_cvt_i32_f32: NaN -> 0
-      const int vv = (int)((p1 / p2) * fy + py + 0.5f);
-      if ((float)u <= border || (float)u >= umax || (float)vv <= border || (float)vv >= vmax) continue;
-      const float* l3 = lv + ((size_t)vv * W + u) * 3;
-      const float l0 = l3[0], l1 = l3[1], l2 = l3[2];
-      if (l2 < znear || l2 > zfar) continue;
-      const float nr = sqrtf(p0 * p0 + p1 * p1 + p2 * p2);
-      if (-((p0 / nr) * nm.x + (p1 / nr) * nm.y + (p2 / nr) * nm.z) < 0.1f) continue;
-      const float e = nm.x * (l0 - p0) + nm.y * (l1 - p1) + nm.z * (l2 - p2);
-      if (fabsf(e) > max_error) continue;
-      const float w = 1.0f / l2;
-      float J[6];
-      J[0] = w * nm.x;
-      J[1] = w * nm.y;
-      J[2] = w * nm.z;
-      J[3] = w * (nm.z * p1 - nm.y * p2);
-      J[4] = w * (nm.x * p2 - nm.z * p0);
-      J[5] = w * (nm.y * p0 - nm.x * p1);
-      const float r = w * e;
-      int k = 0;
-#pragma unroll
-      for (int ii = 0; ii < 6; ii++)
-#pragma unroll
-        for (int jj = ii; jj < 6; jj++) a[k++] += J[ii] * J[jj];
-#pragma unroll
-      for (int ii = 0; ii < 6; ii++) a[21 + ii] += J[ii] * r;
-      a[27] += 1.f;
-    }
-    // fixed-order reduction: wave butterfly, then the waves in order
-#pragma unroll
-    for (int e = 0; e < kSys; e++) {
-      const float s = pcnn::wave_sum(a[e]);
-      if (lane == 0) part[wave][e] = s;
-    }
-    __syncthreads();
-    if (threadIdx.x < kSys) {
-      float s = 0.f;
-      for (int w = 0; w < kIterThreads / 64; w++) s += part[w][threadIdx.x];
-      sys[threadIdx.x] = s;
-      if (systems) systems[((size_t)n * iterations + it) * kSys + threadIdx.x] = s;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      float m[36], b[6], x[6];
-      int k = 0;
-      for (int i = 0; i < 6; i++)
-        for (int j = i; j < 6; j++) {
-          m[i * 6 + j] = sys[k];
-          m[j * 6 + i] = sys[k];
-          k++;
-        }
-      for (int i = 0; i < 6; i++) b[i] = sys[21 + i];
-      ldlt_solve6(m, b, x);
-      acc_sh = se3_mul(se3_exp(x), T);
-    }
-    __syncthreads();
+  for (int e = 0; e < kSys; e++) a[e] = 0.f;
+  const int stride = split * kBlk;
+  int i = g * kBlk + threadIdx.x;
+  float4 vn = make_float4(0.f, 0.f, 0.f, 0.f), nn = vn;
+  if (i < total) {
+    vn = rn[2 * (size_t)i];
+    nn = rn[2 * (size_t)i + 1];
   }
-  if (threadIdx.x == 0) {
-    const SE3 A = acc_sh;
-    float* u = update + (size_t)n * 7;
-    u[0] = A.q.w; u[1] = A.q.x; u[2] = A.q.y; u[3] = A.q.z;
-    u[4] = A.t[0]; u[5] = A.t[1]; u[6] = A.t[2];
+  for (; i < total; i += stride) {
+    const float4 v = vn, nm = nn;  // the next record is in flight under this one's work
+    if (i + stride < total) {
+      vn = rn[2 * ((size_t)i + stride)];
+      nn = rn[2 * ((size_t)i + stride) + 1];
+    }
+    float p0, p1, p2;
+    rotate(T.q, v.x, v.y, v.z, p0, p1, p2);
+    p0 = p0 + T.t[0];
+    p1 = p1 + T.t[1];
+    p2 = p2 + T.t[2];
+    const int u = (int)((p0 / p2) * fx + px + 0.5f);  // v_cvt_i32_f32: NaN -> 0
+    const int vv = (int)((p1 / p2) * fy + py + 0.5f);
+    if ((float)u <= border || (float)u >= umax || (float)vv <= border || (float)vv >= vmax) continue;
+    const float* l3 = lv + ((size_t)vv * W + u) * 3;
+    const float l0 = l3[0], l1 = l3[1], l2 = l3[2];
+    if (l2 < znear || l2 > zfar) continue;
+    const float nr = sqrtf(p0 * p0 + p1 * p1 + p2 * p2);
+    if (-((p0 / nr) * nm.x + (p1 / nr) * nm.y + (p2 / nr) * nm.z) < 0.1f) continue;
+    const float e = nm.x * (l0 - p0) + nm.y * (l1 - p1) + nm.z * (l2 - p2);
+    if (fabsf(e) > max_error) continue;
+    const float w = 1.0f / l2;
+    float J[6];
+    J[0] = w * nm.x;
+    J[1] = w * nm.y;
+    J[2] = w * nm.z;
+    J[3] = w * (nm.z * p1 - nm.y * p2);
+    J[4] = w * (nm.x * p2 - nm.z * p0);
+    J[5] = w * (nm.y * p0 - nm.x * p1);
+    const float r = w * e;
+    int k = 0;
+#pragma unroll
+    for (int ii = 0; ii < 6; ii++)
+#pragma unroll
+      for (int jj = ii; jj < 6; jj++) a[k++] += J[ii] * J[jj];
+#pragma unroll
+    for (int ii = 0; ii < 6; ii++) a[21 + ii] += J[ii] * r;
+    a[27] += 1.f;
+  }
+#pragma unroll
+  for (int e = 0; e < kSys; e++) {
+    const float sum = pcnn::wave_sum(a[e]);
+    if (lane == 0) part[wave][e] = sum;
+  }
+  __syncthreads();
+  if (threadIdx.x < kSys) {
+    float sum = 0.f;
+    for (int w = 0; w < kBlk / 64; w++) sum += part[w][threadIdx.x];
+    partial[((size_t)n * kIcpSplitMax + g) * kSys + threadIdx.x] = sum;
+  }
+}
+
+// The iteration's solve, one wave per problem (the launch boundary orders it
+// after every slice): the slices added in order, the 6x6 LDLT, exp(x)
+// left-multiplied into the accumulated update.
+__global__ void __launch_bounds__(64) k_icp_solve(int it, int iterations, int split, float* __restrict__ acc_pose,
+                                                  const float* __restrict__ partial, const float* __restrict__ pose_in,
+                                                  float* __restrict__ update, float* __restrict__ pose_out,
+                                                  float* __restrict__ systems) {
+  __shared__ float sys[kSys];
+  const int n = blockIdx.x;
+  if (threadIdx.x < kSys) {
+    float sum = 0.f;
+    sum = ordered_sum_strided(partial + (size_t)n * kIcpSplitMax * kSys + threadIdx.x, split, kSys);
+    sys[threadIdx.x] = sum;
+    if (systems) systems[((size_t)n * iterations + it) * kSys + threadIdx.x] = sum;
+  }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  const SE3 T = it == 0 ? SE3{{1.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}} : load_se3(acc_pose + (size_t)n * 8);
+  float m[36], b[6], x[6];
+  int k = 0;
+#pragma unroll
+  for (int i = 0; i < 6; i++)
+#pragma unroll
+    for (int j = i; j < 6; j++) {
+      m[i * 6 + j] = sys[k];
+      m[j * 6 + i] = sys[k];
+      k++;
+    }
+#pragma unroll
+  for (int i = 0; i < 6; i++) b[i] = sys[21 + i];
+  ldlt_solve6(m, b, x);
+  const SE3 A = se3_mul(se3_exp(x), T);
+  store_se3(acc_pose + (size_t)n * 8, A);
+  if (it == iterations - 1) {
+    store_se3(update + (size_t)n * 7, A);
     if (pose_in && pose_out) {  // refinePose: T_co = update * T_co (synthesize.cpp:2023-2025)
       const float* P = pose_in + (size_t)n * 7;
       const float qn = sqrtf(P[0] * P[0] + P[1] * P[1] + P[2] * P[2] + P[3] * P[3]);
       SE3 B;
       B.q = {P[0] / qn, P[1] / qn, P[2] / qn, P[3] / qn};
       B.t[0] = P[4]; B.t[1] = P[5]; B.t[2] = P[6];
-      const SE3 R = se3_mul(A, B);
-      float* o = pose_out + (size_t)n * 7;
-      o[0] = R.q.w; o[1] = R.q.x; o[2] = R.q.y; o[3] = R.q.z;
-      o[4] = R.t[0]; o[5] = R.t[1]; o[6] = R.t[2];
+      store_se3(pose_out + (size_t)n * 7, se3_mul(A, B));
     }
+  }
+}
+
+// iterations == 0: the identity update (and pose_out = pose_in, normalised)
+__global__ void k_icp_identity(int N, const float* __restrict__ pose_in, float* __restrict__ update,
+                               float* __restrict__ pose_out) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  store_se3(update + (size_t)n * 7, SE3{{1.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}});
+  if (pose_in && pose_out) {
+    const float* P = pose_in + (size_t)n * 7;
+    const float qn = sqrtf(P[0] * P[0] + P[1] * P[1] + P[2] * P[2] + P[3] * P[3]);
+    float* o = pose_out + (size_t)n * 7;
+    o[0] = P[0] / qn; o[1] = P[1] / qn; o[2] = P[2] / qn; o[3] = P[3] / qn;
+    o[4] = P[4]; o[5] = P[5]; o[6] = P[6];
   }
 }
 
@@ -420,7 +535,7 @@ __device__ __forceinline__ bool finish_partials(const float (&v)[NV], float* par
   __threadfence();
   if (threadIdx.x < NV) {  // totals -> sh[0, NV)
     float s = 0.f;
-    for (int b = 0; b < nblk; b++) s += __builtin_nontemporal_load(partial + (size_t)b * NV + threadIdx.x);
+    s = ordered_sum_strided(partial + threadIdx.x, nblk, NV);
     sh[threadIdx.x] = s;
   }
   if (threadIdx.x == 0) *ticket = 0u;
@@ -661,12 +776,16 @@ __global__ void __launch_bounds__(kBlk) k_score_select(const uint8_t* __restrict
 struct IcpWs {
   int32_t* cnt;
   float4* rec;
+  float* acc;         // [N][8] accumulated update
+  float* partial;     // [N][kIcpSplitMax][kSys]
 };
 
 inline IcpWs carve_icp(void* base, int N, int HW, size_t* bytes) {
   pcnn::Carve cv(base);
   IcpWs ws;
   const int nseg = (HW + kSeg - 1) / kSeg;
+  ws.acc = cv.take<float>((size_t)N * 8);
+  ws.partial = cv.take<float>((size_t)N * kIcpSplitMax * kSys);
   ws.cnt = cv.take<int32_t>((size_t)N * nseg);
   ws.rec = cv.take<float4>((size_t)N * HW * 2);
   if (bytes) *bytes = cv.off;
@@ -720,8 +839,16 @@ extern "C" int pcnn_icp(const float* live, const int32_t* live_index, const floa
   hipLaunchKernelGGL(k_icp_count, dim3(nseg, N), dim3(kBlk), 0, st, pred_vertices, HW, znear, zfar, nseg, ws.cnt);
   hipLaunchKernelGGL(k_icp_scatter, dim3(nseg, N), dim3(kBlk), 0, st, pred_vertices, pred_normals, HW, znear, zfar,
                      nseg, ws.cnt, ws.rec);
-  hipLaunchKernelGGL(k_icp_iterate, dim3(N), dim3(kIterThreads), 0, st, ws.rec, ws.cnt, nseg, live, live_index, H, W,
-                     fx, fy, px, py, znear, zfar, max_error, iterations, pose_in, update, pose_out, systems);
+  if (iterations == 0)
+    hipLaunchKernelGGL(k_icp_identity, dim3((N + 63) / 64), dim3(64), 0, st, N, pose_in, update, pose_out);
+  // about 512+ workgroups per launch: 1-2 records per lane for the usual footprints
+  const int split = N >= 64 ? 8 : (512 / N > kIcpSplitMax ? kIcpSplitMax : (512 / N < 8 ? 8 : 512 / N));
+  for (int it = 0; it < iterations; it++) {
+    hipLaunchKernelGGL(k_icp_step, dim3(split, N), dim3(kBlk), 0, st, ws.rec, ws.cnt, nseg, live, live_index, H, W,
+                       fx, fy, px, py, znear, zfar, max_error, it, split, ws.acc, ws.partial);
+    hipLaunchKernelGGL(k_icp_solve, dim3(N), dim3(64), 0, st, it, iterations, split, ws.acc, ws.partial, pose_in,
+                       update, pose_out, systems);
+  }
   PCNN_CHECK_LAUNCH();
   return PCNN_OK;
 }

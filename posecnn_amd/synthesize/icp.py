@@ -25,9 +25,9 @@ def _f(t):
 
 def live_vertices(depth, label, obj_ids, factor, camera, stream=None):
     """df::backproject of the depth masked to each object (synthesize.cpp:2140-2160)."""
-    _lib.require_gpu(depth, label, obj_ids)
+    _lib.require_gpu(depth, label)
     H, W = depth.shape[-2:]
-    obj = obj_ids.to(torch.int32).contiguous()
+    obj = torch.as_tensor(obj_ids).to(device=depth.device, dtype=torch.int32).contiguous()
     L = obj.numel()
     out = torch.empty((L, H, W, 3), dtype=torch.float32, device=depth.device)
     fx, fy, px, py = (float(c) for c in camera)
@@ -49,9 +49,12 @@ def icp(live, pred_vertices, pred_normals, camera, depth_range=(0.25, 6.0), max_
         raise ValueError("icp: pred maps (N,H,W,4), live (L,H,W,3)")
     li = None
     if live_index is not None:
-        li = live_index.to(device=pv.device, dtype=torch.int32).contiguous()
-        if li.numel() != N or int(li.min()) < 0 or int(li.max()) >= lv.shape[0]:
+        if li_host := not live_index.is_cuda:  # validated on the host; a device index is trusted (no sync)
+            if live_index.numel() != N or int(live_index.min()) < 0 or int(live_index.max()) >= lv.shape[0]:
+                raise ValueError("icp: live_index must map each problem to a live map")
+        elif live_index.numel() != N:
             raise ValueError("icp: live_index must map each problem to a live map")
+        li = live_index.to(device=pv.device, dtype=torch.int32).contiguous()
     elif lv.shape[0] != N:
         raise ValueError("icp: one live map per problem, or a live_index")
     dev = pv.device
@@ -77,7 +80,7 @@ def icp_center(live, label, obj_ids, vertmap, pred_vertices, pred_normals, max_e
     _lib.require_gpu(live, label, vertmap, pred_vertices, pred_normals)
     lv, vm, pv, pn = _f(live), _f(vertmap), _f(pred_vertices), _f(pred_normals)
     L_, H, W = lv.shape[0], lv.shape[1], lv.shape[2]
-    obj = obj_ids.to(device=lv.device, dtype=torch.int32).contiguous()
+    obj = torch.as_tensor(obj_ids).to(device=lv.device, dtype=torch.int32).contiguous()
     if obj.numel() != L_ or vm.shape != (L_, H, W, 3) or pv.shape != (L_, H, W, 4) or pn.shape != (L_, H, W, 4):
         raise ValueError("icp_center: live (L,H,W,3), vertmap (L,H,W,3), pred maps (L,H,W,4), obj_ids (L)")
     dev = lv.device

@@ -28,7 +28,7 @@ lab = t(sc["live"]["label"])
 obj = torch.tensor([sc["cls"]], dtype=torch.int32)
 pv = t(np.repeat(sc["pred"]["pred_v"][None], a.n, 0))
 pn = t(np.repeat(sc["pred"]["pred_n"][None], a.n, 0))
-li = torch.zeros(a.n, dtype=torch.int32)
+li = torch.zeros(a.n, dtype=torch.int32, device=D)
 lv = R.live_vertices(depth, lab, obj, 10000.0, CAMERA)
 
 

@@ -59,6 +59,49 @@ class _HostStaged:
         return self._ret(async_op)
 
 
+class _Work:
+    """Async handle of _HostStagedAsync: the gloo op runs on host copies; the
+    device tensor receives the result only in wait(), as an H2D copy enqueued
+    on the waiter's current stream -- a step that reads a collective's output
+    before waiting on its handle reads stale data and fails the comparison."""
+
+    def __init__(self, work, finish):
+        self.work, self.finish = work, finish
+
+    def wait(self):
+        self.work.wait()
+        self.finish()
+
+
+class _HostStagedAsync(_HostStaged):
+    """gloo collectives with real async work handles and no device-wide sync:
+    the D2H copy of the input orders only against the current stream, the
+    collective itself runs asynchronously, and the result lands at wait()."""
+
+    def _go(self, fn, dst, h, async_op):
+        work = fn()
+        finish = lambda: dst.copy_(h, non_blocking=False)
+        if not async_op:
+            work.wait()
+            finish()
+            return None
+        return _Work(work, finish)
+
+    def all_reduce(self, t, async_op=False):
+        h = t.cpu()
+        return self._go(lambda: self.d.all_reduce(h, async_op=True), t, h, async_op)
+
+    def all_gather_into_tensor(self, out, inp, async_op=False):
+        h = torch.empty(out.shape, dtype=out.dtype)
+        src = inp.cpu()
+        return self._go(lambda: self.d.all_gather_into_tensor(h, src, async_op=True), out, h, async_op)
+
+    def all_to_all_single(self, out, inp, async_op=False):
+        h = torch.empty(out.shape, dtype=out.dtype)
+        src = inp.contiguous().cpu()
+        return self._go(lambda: self.d.all_to_all_single(h, src, async_op=True), out, h, async_op)
+
+
 def _inputs(world):
     from posecnn_amd import synth
     fr = synth.make_frames(B_RANK * world, H=H, W=W, num_classes=C, objects_per_image=4, seed=77)
@@ -90,14 +133,15 @@ def _run(fr, sl, global_batch, batch_base, d):
     return out
 
 
-def _worker(rank, world, port, out_dir):
+def _worker(rank, world, port, out_dir, mode="sync"):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         fr = _inputs(world)
-        o = _run(fr, slice(rank * B_RANK, (rank + 1) * B_RANK), B_RANK * world, rank * B_RANK, _HostStaged(dist))
+        wrap = _HostStagedAsync(dist) if mode == "async" else _HostStaged(dist)
+        o = _run(fr, slice(rank * B_RANK, (rank + 1) * B_RANK), B_RANK * world, rank * B_RANK, wrap)
         np.savez(os.path.join(out_dir, f"rank{rank}.npz"), **o)
         dist.barrier()
     finally:
@@ -112,9 +156,14 @@ def _free_port():
     return p
 
 
-def test_sharded_step_matches_single_device(hip, tmp_path):
+@pytest.mark.parametrize("mode", ["sync", "async"])
+def test_sharded_step_matches_single_device(hip, tmp_path, mode):
+    """mode "async": the collectives return real async handles whose results
+    land only at wait(), so the step's wait placement (loss, rows, weight
+    gradient shards, reused exchange buffers across two steps) is exercised;
+    RCCL's own stream ordering stays unpinned until a multi-GPU run."""
     world = 2
-    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), mode), nprocs=world, join=True)
     fr = _inputs(world)
     ref = _run(fr, slice(0, B_RANK * world), B_RANK * world, 0, None)
     ranks = [dict(np.load(tmp_path / f"rank{r}.npz")) for r in range(world)]
