@@ -50,9 +50,8 @@ struct HoughWs {
   float4* vcone;      // [B][VCAP] row-bound slopes (outer s1, s2, inner s1, s2), |s| <= 1e30
   int32_t* vcode;     // [B][VCAP] bound codes | kSlowVoter | kDeadVoter
   unsigned long long* key;  // [B][C] argmax key per slot
-  int32_t* rowstart;  // [B][C][H+1] per slot: first voter (slot-relative) with row >= r
+  int32_t* rowcnt;    // [B][C][H] per slot: sampled voters in row y (the list is raster-ordered)
   int32_t* kmax;      // [B][C] per slot: largest box radius of its voters
-  int32_t* yspan;     // [B][C][2] per slot: rows of its first and last voter (rowstart valid in between)
   float* peak;        // [B][PKS][8] count, distance, 2bb_h, 2bb_w, cx, cy, slot
   int32_t* counts;    // [B][C-1][H*W] (NMS path)
   int32_t* ncand;     // [B]
@@ -83,9 +82,8 @@ inline HoughWs carve_ws(void* base, int B, int H, int W, int C, int skip, bool n
   ws.vcone = cv.take<float4>((size_t)B * ws.vcap);
   ws.vcode = cv.take<int32_t>((size_t)B * ws.vcap);
   ws.key = cv.take<unsigned long long>((size_t)B * C);
-  ws.rowstart = cv.take<int32_t>((size_t)B * C * (H + 1));
+  ws.rowcnt = cv.take<int32_t>((size_t)B * C * H);
   ws.kmax = cv.take<int32_t>((size_t)B * C);
-  ws.yspan = cv.take<int32_t>((size_t)B * C * 2);
   ws.peak = cv.take<float>((size_t)B * ws.pks * 8);
   ws.ncand = cv.take<int32_t>(B);
   if (nms) {
@@ -375,13 +373,12 @@ __device__ __forceinline__ int wave_argmax_rows(const float* __restrict__ img, i
 
 // ---------------------------------------------------------------------------
 // kernels (defined in the TUs listed above)
-__global__ void k_label_hist(const int32_t* __restrict__ label, int HW, int C, HoughWs ws);
+__global__ void k_label_hist(const int32_t* __restrict__ label, int HW, int C, int H, HoughWs ws);
 __global__ void k_label_hist_prob(const float* __restrict__ prob, int32_t* __restrict__ label_out, int HW, int C,
-                                  HoughWs ws);
-__global__ void k_label_scan(int C, int label_thr, int index_size, int nms, int skip, HoughWs ws);
-__global__ void k_label_scatter(const int32_t* __restrict__ label, const float* __restrict__ vertex, int vch,
-                                const float* __restrict__ extents, const float* __restrict__ meta, int num_meta,
-                                int H, int W, int C, int skip, HoughWs ws);
+                                  int H, HoughWs ws);
+__global__ void k_label_place(const int32_t* __restrict__ label, const float* __restrict__ vertex, int vch,
+                              const float* __restrict__ extents, const float* __restrict__ meta, int num_meta, int H,
+                              int W, int C, int skip, int label_thr, int index_size, int nms, HoughWs ws);
 __global__ void k_voter_setup(int H, int W, int C, float inlier, double so, double si, HoughWs ws);
 __global__ void k_hough_vote(int H, int W, int C, float inlier, HoughWs ws, int32_t* __restrict__ counts_out);
 __global__ void k_hough_peak(int B, int H, int W, int C, float inlier, const float* __restrict__ extents,

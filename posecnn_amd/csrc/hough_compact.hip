@@ -15,11 +15,26 @@
 
 namespace pcnn_hough {
 
+// Per-call accumulators zeroed by the histogram kernels, which precede every
+// atomic on them: the argmax keys, the slots' largest box radius and the
+// per-(slot, row) sampled-voter counts.
+__device__ __forceinline__ void zero_accumulators(int b, int blk, int nblk, int C, int H, HoughWs ws) {
+  const int n = C * H;
+  int32_t* rc = ws.rowcnt + (size_t)b * n;
+  for (int i = blk * (int)blockDim.x + (int)threadIdx.x; i < n; i += nblk * (int)blockDim.x) rc[i] = 0;
+  if (blk == 0)
+    for (int c = threadIdx.x; c < C; c += blockDim.x) {
+      ws.key[(size_t)b * C + c] = 0ull;
+      ws.kmax[(size_t)b * C + c] = -1;
+    }
+}
+
 __global__ void __launch_bounds__(kCompactThreads) k_label_hist(const int32_t* __restrict__ label, int HW, int C,
-                                                                 HoughWs ws) {
+                                                                 int H, HoughWs ws) {
   __shared__ int h[kMaxClasses];
   const int b = blockIdx.y, blk = blockIdx.x;
   for (int i = threadIdx.x; i < C; i += blockDim.x) h[i] = 0;
+  zero_accumulators(b, blk, ws.nblk, C, H, ws);
   __syncthreads();
   const int32_t* lab = label + (size_t)b * HW;
   const int base = blk * kPixPerBlk;
@@ -38,16 +53,17 @@ __global__ void __launch_bounds__(kCompactThreads) k_label_hist(const int32_t* _
 // k_label_hist with the label producer fused in: the
 // block's pixels are labelled by argmax over prob_normalized (argmax_2d,
 // network.py:433-434) as they are counted, and label_2d is written once for
-// k_label_scatter (and the caller).  One pass over the (B,H,W,C) prob map
+// k_label_place (and the caller).  One pass over the (B,H,W,C) prob map
 // replaces the argmax pass + label write + label re-read of the unfused graph.
 // Dynamic LDS: kCompactThreads/64 waves x 64 px x C floats when C is staged.
 __global__ void __launch_bounds__(kCompactThreads) k_label_hist_prob(const float* __restrict__ prob,
                                                                       int32_t* __restrict__ label_out, int HW,
-                                                                      int C, HoughWs ws) {
+                                                                      int C, int H, HoughWs ws) {
   extern __shared__ __attribute__((aligned(16))) float stage_all[];
   __shared__ int h[kMaxClasses];
   const int b = blockIdx.y, blk = blockIdx.x;
   for (int i = threadIdx.x; i < C; i += blockDim.x) h[i] = 0;
+  zero_accumulators(b, blk, ws.nblk, C, H, ws);
   const float* img = prob + (size_t)b * HW * C;
   float* stage = stage_all + (threadIdx.x >> 6) * 64 * (C <= kArgmaxStagedMaxC ? C : 0);
   const int base = blk * kPixPerBlk;
@@ -63,81 +79,6 @@ __global__ void __launch_bounds__(kCompactThreads) k_label_hist_prob(const float
   }
   __syncthreads();
   for (int i = threadIdx.x; i < C; i += blockDim.x) ws.blk[((size_t)b * ws.nblk + blk) * C + i] = h[i];
-}
-
-constexpr int kScanLds = 16384;
-
-// Exclusive scan of the block histograms per class, present-class selection
-// (class c >= 1 with > label_thr pixels, cu.cc:654-664) and voter offsets.
-__global__ void __launch_bounds__(1024) k_label_scan(int C, int label_thr, int index_size, int nms, int skip,
-                                                      HoughWs ws) {
-  __shared__ int tile[kScanLds];
-  __shared__ int tot[kMaxClasses];
-  const int b = blockIdx.x;
-  const int n = ws.nblk * C;
-  int32_t* hb = ws.blk + (size_t)b * n;
-  const int lane = pcnn::lane_id(), wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  if (n <= kScanLds) {
-    for (int i = threadIdx.x; i < n; i += blockDim.x) tile[i] = hb[i];
-    __syncthreads();
-    for (int c = wave; c < C; c += nw) {
-      int run = 0;
-      for (int k0 = 0; k0 < ws.nblk; k0 += 64) {
-        const int k = k0 + lane;
-        const int v = k < ws.nblk ? tile[k * C + c] : 0;
-        int incl = v;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-          int t = __shfl_up(incl, o, 64);
-          if (lane >= o) incl += t;
-        }
-        if (k < ws.nblk) tile[k * C + c] = run + incl - v;
-        run += __shfl(incl, 63, 64);
-      }
-      if (lane == 0) tot[c] = run;
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < n; i += blockDim.x) hb[i] = tile[i];
-  } else {
-    for (int c = threadIdx.x; c < C; c += blockDim.x) {
-      int run = 0;
-      for (int k = 0; k < ws.nblk; k++) {
-        int v = hb[(size_t)k * C + c];
-        hb[(size_t)k * C + c] = run;
-        run += v;
-      }
-      tot[c] = run;
-    }
-    __syncthreads();
-  }
-  for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    ws.total[(size_t)b * C + c] = tot[c];
-    ws.key[(size_t)b * C + c] = 0ull;
-    ws.kmax[(size_t)b * C + c] = -1;
-    ws.vcount[(size_t)b * C + c] = 0;
-    ws.vbase[(size_t)b * C + c] = 0;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    if (b == 0)
-      for (int i = 0; i < 4; i++) ws.diag[i] = 0;  // self-check counters of this call (pcnn_hough_voting_diag)
-    int count = 0;
-    for (int c = 1; c < C; c++)
-      if (tot[c] > label_thr) ws.slot_cls[(size_t)b * C + count++] = c;
-    int nvote = nms ? count : (count < index_size ? count : index_size);  // cu.cc:775-776
-    ws.nslots[b] = count;
-    ws.nvote[b] = nvote;
-    ws.ncand[b] = 0;
-    int vb = 0;
-    for (int s = 0; s < nvote; s++) {
-      int c = ws.slot_cls[(size_t)b * C + s];
-      int nv = (tot[c] + skip - 1) / skip;
-      ws.vbase[(size_t)b * C + c] = vb;
-      ws.vcount[(size_t)b * C + c] = nv;
-      vb += nv;
-    }
-    ws.nvtot[b] = vb;
-  }
 }
 
 // Row-bound setup of one cone (threshold cc, ss = sqrt(1 - cc^2)): the cone is
@@ -161,44 +102,146 @@ __device__ __forceinline__ void bound_setup(double ex, double ey, double cc, dou
   else c2 = qx > 0.0 ? kNeedNegDy : kNeedPosDy;
 }
 
+// Cone row-bound slopes and code of one voter (u, v, d, T): the outer / inner
+// cone at the inlier threshold -/+ kConeEps (so / si = sqrt(1 - c^2) of each);
+// returns the box radius k (-1: votes for no cell).
+__device__ __forceinline__ int voter_cone(float4 q, float inlier, double so, double si, float4& cone, int& code) {
+  const double c = (double)inlier;
+  const bool fast_ok = c > 0.05 && c < 0.999;
+  const float u = q.x, v = q.y;
+  const float n1f = sqrtf(u * u + v * v);
+  double sl[4] = {0.0, 0.0, 0.0, 0.0};
+  const int k = box_radius(q.w);
+  code = 0;
+  if (k < 0) {
+    code = kDeadVoter;
+  } else if (!fast_ok || !(n1f >= 1e-18f && n1f <= 1e18f)) {
+    code = kSlowVoter;
+  } else {
+    const double ud = u, vd = v;
+    const double nd = sqrt(ud * ud + vd * vd);
+    const double ex = ud / nd, ey = vd / nd;
+    int c0, c1, c2, c3;
+    bound_setup(ex, ey, c - kConeEps, so, sl[0], c0, sl[1], c1);  // outer cone
+    bound_setup(ex, ey, c + kConeEps, si, sl[2], c2, sl[3], c3);  // inner cone
+    code = c0 | (c1 << 2) | (c2 << 4) | (c3 << 6);
+  }
+  // slopes are evaluated in float per row (hough_vote.hip): the float error
+  // of an interval end is <= ~2.6% of the +-kConeEps margin in x there
+  auto cl = [](double x) { return (float)(x > 1e30 ? 1e30 : (x < -1e30 ? -1e30 : x)); };
+  cone = make_float4(cl(sl[0]), cl(sl[1]), cl(sl[2]), cl(sl[3]));
+  return k;
+}
+
 // vch = channels per vertex pixel: 3C (the reference's (B,H,W,3C) map, a
 // voter reads its class's channels 3l..3l+2) or 3 (the class-compact map of
 // the pixel's own class only).
-__global__ void __launch_bounds__(kCompactThreads) k_label_scatter(const int32_t* __restrict__ label,
-                                                                    const float* __restrict__ vertex, int vch,
-                                                                    const float* __restrict__ extents,
-                                                                    const float* __restrict__ meta, int num_meta,
-                                                                    int H, int W, int C, int skip, HoughWs ws) {
+//
+// One pass per (pixel block, image) after the histograms: the block's
+// exclusive offsets and the class totals from the block histograms (every
+// block reads them; no separate scan launch), the present-class selection
+// (class c >= 1 with > label_thr pixels, cu.cc:654-664; the first index_size
+// vote, cu.cc:775-776) and the voter-list offsets in LDS -- block 0 publishes
+// them for the later kernels -- then the ranked scatter of the sampled voters
+// (list positions 0, skip, 2 skip, ...: cu.cc:269) with each voter's record
+// (u, v, d = exp(z), T(d)).  (The per-voter cone setup stays a dense pass of
+// its own: inline here, one lane in ten of a wave runs the double-precision
+// setup, 25.9 -> 35.2 us at B = 1.)
+__global__ void __launch_bounds__(kCompactThreads) k_label_place(
+    const int32_t* __restrict__ label, const float* __restrict__ vertex, int vch, const float* __restrict__ extents,
+    const float* __restrict__ meta, int num_meta, int H, int W, int C, int skip, int label_thr, int index_size,
+    int nms, HoughWs ws) {
   __shared__ int run[kMaxClasses];
-  __shared__ int vc[kMaxClasses];
+  __shared__ int tot[kMaxClasses];
+  __shared__ int vbl[kMaxClasses], vcl[kMaxClasses], slot_of[kMaxClasses], scls[kMaxClasses];
+  __shared__ int pe[kCompactThreads], pa[kCompactThreads];
   __shared__ int wcnt[kCompactThreads / 64][kMaxClasses];
-  const int b = blockIdx.y, blk = blockIdx.x;
+  __shared__ int s_nvote, s_count;
+  const int b = blockIdx.y, blk = blockIdx.x, nblk = ws.nblk;
   const int HW = H * W;
-  const int wave = threadIdx.x >> 6;
-  for (int i = threadIdx.x; i < C; i += blockDim.x) {
-    run[i] = ws.blk[((size_t)b * ws.nblk + blk) * C + i];
-    vc[i] = ws.vcount[(size_t)b * C + i];
+  const int wave = threadIdx.x >> 6, t = threadIdx.x;
+  // 1. exclusive offsets of this block and class totals (G interleaved partial sums per class)
+  const int G = kCompactThreads / C > 0 ? kCompactThreads / C : 1;
+  if (t < G * C) {
+    const int c = t % C, g = t / C;
+    int e = 0, a = 0;
+    for (int k = g; k < nblk; k += G) {
+      const int v = ws.blk[((size_t)b * nblk + k) * C + c];
+      a += v;
+      e += k < blk ? v : 0;
+    }
+    pe[t] = e;
+    pa[t] = a;
   }
+  __syncthreads();
+  for (int c = t; c < C; c += blockDim.x) {
+    int e = 0, a = 0;
+    for (int g = 0; g < G; g++) {
+      e += pe[g * C + c];
+      a += pa[g * C + c];
+    }
+    run[c] = e;
+    tot[c] = a;
+    vbl[c] = 0;
+    vcl[c] = 0;
+    slot_of[c] = -1;
+  }
+  __syncthreads();
+  // 2. slot table
+  if (t == 0) {
+    int count = 0;
+    for (int c = 1; c < C; c++)
+      if (tot[c] > label_thr) scls[count++] = c;
+    const int nvote = nms ? count : (count < index_size ? count : index_size);
+    int vb = 0;
+    for (int sl = 0; sl < nvote; sl++) {
+      const int c = scls[sl];
+      const int nv = (tot[c] + skip - 1) / skip;
+      vbl[c] = vb;
+      vcl[c] = nv;
+      slot_of[c] = sl;
+      vb += nv;
+    }
+    s_nvote = nvote;
+    s_count = count;
+    if (blk == 0) {
+      if (b == 0)
+        for (int i = 0; i < 4; i++) ws.diag[i] = 0;  // self-check counters of this call (pcnn_hough_voting_diag)
+      ws.nslots[b] = count;
+      ws.nvote[b] = nvote;
+      ws.ncand[b] = 0;
+      ws.nvtot[b] = vb;
+    }
+  }
+  __syncthreads();
+  if (blk == 0)
+    for (int c = t; c < C; c += blockDim.x) {
+      ws.total[(size_t)b * C + c] = tot[c];
+      ws.vbase[(size_t)b * C + c] = vbl[c];
+      ws.vcount[(size_t)b * C + c] = vcl[c];
+    }
+  if (blk == 0)
+    for (int sl = t; sl < s_count; sl += blockDim.x) ws.slot_cls[(size_t)b * C + sl] = scls[sl];
+  // 3. ranked scatter + voter setup
   const int32_t* lab = label + (size_t)b * HW;
   const float* mb = meta + (size_t)b * num_meta;
   const int base = blk * kPixPerBlk;
-  __syncthreads();
   for (int r = 0; r < kPixPerBlk / kCompactThreads; r++) {
     for (int i = pcnn::lane_id(); i < C; i += 64) wcnt[wave][i] = 0;
-    int p = base + r * kCompactThreads + threadIdx.x;
-    int l = p < HW ? lab[p] : -1;
-    bool valid = p < HW && l > 0 && l < C;
+    const int p = base + r * kCompactThreads + t;
+    const int l = p < HW ? lab[p] : -1;
+    const bool valid = p < HW && l > 0 && l < C;
     int rank_w = 0;
     for_each_label_group(l, valid, [&](int l0, uint64_t m) {
       if (l == l0 && valid) rank_w = __popcll(m & pcnn::lanemask_lt());
       if (pcnn::lane_id() == __ffsll((long long)m) - 1) wcnt[wave][l0] = __popcll(m);
     });
     __syncthreads();
-    if (valid && vc[l] > 0) {
+    if (valid && vcl[l] > 0) {
       int rank = run[l] + rank_w;
       for (int w = 0; w < wave; w++) rank += wcnt[w][l];
       if (rank % skip == 0) {  // list positions 0, skip, 2 skip, ... (cu.cc:269)
-        const size_t vi = (size_t)b * ws.vcap + ws.vbase[(size_t)b * C + l] + rank / skip;
+        const size_t vi = (size_t)b * ws.vcap + vbl[l] + rank / skip;
         const size_t off = ((size_t)b * HW + p) * (size_t)vch + (vch == 3 ? 0 : 3 * l);
         const float u = vertex[off], v = vertex[off + 1];
         const float d = (float)exp((double)vertex[off + 2]);  // cu.cc:280
@@ -208,90 +251,52 @@ __global__ void __launch_bounds__(kCompactThreads) k_label_scatter(const int32_t
       }
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < C; i += blockDim.x) {
-      int s = 0;
-      for (int w = 0; w < kCompactThreads / 64; w++) s += wcnt[w][i];
-      run[i] += s;
+    for (int i = t; i < C; i += blockDim.x) {
+      int sum = 0;
+      for (int w = 0; w < kCompactThreads / 64; w++) sum += wcnt[w][i];
+      run[i] += sum;
     }
     __syncthreads();
   }
 }
 
-// Cone row-bound slopes of every voter (one thread per voter): outer / inner
-// cone at the inlier threshold -/+ kConeEps (so / si = sqrt(1 - c^2) of each).
-// Also the per-slot row index of the (raster-ordered) voter list, rowstart[r]
-// = first voter with row >= r for rows r in [yfirst, ylast] (yspan), and the
-// slot's largest box radius: a vote band [y0, y1) then only visits voters
-// with rows in [y0 - kmax, y1 - 1 + kmax].
+// One lane per sampled voter: the cone row-bound slopes and code, the
+// (slot, row) voter counts that let a vote band find its voter range, and
+// each slot's largest box radius: a band [y0, y1) visits only voters with rows
+// in [y0 - kmax, y1 - 1 + kmax].
 __global__ void __launch_bounds__(256) k_voter_setup(int H, int W, int C, float inlier, double so, double si,
                                                       HoughWs ws) {
+  __shared__ int sbase[kMaxClasses + 1];  // slot s covers voters [sbase[s], sbase[s + 1])
   const int b = blockIdx.y;
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  const bool in = i < ws.nvtot[b];
-  int k = -1, kslot = 0;
+  const int nvote = ws.nvote[b];
+  for (int sl = threadIdx.x; sl < nvote; sl += blockDim.x) {
+    const int cls = ws.slot_cls[(size_t)b * C + sl];
+    sbase[sl] = ws.vbase[(size_t)b * C + cls];
+    if (sl == nvote - 1) sbase[nvote] = ws.vbase[(size_t)b * C + cls] + ws.vcount[(size_t)b * C + cls];
+  }
+  __syncthreads();
+  const bool in = nvote > 0 && i < sbase[nvote];
+  int k = -1, slot = 0, y = 0;
   if (in) {
     const size_t vi = (size_t)b * ws.vcap + i;
-    const float4 q = ws.vdat[vi];
-    const double c = (double)inlier;
-    const bool fast_ok = c > 0.05 && c < 0.999;
-    const float u = q.x, v = q.y;
-    const float n1f = sqrtf(u * u + v * v);
-    int code = 0;
-    double sl[4] = {0.0, 0.0, 0.0, 0.0};
-    k = box_radius(q.w);
-    if (k < 0) {
-      code = kDeadVoter;
-    } else if (!fast_ok || !(n1f >= 1e-18f && n1f <= 1e18f)) {
-      code = kSlowVoter;
-    } else {
-      const double ud = u, vd = v;
-      const double nd = sqrt(ud * ud + vd * vd);
-      const double ex = ud / nd, ey = vd / nd;
-      int c0, c1, c2, c3;
-      bound_setup(ex, ey, c - kConeEps, so, sl[0], c0, sl[1], c1);  // outer cone
-      bound_setup(ex, ey, c + kConeEps, si, sl[2], c2, sl[3], c3);  // inner cone
-      code = c0 | (c1 << 2) | (c2 << 4) | (c3 << 6);
-    }
-    // slopes are evaluated in float per row (hough_vote.hip): the float error
-    // of an interval end is <= ~2.6% of the +-kConeEps margin in x there
-    auto cl = [](double v) { return (float)(v > 1e30 ? 1e30 : (v < -1e30 ? -1e30 : v)); };
-    ws.vcone[vi] = make_float4(cl(sl[0]), cl(sl[1]), cl(sl[2]), cl(sl[3]));
+    float4 cone;
+    int code;
+    k = voter_cone(ws.vdat[vi], inlier, so, si, cone, code);
+    ws.vcone[vi] = cone;
     ws.vcode[vi] = code;
-    // slot of voter i (slots occupy consecutive voter ranges in slot order)
-    const int nvote = ws.nvote[b];
-    int slot = 0, base = 0, cnt = 0;
-    for (int s = 0; s < nvote; s++) {
-      const int cls = ws.slot_cls[(size_t)b * C + s];
-      base = ws.vbase[(size_t)b * C + cls];
-      cnt = ws.vcount[(size_t)b * C + cls];
-      slot = s;
-      if (i < base + cnt) break;
-    }
-    const int j = i - base;
-    const int y = ws.vpos[vi] / W;
-    const int yprev = j > 0 ? ws.vpos[vi - 1] / W : -1;
-    int32_t* rs = ws.rowstart + ((size_t)b * C + slot) * (H + 1);
-    if (j == 0) {
-      rs[y] = 0;
-      ws.yspan[((size_t)b * C + slot) * 2] = y;
-    } else {
-      for (int r = yprev + 1; r <= y; r++) rs[r] = j;  // rows (yprev, y]: usually 0 or 1
-    }
-    if (j == cnt - 1) ws.yspan[((size_t)b * C + slot) * 2 + 1] = y;
-    kslot = slot;
+    while (slot + 1 < nvote && i >= sbase[slot + 1]) slot++;
+    y = ws.vpos[vi] / W;
   }
-  // slot max of k: lanes grouped by slot (a wave spans at most a few slots),
-  // one atomic per (wave, slot) group
-  uint64_t active = __ballot(in && k >= 0);
-  while (active) {
-    const int leader = __ffsll((long long)active) - 1;
-    const int s0 = __shfl(kslot, leader, 64);
-    const uint64_t m = __ballot(in && k >= 0 && kslot == s0);
-    int kk = (in && k >= 0 && kslot == s0) ? k : -1;
+  int32_t* rowcnt = ws.rowcnt + (size_t)b * C * H;
+  for_each_label_group(slot * H + y, in, [&](int key, uint64_t m) {
+    if (pcnn::lane_id() == __ffsll((long long)m) - 1) atomicAdd(&rowcnt[key], __popcll(m));
+  });
+  for_each_label_group(slot, in && k >= 0, [&](int s0, uint64_t m) {
+    int kk = (in && k >= 0 && slot == s0) ? k : -1;
     kk = pcnn::wave_max(kk);
-    if (pcnn::lane_id() == leader) atomicMax(ws.kmax + (size_t)b * C + s0, kk);
-    active &= ~m;
-  }
+    if (pcnn::lane_id() == __ffsll((long long)m) - 1) atomicMax(ws.kmax + (size_t)b * C + s0, kk);
+  });
 }
 
 }  // namespace pcnn_hough

@@ -94,20 +94,18 @@ static int hough_voting_impl(const int32_t* label, const float* prob, int32_t* l
   const int HW = H * W;
 
   if (label) {
-    hipLaunchKernelGGL(k_label_hist, dim3(ws.nblk, B), dim3(kCompactThreads), 0, st, label, HW, C, ws);
+    hipLaunchKernelGGL(k_label_hist, dim3(ws.nblk, B), dim3(kCompactThreads), 0, st, label, HW, C, H, ws);
   } else {
     const size_t lds = C <= kArgmaxStagedMaxC ? (size_t)kCompactThreads * C * sizeof(float) : 0;
-    hipLaunchKernelGGL(k_label_hist_prob, dim3(ws.nblk, B), dim3(kCompactThreads), lds, st, prob, label_out, HW, C,
+    hipLaunchKernelGGL(k_label_hist_prob, dim3(ws.nblk, B), dim3(kCompactThreads), lds, st, prob, label_out, HW, C, H,
                        ws);
     label = label_out;
   }
-  hipLaunchKernelGGL(k_label_scan, dim3(B), dim3(1024), 0, st, C, label_thr, index_size, nms ? 1 : 0, skip_pixels,
-                     ws);
-  hipLaunchKernelGGL(k_label_scatter, dim3(ws.nblk, B), dim3(kCompactThreads), 0, st, label, vertex, vch, extents, meta,
-                     num_meta, H, W, C, skip_pixels, ws);
   {
     const double c = (double)inlier_thr, co = c - kConeEps, ci = c + kConeEps;
     const double so = std::sqrt(std::max(0.0, 1.0 - co * co)), si = std::sqrt(std::max(0.0, 1.0 - ci * ci));
+    hipLaunchKernelGGL(k_label_place, dim3(ws.nblk, B), dim3(kCompactThreads), 0, st, label, vertex, vch, extents,
+                       meta, num_meta, H, W, C, skip_pixels, label_thr, index_size, nms ? 1 : 0, ws);
     hipLaunchKernelGGL(k_voter_setup, dim3((ws.vcap + 255) / 256, B), dim3(256), 0, st, H, W, C, inlier_thr, so, si,
                        ws);
   }

@@ -84,14 +84,28 @@ __global__ void __launch_bounds__(kVoteThreads) k_hough_vote(int H, int W, int C
   const int Wp = W + 1;
   // only voters whose +-k rows can reach the band (rows in [y0 - kmax, y1 - 1 + kmax])
   const int kx = ws.kmax[(size_t)b * C + slot];
+  __shared__ int red[2][kVoteThreads / 64];
   int ibeg = 0, iend = 0;
-  if (kx >= 0) {
-    const int32_t* rs = ws.rowstart + ((size_t)b * C + slot) * (H + 1);
-    const int yf = ws.yspan[((size_t)b * C + slot) * 2], yl = ws.yspan[((size_t)b * C + slot) * 2 + 1];
-    const int cnt = ws.vcount[(size_t)b * C + cls];
+  if (kx >= 0) {  // block-uniform: voters in rows < ylo and < yhi1 of the raster-ordered list
+    const int32_t* rc = ws.rowcnt + ((size_t)b * C + slot) * H;
     const int ylo = max(0, y0 - kx), yhi1 = (int)min((long)H, (long)y1 + kx);  // rows [ylo, yhi1)
-    ibeg = ylo <= yf ? 0 : (ylo > yl ? cnt : rs[ylo]);
-    iend = yhi1 > yl ? cnt : (yhi1 <= yf ? 0 : rs[yhi1]);
+    int a = 0, c = 0;
+    for (int r = threadIdx.x; r < yhi1; r += blockDim.x) {
+      const int v = rc[r];
+      a += r < ylo ? v : 0;
+      c += v;
+    }
+    a = pcnn::wave_sum(a);
+    c = pcnn::wave_sum(c);
+    if (pcnn::lane_id() == 0) {
+      red[0][threadIdx.x >> 6] = a;
+      red[1][threadIdx.x >> 6] = c;
+    }
+    __syncthreads();
+    for (int w = 0; w < kVoteThreads / 64; w++) {
+      ibeg += red[0][w];
+      iend += red[1][w];
+    }
   }
   if (ibeg >= iend && !counts_out) {
     // no voter reaches the band: all its counts are 0; its first-max key is
