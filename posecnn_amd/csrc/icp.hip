@@ -16,12 +16,13 @@
 // (icp.cpp:51-103).  Here the pixels whose rendered depth lies in the depth
 // range (the only ones icpKernel can use: icp.cu:56-63) are compacted once per
 // problem, in raster order, into dense (vertex, normal) records; then each
-// Gauss-Newton iteration is two launches over all N problems: 8-64
-// workgroups per problem accumulate J^T J and J^T r in registers and reduce
-// them through the wave and the workgroup, and one wave per problem adds the
-// slices in order, solves the 6x6 system (Eigen LDLT with diagonal
-// pivoting), exponentiates the twist (Sophus SE3::exp) and left-multiplies it
-// into the accumulated update that the next iteration reads.  No per-pixel Jacobian ever
+// Gauss-Newton iteration is one launch over all N problems: 8-64 workgroups
+// per problem each first finish the previous iteration (its slices added in
+// order, the 6x6 system solved by Eigen's LDLT with diagonal pivoting, the
+// twist exponentiated by Sophus SE3::exp and left-multiplied into the
+// accumulated update -- redundantly and identically in every workgroup), then
+// accumulate J^T J and J^T r in registers and reduce them through the wave and
+// the workgroup into their slice of the iteration's system.  No per-pixel Jacobian ever
 // reaches HBM and the host is never involved.
 //
 // Rendering (the OpenGL vertex / normal / canonical-coordinate maps of the
@@ -348,10 +349,32 @@ __global__ void __launch_bounds__(kBlk) k_icp_scatter(const float* __restrict__ 
   }
 }
 
-// One Gauss-Newton iteration of df::icp for N problems: grid (split, N),
-// each workgroup accumulates J^T J / J^T r over a strided slice of its
-// problem's records into its slot of `partial`; k_icp_solve then adds the
-// slices in slice order.  The order of every sum is fixed (lane, wave tree,
+
+// T_next = exp(LDLT solve of the 28-entry system) * T  (one lane)
+__device__ SE3 icp_advance(const float* sys, const SE3& T) {
+  float m[36], b[6], x[6];
+  int k = 0;
+#pragma unroll
+  for (int i = 0; i < 6; i++)
+#pragma unroll
+    for (int j = i; j < 6; j++) {
+      m[i * 6 + j] = sys[k];
+      m[j * 6 + i] = sys[k];
+      k++;
+    }
+#pragma unroll
+  for (int i = 0; i < 6; i++) b[i] = sys[21 + i];
+  ldlt_solve6(m, b, x);
+  return se3_mul(se3_exp(x), T);
+}
+
+// One Gauss-Newton iteration of df::icp for N problems: grid (split, N).
+// Each workgroup first finishes the previous iteration itself -- the slices
+// of its system added in slice order, the LDLT solve and exp(x) applied to
+// the previous pose, identically in every workgroup (workgroup 0 publishes
+// the pose for the next launch) -- then accumulates J^T J / J^T r over a
+// strided slice of its problem's records into its slot of this iteration's
+// `partial` buffer (double-buffered); k_icp_finish solves the last one.  The order of every sum is fixed (lane, wave tree,
 // waves, slices): results are run-to-run identical.  (A last-arriver ticket
 // in place of the second launch measured 28 us per iteration at 16 slices
 // and 65 us at 64: each workgroup's device-scope release fence costs more
@@ -372,18 +395,37 @@ __device__ __forceinline__ void store_se3(float* p, const SE3& T) {
 __global__ void __launch_bounds__(kBlk) k_icp_step(
     const float4* __restrict__ rec, const int32_t* __restrict__ cnt, int nseg, const float* __restrict__ live,
     const int32_t* __restrict__ live_index, int H, int W, float fx, float fy, float px, float py, float znear,
-    float zfar, float max_error, int it, int split, const float* __restrict__ acc_pose,
-    float* __restrict__ partial) {
+    float zfar, float max_error, int it, int iterations, int split, float* __restrict__ acc_pose,
+    float* __restrict__ partial, float* __restrict__ systems) {
   __shared__ float part[kBlk / 64][kSys];
   __shared__ int ish[kBlk / 64];
+  __shared__ float psys[kSys];
+  __shared__ SE3 Tsh;
   const int n = blockIdx.y, g = blockIdx.x;
   const int HW = H * W;
+  const size_t pstride = (size_t)kIcpSplitMax * kSys;  // one problem's slices
   int c = 0;
   for (int s = threadIdx.x; s < nseg; s += kBlk) c += cnt[(size_t)n * nseg + s];
   const int total = block_sum_int<kBlk>(c, ish);
   const float4* rn = rec + (size_t)n * HW * 2;
   const float* lv = live + (size_t)(live_index ? live_index[n] : n) * HW * 3;
-  const SE3 T = it == 0 ? SE3{{1.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}} : load_se3(acc_pose + (size_t)n * 8);
+  if (it > 0) {  // finish iteration it - 1
+    const float* pp = partial + ((size_t)((it - 1) & 1) * gridDim.y + n) * pstride;
+    if (threadIdx.x < kSys) psys[threadIdx.x] = ordered_sum_strided(pp + threadIdx.x, split, kSys);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const SE3 Tp = it == 1 ? SE3{{1.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}}
+                             : load_se3(acc_pose + ((size_t)((it - 1) & 1) * gridDim.y + n) * 8);
+      Tsh = icp_advance(psys, Tp);
+      if (g == 0) store_se3(acc_pose + ((size_t)(it & 1) * gridDim.y + n) * 8, Tsh);
+    }
+    if (g == 0 && systems && threadIdx.x < kSys)
+      systems[((size_t)n * iterations + it - 1) * kSys + threadIdx.x] = psys[threadIdx.x];
+  } else if (threadIdx.x == 0) {
+    Tsh = SE3{{1.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}};
+  }
+  __syncthreads();
+  const SE3 T = Tsh;
   const float border = 2.f;
   const float umax = (float)(W - 1) - border, vmax = (float)(H - 1) - border;
   const int wave = threadIdx.x >> 6, lane = pcnn::lane_id();
@@ -445,53 +487,35 @@ __global__ void __launch_bounds__(kBlk) k_icp_step(
   if (threadIdx.x < kSys) {
     float sum = 0.f;
     for (int w = 0; w < kBlk / 64; w++) sum += part[w][threadIdx.x];
-    partial[((size_t)n * kIcpSplitMax + g) * kSys + threadIdx.x] = sum;
+    partial[((size_t)(it & 1) * gridDim.y + n) * pstride + (size_t)g * kSys + threadIdx.x] = sum;
   }
 }
 
-// The iteration's solve, one wave per problem (the launch boundary orders it
-// after every slice): the slices added in order, the 6x6 LDLT, exp(x)
-// left-multiplied into the accumulated update.
-__global__ void __launch_bounds__(64) k_icp_solve(int it, int iterations, int split, float* __restrict__ acc_pose,
-                                                  const float* __restrict__ partial, const float* __restrict__ pose_in,
-                                                  float* __restrict__ update, float* __restrict__ pose_out,
-                                                  float* __restrict__ systems) {
+// The last iteration's solve, one wave per problem: its slices added in
+// order, the update and (optionally) update * pose_in written out.
+__global__ void __launch_bounds__(64) k_icp_finish(int N, int iterations, int split, const float* __restrict__ acc_pose,
+                                                   const float* __restrict__ partial, const float* __restrict__ pose_in,
+                                                   float* __restrict__ update, float* __restrict__ pose_out,
+                                                   float* __restrict__ systems) {
   __shared__ float sys[kSys];
-  const int n = blockIdx.x;
+  const int n = blockIdx.x, it = iterations - 1;
+  const float* pp = partial + ((size_t)(it & 1) * N + n) * (size_t)kIcpSplitMax * kSys;
   if (threadIdx.x < kSys) {
-    float sum = 0.f;
-    sum = ordered_sum_strided(partial + (size_t)n * kIcpSplitMax * kSys + threadIdx.x, split, kSys);
-    sys[threadIdx.x] = sum;
-    if (systems) systems[((size_t)n * iterations + it) * kSys + threadIdx.x] = sum;
+    sys[threadIdx.x] = ordered_sum_strided(pp + threadIdx.x, split, kSys);
+    if (systems) systems[((size_t)n * iterations + it) * kSys + threadIdx.x] = sys[threadIdx.x];
   }
   __syncthreads();
   if (threadIdx.x != 0) return;
-  const SE3 T = it == 0 ? SE3{{1.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}} : load_se3(acc_pose + (size_t)n * 8);
-  float m[36], b[6], x[6];
-  int k = 0;
-#pragma unroll
-  for (int i = 0; i < 6; i++)
-#pragma unroll
-    for (int j = i; j < 6; j++) {
-      m[i * 6 + j] = sys[k];
-      m[j * 6 + i] = sys[k];
-      k++;
-    }
-#pragma unroll
-  for (int i = 0; i < 6; i++) b[i] = sys[21 + i];
-  ldlt_solve6(m, b, x);
-  const SE3 A = se3_mul(se3_exp(x), T);
-  store_se3(acc_pose + (size_t)n * 8, A);
-  if (it == iterations - 1) {
-    store_se3(update + (size_t)n * 7, A);
-    if (pose_in && pose_out) {  // refinePose: T_co = update * T_co (synthesize.cpp:2023-2025)
-      const float* P = pose_in + (size_t)n * 7;
-      const float qn = sqrtf(P[0] * P[0] + P[1] * P[1] + P[2] * P[2] + P[3] * P[3]);
-      SE3 B;
-      B.q = {P[0] / qn, P[1] / qn, P[2] / qn, P[3] / qn};
-      B.t[0] = P[4]; B.t[1] = P[5]; B.t[2] = P[6];
-      store_se3(pose_out + (size_t)n * 7, se3_mul(A, B));
-    }
+  const SE3 Tp = it == 0 ? SE3{{1.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}} : load_se3(acc_pose + ((size_t)(it & 1) * N + n) * 8);
+  const SE3 A = icp_advance(sys, Tp);
+  store_se3(update + (size_t)n * 7, A);
+  if (pose_in && pose_out) {  // refinePose: T_co = update * T_co (synthesize.cpp:2023-2025)
+    const float* P = pose_in + (size_t)n * 7;
+    const float qn = sqrtf(P[0] * P[0] + P[1] * P[1] + P[2] * P[2] + P[3] * P[3]);
+    SE3 B;
+    B.q = {P[0] / qn, P[1] / qn, P[2] / qn, P[3] / qn};
+    B.t[0] = P[4]; B.t[1] = P[5]; B.t[2] = P[6];
+    store_se3(pose_out + (size_t)n * 7, se3_mul(A, B));
   }
 }
 
@@ -776,16 +800,16 @@ __global__ void __launch_bounds__(kBlk) k_score_select(const uint8_t* __restrict
 struct IcpWs {
   int32_t* cnt;
   float4* rec;
-  float* acc;         // [N][8] accumulated update
-  float* partial;     // [N][kIcpSplitMax][kSys]
+  float* acc;         // [2][N][8] accumulated update, by iteration parity
+  float* partial;     // [2][N][kIcpSplitMax][kSys] per-slice systems, by iteration parity
 };
 
 inline IcpWs carve_icp(void* base, int N, int HW, size_t* bytes) {
   pcnn::Carve cv(base);
   IcpWs ws;
   const int nseg = (HW + kSeg - 1) / kSeg;
-  ws.acc = cv.take<float>((size_t)N * 8);
-  ws.partial = cv.take<float>((size_t)N * kIcpSplitMax * kSys);
+  ws.acc = cv.take<float>((size_t)2 * N * 8);
+  ws.partial = cv.take<float>((size_t)2 * N * kIcpSplitMax * kSys);
   ws.cnt = cv.take<int32_t>((size_t)N * nseg);
   ws.rec = cv.take<float4>((size_t)N * HW * 2);
   if (bytes) *bytes = cv.off;
@@ -843,12 +867,12 @@ extern "C" int pcnn_icp(const float* live, const int32_t* live_index, const floa
     hipLaunchKernelGGL(k_icp_identity, dim3((N + 63) / 64), dim3(64), 0, st, N, pose_in, update, pose_out);
   // about 512+ workgroups per launch: 1-2 records per lane for the usual footprints
   const int split = N >= 64 ? 8 : (512 / N > kIcpSplitMax ? kIcpSplitMax : (512 / N < 8 ? 8 : 512 / N));
-  for (int it = 0; it < iterations; it++) {
+  for (int it = 0; it < iterations; it++)
     hipLaunchKernelGGL(k_icp_step, dim3(split, N), dim3(kBlk), 0, st, ws.rec, ws.cnt, nseg, live, live_index, H, W,
-                       fx, fy, px, py, znear, zfar, max_error, it, split, ws.acc, ws.partial);
-    hipLaunchKernelGGL(k_icp_solve, dim3(N), dim3(64), 0, st, it, iterations, split, ws.acc, ws.partial, pose_in,
+                       fx, fy, px, py, znear, zfar, max_error, it, iterations, split, ws.acc, ws.partial, systems);
+  if (iterations > 0)
+    hipLaunchKernelGGL(k_icp_finish, dim3(N), dim3(64), 0, st, N, iterations, split, ws.acc, ws.partial, pose_in,
                        update, pose_out, systems);
-  }
   PCNN_CHECK_LAUNCH();
   return PCNN_OK;
 }

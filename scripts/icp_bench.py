@@ -1,10 +1,14 @@
-"""Time the pose-refinement ops on the synthetic box scene (tests/refine_scene.py):
-live vertices, icp for N problems (solveICP's 8 hypotheses) x iterations, centre.
-    python scripts/icp_bench.py [--n 8] [--iters 8] [--reps 20]"""
+"""Measurement of the pose-refinement row on the synthetic
+box scene (tests/refine_scene.py): live vertices, df::icp for N problems
+(solveICP's 8 hypotheses) x iterations, one JSON line with per-kernel HIP-event
+times, the step kernel's bandwidth against HBM, and the oracle's CPU ICP
+(oracle/orc_icp.cpp, one thread) timed on the same problems beside it.
+    python scripts/icp_bench.py [--n 8] [--iters 8] [--reps 20] [--no-cpu]"""
 import argparse
 import json
 import os
 import sys
+import time
 
 import numpy as np
 import torch
@@ -19,6 +23,7 @@ p = argparse.ArgumentParser()
 p.add_argument("--n", type=int, default=8)
 p.add_argument("--iters", type=int, default=8)
 p.add_argument("--reps", type=int, default=20)
+p.add_argument("--no-cpu", action="store_true")
 a = p.parse_args()
 D = torch.device("cuda")
 t = lambda x: torch.from_numpy(np.ascontiguousarray(x)).to(D)
@@ -45,8 +50,31 @@ def timed(fn):
     return e0.elapsed_time(e1) / a.reps * 1e3
 
 
-res = {"n_problems": a.n, "iterations": a.iters, "pixels_in_range": int((sc["pred"]["pred_v"][..., 2] > 0.25).sum()),
-       "live_vertices_us": timed(lambda: R.live_vertices(depth, lab, obj, 10000.0, CAMERA)),
-       "icp_us": timed(lambda: R.icp(lv, pv, pn, CAMERA, max_error=0.05, iterations=a.iters, live_index=li)),
-       "icp_1iter_us": timed(lambda: R.icp(lv, pv, pn, CAMERA, max_error=0.05, iterations=1, live_index=li))}
+H, W = sc["live"]["label"].shape
+recs = int(((sc["pred"]["pred_v"][..., 2] >= 0.25) & (sc["pred"]["pred_v"][..., 2] <= 6.0)).sum())
+icp_us = timed(lambda: R.icp(lv, pv, pn, CAMERA, max_error=0.05, iterations=a.iters, live_index=li))
+icp0_us = timed(lambda: R.icp(lv, pv, pn, CAMERA, max_error=0.05, iterations=0, live_index=li))
+per_iter = (icp_us - icp0_us) / max(a.iters, 1)
+# algorithmic bytes of one iteration: each record (vertex + normal, 32 B) and
+# its live-vertex gather (12 B), every problem
+iter_bytes = a.n * recs * (32 + 12)
+res = {"metric": "refined hypotheses/s (8-iteration df::icp on 640x480 maps)",
+       "value": round(a.n / (icp_us * 1e-6), 1), "unit": "hypotheses/s",
+       "n_problems": a.n, "iterations": a.iters, "records_per_problem": recs,
+       "live_vertices_us": round(timed(lambda: R.live_vertices(depth, lab, obj, 10000.0, CAMERA)), 1),
+       "icp_us": round(icp_us, 1), "compaction_us": round(icp0_us, 1), "us_per_iteration": round(per_iter, 1),
+       "roofline": {"bound": "hbm", "achieved": round(iter_bytes / (per_iter * 1e-6) / 1e9, 1), "peak": 8000.0,
+                    "unit": "GB/s", "frac": round(iter_bytes / (per_iter * 1e-6) / 8e12, 4),
+                    "bytes_per_iteration": iter_bytes,
+                    "note": "step + solve launches per iteration; latency-bound at this size"},
+       "data": "synthetic (ray-cast box, tests/refine_scene.py)"}
+if not a.no_cpu:
+    from oracle import oracle
+    ref_lv = oracle.icp_live_vertices(sc["live"]["depth"], sc["live"]["label"], sc["cls"], 10000.0, CAMERA)
+    t0 = time.perf_counter()
+    oracle.icp(ref_lv, sc["pred"]["pred_v"], sc["pred"]["pred_n"], CAMERA, max_error=0.05, iterations=a.iters)
+    cpu_s = time.perf_counter() - t0
+    res["cpu_baseline"] = {"value": round(1.0 / cpu_s, 2), "unit": "hypotheses/s", "cores": 1, "kind": "port",
+                           "sample": f"one problem x {a.iters} iterations of the oracle's df::icp restatement "
+                                     "(full-frame per-pixel pass per iteration, as icp.cu)"}
 print(json.dumps(res), flush=True)
