@@ -327,7 +327,8 @@ int pcnn_vertex_pred_compact(const float* feat, const float* weights, const floa
  *   projective point-to-plane residual (border 2 px, ray/normal test 0.1,
  *   |error| <= max_error, weight 1/live depth), each solving JTJ x = JTr
  *   (Eigen LDLT) and left-multiplying SE3::exp(x) into the accumulated update.
- *   live (L,H,W,3) with live_index (N) selecting problem n's map (NULL: n);
+ *   live (num_live,H,W,3) with live_index (N) selecting problem n's map (NULL:
+ *   n; an index outside [0, num_live) contributes no pixel);
  *   update (N,7); pose_in / pose_out (N,7) optional: pose_out = update * pose_in
  *   (refinePose, synthesize.cpp:2023-2025); systems (N,iterations,28) optional:
  *   per iteration the 21 upper-triangle JTJ entries, 6 JTr and the pixel count.
@@ -343,8 +344,8 @@ int pcnn_vertex_pred_compact(const float* feat, const float* weights, const floa
 int pcnn_icp_live_vertices(const uint16_t* depth, const int32_t* label, int H, int W, const int32_t* obj_ids, int L,
                            float factor, float fx, float fy, float px, float py, float* live, void* stream);
 size_t pcnn_icp_workspace_size(int N, int H, int W);
-int pcnn_icp(const float* live, const int32_t* live_index, const float* pred_vertices, const float* pred_normals,
-             int N, int H, int W, float fx, float fy, float px, float py, float znear, float zfar, float max_error,
+int pcnn_icp(const float* live, int num_live, const int32_t* live_index, const float* pred_vertices,
+             const float* pred_normals, int N, int H, int W, float fx, float fy, float px, float py, float znear, float zfar, float max_error,
              int iterations, const float* pose_in, float* update, float* pose_out, float* systems, void* workspace,
              size_t workspace_bytes, void* stream);
 size_t pcnn_icp_reduce_workspace_size(int L, int H, int W);

@@ -86,7 +86,7 @@ _SIGS = {
     "pcnn_icp_live_vertices": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_float, c_float, c_float,
                                        c_float, c_float, c_void_p, c_void_p]),
     "pcnn_icp_workspace_size": (c_size_t, [c_int, c_int, c_int]),
-    "pcnn_icp": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_float, c_float,
+    "pcnn_icp": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_float, c_float,
                          c_float, c_float, c_float, c_float, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                          c_size_t, c_void_p]),
     "pcnn_icp_reduce_workspace_size": (c_size_t, [c_int, c_int, c_int]),

@@ -394,8 +394,8 @@ __device__ __forceinline__ void store_se3(float* p, const SE3& T) {
 
 __global__ void __launch_bounds__(kBlk) k_icp_step(
     const float4* __restrict__ rec, const int32_t* __restrict__ cnt, int nseg, const float* __restrict__ live,
-    const int32_t* __restrict__ live_index, int H, int W, float fx, float fy, float px, float py, float znear,
-    float zfar, float max_error, int it, int iterations, int split, float* __restrict__ acc_pose,
+    const int32_t* __restrict__ live_index, int num_live, int H, int W, float fx, float fy, float px, float py,
+    float znear, float zfar, float max_error, int it, int iterations, int split, float* __restrict__ acc_pose,
     float* __restrict__ partial, float* __restrict__ systems) {
   __shared__ float part[kBlk / 64][kSys];
   __shared__ int ish[kBlk / 64];
@@ -406,9 +406,11 @@ __global__ void __launch_bounds__(kBlk) k_icp_step(
   const size_t pstride = (size_t)kIcpSplitMax * kSys;  // one problem's slices
   int c = 0;
   for (int s = threadIdx.x; s < nseg; s += kBlk) c += cnt[(size_t)n * nseg + s];
-  const int total = block_sum_int<kBlk>(c, ish);
+  const int li = live_index ? live_index[n] : n;
+  // a live index outside [0, num_live) contributes no pixel (identity update)
+  const int total = (li >= 0 && li < num_live) ? block_sum_int<kBlk>(c, ish) : (block_sum_int<kBlk>(0, ish), 0);
   const float4* rn = rec + (size_t)n * HW * 2;
-  const float* lv = live + (size_t)(live_index ? live_index[n] : n) * HW * 3;
+  const float* lv = live + (size_t)(li >= 0 && li < num_live ? li : 0) * HW * 3;
   if (it > 0) {  // finish iteration it - 1
     const float* pp = partial + ((size_t)((it - 1) & 1) * gridDim.y + n) * pstride;
     if (threadIdx.x < kSys) psys[threadIdx.x] = ordered_sum_strided(pp + threadIdx.x, split, kSys);
@@ -848,12 +850,12 @@ extern "C" size_t pcnn_icp_workspace_size(int N, int H, int W) {
   return b + 256;
 }
 
-extern "C" int pcnn_icp(const float* live, const int32_t* live_index, const float* pred_vertices,
+extern "C" int pcnn_icp(const float* live, int num_live, const int32_t* live_index, const float* pred_vertices,
                         const float* pred_normals, int N, int H, int W, float fx, float fy, float px, float py,
                         float znear, float zfar, float max_error, int iterations, const float* pose_in, float* update,
                         float* pose_out, float* systems, void* workspace, size_t workspace_bytes, void* stream) {
   PCNN_REQUIRE(live && pred_vertices && pred_normals && update && workspace && N > 0 && H > 0 && W > 0 &&
-               iterations >= 0 && (long)H * W * 2 * N < (1l << 31));
+               num_live > 0 && (live_index || num_live >= N) && iterations >= 0 && (long)H * W * 2 * N < (1l << 31));
   size_t need = 0;
   carve_icp(nullptr, N, H * W, &need);
   if (workspace_bytes < need) return PCNN_ECAPACITY;
@@ -868,8 +870,9 @@ extern "C" int pcnn_icp(const float* live, const int32_t* live_index, const floa
   // about 512+ workgroups per launch: 1-2 records per lane for the usual footprints
   const int split = N >= 64 ? 8 : (512 / N > kIcpSplitMax ? kIcpSplitMax : (512 / N < 8 ? 8 : 512 / N));
   for (int it = 0; it < iterations; it++)
-    hipLaunchKernelGGL(k_icp_step, dim3(split, N), dim3(kBlk), 0, st, ws.rec, ws.cnt, nseg, live, live_index, H, W,
-                       fx, fy, px, py, znear, zfar, max_error, it, iterations, split, ws.acc, ws.partial, systems);
+    hipLaunchKernelGGL(k_icp_step, dim3(split, N), dim3(kBlk), 0, st, ws.rec, ws.cnt, nseg, live, live_index,
+                       num_live, H, W, fx, fy, px, py, znear, zfar, max_error, it, iterations, split, ws.acc,
+                       ws.partial, systems);
   if (iterations > 0)
     hipLaunchKernelGGL(k_icp_finish, dim3(N), dim3(64), 0, st, N, iterations, split, ws.acc, ws.partial, pose_in,
                        update, pose_out, systems);

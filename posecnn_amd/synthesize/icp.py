@@ -49,7 +49,7 @@ def icp(live, pred_vertices, pred_normals, camera, depth_range=(0.25, 6.0), max_
         raise ValueError("icp: pred maps (N,H,W,4), live (L,H,W,3)")
     li = None
     if live_index is not None:
-        if li_host := not live_index.is_cuda:  # validated on the host; a device index is trusted (no sync)
+        if not live_index.is_cuda:  # validated here; a device index out of range contributes no pixel (no sync)
             if live_index.numel() != N or int(live_index.min()) < 0 or int(live_index.max()) >= lv.shape[0]:
                 raise ValueError("icp: live_index must map each problem to a live map")
         elif live_index.numel() != N:
@@ -66,7 +66,7 @@ def icp(live, pred_vertices, pred_normals, camera, depth_range=(0.25, 6.0), max_
     nbytes = L.pcnn_icp_workspace_size(N, H, W)
     ws = _lib.workspace(nbytes, dev, "icp", stream)
     fx, fy, px, py = (float(c) for c in camera)
-    rc = L.pcnn_icp(_lib.ptr(lv), _lib.ptr(li), _lib.ptr(pv), _lib.ptr(pn), N, H, W, fx, fy, px, py,
+    rc = L.pcnn_icp(_lib.ptr(lv), lv.shape[0], _lib.ptr(li), _lib.ptr(pv), _lib.ptr(pn), N, H, W, fx, fy, px, py,
                     float(depth_range[0]), float(depth_range[1]), float(max_error), int(iterations), _lib.ptr(pin),
                     _lib.ptr(update), _lib.ptr(pout), _lib.ptr(systems), _lib.ptr(ws), ws.numel(),
                     _lib.stream_ptr(stream))

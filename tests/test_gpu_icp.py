@@ -71,6 +71,12 @@ def test_icp_batched_problems_and_live_index(hip, orc):
         o, _ = orc.icp(ref_lv, sc["pred"]["pred_v"], sc["pred"]["pred_n"], CAMERA, max_error=0.05, iterations=8)
         np.testing.assert_allclose(u[k], o, atol=2e-4)
     np.testing.assert_array_equal(u[2], np.array([1, 0, 0, 0, 0, 0, 0], np.float32))
+    # a device-side live index is not checked on the host: out of range, the problem contributes nothing
+    bad = torch.tensor([0, 5, -1], dtype=torch.int32, device=D)
+    u2, _ = R.icp(lv, pv, pn, CAMERA, max_error=0.05, iterations=8, live_index=bad)
+    u2 = u2.cpu().numpy()
+    np.testing.assert_array_equal(u2[0], u[0])
+    np.testing.assert_array_equal(u2[1:], np.tile(np.array([1, 0, 0, 0, 0, 0, 0], np.float32), (2, 1)))
 
 
 def test_icp_center_and_energy(hip, orc):
