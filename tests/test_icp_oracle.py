@@ -73,3 +73,36 @@ def test_score_prefers_the_truth(orc):
     vm = render_box(sc["true"], sc["half"], sc["cls"])["vertmap"]
     s, ch = orc.icp_score(lv, sc["live"]["label"], sc["cls"], vm, hyps)
     assert ch == 1 and s[1] > 0.9 and s[2] < s[1]
+
+
+def test_nelder_mead_bounded_quadratic():
+    """The host Nelder-Mead of solve_icp's optEnergy stage: finds a bounded
+    quadratic's minimum, never leaves the box, stops at max_eval."""
+    from posecnn_amd.synthesize.icp import nelder_mead
+    calls = []
+    target = np.array([0.05, -0.02, 0.3])
+
+    def f(x):
+        calls.append(x.copy())
+        return float(np.sum((x - target) ** 2))
+
+    x0 = np.zeros(3)
+    lb, ub = np.array([-0.1, -0.1, -0.1]), np.array([0.1, 0.1, 0.1])
+    x, fx = nelder_mead(f, x0, lb, ub, 200)
+    assert len(calls) <= 200
+    assert all(np.all(c >= lb - 1e-12) and np.all(c <= ub + 1e-12) for c in calls)
+    np.testing.assert_allclose(x, [0.05, -0.02, 0.1], atol=2e-3)  # z pinned at its bound
+    calls.clear()
+    nelder_mead(f, x0, lb, ub, 10)
+    assert len(calls) <= 10
+
+
+def test_host_se3_mul_matches_oracle(orc):
+    from posecnn_amd.synthesize.icp import _se3_mul
+    rng = np.random.default_rng(7)
+    for _ in range(10):
+        a = np.concatenate([rng.normal(size=4), rng.normal(size=3)])
+        b = np.concatenate([rng.normal(size=4), rng.normal(size=3)])
+        a[:4] /= np.linalg.norm(a[:4])
+        b[:4] /= np.linalg.norm(b[:4])
+        np.testing.assert_allclose(_se3_mul(a, b), orc.se3_mul(a, b), atol=1e-5)
