@@ -16,15 +16,9 @@ constexpr int kMaxClasses = 256;
 #endif
 constexpr int kPixPerBlk = PCNN_PIXBLK;   // label pixels per compaction block
 constexpr int kCompactThreads = 256;
-#ifndef PCNN_VBAND
-#define PCNN_VBAND 4
-#define PCNN_VTHREADS 512
-#endif
 #ifndef PCNN_PTHREADS
 #define PCNN_PTHREADS 1024
 #endif
-constexpr int kBand = PCNN_VBAND;           // Hough rows per vote workgroup
-constexpr int kVoteThreads = PCNN_VTHREADS;
 constexpr int kPeakThreads = PCNN_PTHREADS;
 constexpr int kPeakChunk = 4096;   // voters per ordered-sum chunk (LDS floats)
 constexpr int kCandCap = 4096;     // NMS candidates per image
@@ -380,6 +374,7 @@ __global__ void k_label_place(const int32_t* __restrict__ label, const float* __
                               const float* __restrict__ extents, const float* __restrict__ meta, int num_meta, int H,
                               int W, int C, int skip, int label_thr, int index_size, int nms, HoughWs ws);
 __global__ void k_voter_setup(int H, int W, int C, float inlier, double so, double si, HoughWs ws);
+template <int kBand, int kVoteThreads>
 __global__ void k_hough_vote(int H, int W, int C, float inlier, HoughWs ws, int32_t* __restrict__ counts_out);
 __global__ void k_hough_peak(int B, int H, int W, int C, float inlier, const float* __restrict__ extents,
                              const float* __restrict__ meta, int num_meta, HoughWs ws, int is_train, int batch_base,

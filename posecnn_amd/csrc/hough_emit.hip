@@ -114,9 +114,14 @@ static int hough_voting_impl(const int32_t* label, const float* prob, int32_t* l
   // slots that can vote: all present classes (NMS) or the first index_size (cu.cc:775-776)
   const int slots = nms ? C - 1 : (C - 1 < index_size ? C - 1 : index_size);
   if (slots > 0) {
-    const size_t lds = (size_t)kBand * (W + 1) * sizeof(int);
-    hipLaunchKernelGGL(k_hough_vote, dim3((H + kBand - 1) / kBand, slots, B), dim3(kVoteThreads), lds, st, H, W, C,
-                       inlier_thr, ws, counts_out);
+    // vote geometry by batch (hough_vote.hip): two-row bands when B <= 2
+    const int band = B <= 2 ? 2 : 4;
+    const size_t lds = (size_t)band * (W + 1) * sizeof(int);
+    const dim3 vgrid((H + band - 1) / band, slots, B);
+    if (band == 4)
+      hipLaunchKernelGGL((k_hough_vote<4, 512>), vgrid, dim3(512), lds, st, H, W, C, inlier_thr, ws, counts_out);
+    else
+      hipLaunchKernelGGL((k_hough_vote<2, 512>), vgrid, dim3(512), lds, st, H, W, C, inlier_thr, ws, counts_out);
     PCNN_CHECK_LAUNCH();
     if (!nms) {
       hipLaunchKernelGGL(k_hough_peak, dim3(slots, B), dim3(kPeakThreads), 0, st, B, H, W, C, inlier_thr, extents,

@@ -71,6 +71,13 @@ __device__ __forceinline__ void exact_cells(int* row, int a, int b, int r, int x
   if (start >= 0) add_run(row, start, b);
 }
 
+// kBand rows x kVoteThreads lanes per workgroup: (4, 512) for B >= 3, (2, 512)
+// for B <= 2, where the grid is small and one workgroup's voter loop is the
+// critical path.  Measured op times (scripts/vote_ab.sh), B = 1 / 2 / 4 / 8:
+// 4 x 512: 88.4 / 121.5 / 131.1 / 169.0 us; 2 x 512: 80.0 / 118.4 / 143.0 /
+// 196.1; 2 x 1024: 89.2 / 133.4 / 190.0 / 294.6; 1 x 1024: 112.4 / 178.7 /
+// 280.6 / 463.2; 4 x 1024 at B = 1 / 8: 82.2 / 217.0.
+template <int kBand, int kVoteThreads>
 __global__ void __launch_bounds__(kVoteThreads) k_hough_vote(int H, int W, int C, float inlier, HoughWs ws,
                                                               int32_t* __restrict__ counts_out) {
   extern __shared__ __attribute__((aligned(16))) int diff[];  // [kBand][W + 1]
@@ -220,5 +227,8 @@ __global__ void __launch_bounds__(kVoteThreads) k_hough_vote(int H, int W, int C
     atomicMax(ws.key + (size_t)b * C + slot, m);
   }
 }
+
+template __global__ void k_hough_vote<4, 512>(int, int, int, float, HoughWs, int32_t*);
+template __global__ void k_hough_vote<2, 512>(int, int, int, float, HoughWs, int32_t*);
 
 }  // namespace pcnn_hough
