@@ -374,11 +374,12 @@ __device__ SE3 icp_advance(const float* sys, const SE3& T) {
 // the previous pose, identically in every workgroup (workgroup 0 publishes
 // the pose for the next launch) -- then accumulates J^T J / J^T r over a
 // strided slice of its problem's records into its slot of this iteration's
-// `partial` buffer (double-buffered); k_icp_finish solves the last one.  The order of every sum is fixed (lane, wave tree,
-// waves, slices): results are run-to-run identical.  (A last-arriver ticket
-// in place of the second launch measured 28 us per iteration at 16 slices
-// and 65 us at 64: each workgroup's device-scope release fence costs more
-// than the launch it saves.)
+// `partial` buffer (double-buffered); k_icp_finish solves the last one.  The
+// order of every sum is fixed (lane, wave tree, waves, slices): results are
+// run-to-run identical.  (Measured alternatives: a last-arriver ticket that
+// solves inside the iteration, 28 us per iteration at 16 slices and 65 at 64
+// -- each workgroup's device-scope release fence costs more than a launch;
+// a separate one-wave solve launch per iteration, 185 vs 163 us per 8 x 8.)
 constexpr int kIcpSplitMax = 64;  // workgroups per problem (the launcher picks 8..64 by N)
 
 __device__ __forceinline__ SE3 load_se3(const float* p) {
