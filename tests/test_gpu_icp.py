@@ -149,3 +149,22 @@ def test_solve_icp_end_to_end(hip, orc):
                                nm_evals=50)
     assert abs(np.linalg.norm(picp2[0, :4]) - 1) < 1e-4
     assert np.linalg.norm(picp2[0, 4:] - sc["true"][4:]) < 5e-3
+
+
+def test_icp_edges(hip, orc):
+    """iterations = 0 is the identity update (pose_out = pose_in normalised);
+    argument errors come back as ValueError (PCNN_EINVAL), never a crash."""
+    from posecnn_amd.synthesize import icp as R
+    sc = scene(0)
+    lv, _ = _live(sc, orc)
+    pv, pn = t(sc["pred"]["pred_v"])[None], t(sc["pred"]["pred_n"])[None]
+    pin = np.array([[2.0, 0, 0, 0, 0.1, 0.2, 0.7]], np.float32)
+    upd, pout = R.icp(lv, pv, pn, CAMERA, iterations=0, pose_in=t(pin))
+    np.testing.assert_array_equal(upd.cpu().numpy(), [[1, 0, 0, 0, 0, 0, 0]])
+    np.testing.assert_allclose(pout.cpu().numpy(), [[1, 0, 0, 0, 0.1, 0.2, 0.7]], atol=1e-7)
+    with pytest.raises(ValueError):  # H * W % 4 != 0 for the float4 live-vertex stores
+        R.live_vertices(torch.zeros((3, 3), dtype=torch.uint16, device=D), torch.zeros((3, 3), dtype=torch.int32,
+                                                                                      device=D), [1], 1.0, CAMERA)
+    with pytest.raises(ValueError):  # more than 64 hypotheses
+        R.icp_score(lv[0], t(sc["live"]["label"]), sc["cls"], t(sc["pred"]["vertmap"]),
+                    torch.zeros((65, 7), device=D))
