@@ -76,7 +76,9 @@ __device__ __forceinline__ void exact_cells(int* row, int a, int b, int r, int x
 // critical path.  Measured op times (scripts/vote_ab.sh), B = 1 / 2 / 4 / 8:
 // 4 x 512: 88.4 / 121.5 / 131.1 / 169.0 us; 2 x 512: 80.0 / 118.4 / 143.0 /
 // 196.1; 2 x 1024: 89.2 / 133.4 / 190.0 / 294.6; 1 x 1024: 112.4 / 178.7 /
-// 280.6 / 463.2; 4 x 1024 at B = 1 / 8: 82.2 / 217.0.
+// 280.6 / 463.2; 4 x 1024 at B = 1 / 8: 82.2 / 217.0; at B = 4 / 8:
+// 4 x 256 150 / 177, 8 x 256 194 / 217, 2 x 256 134 / 173, 3 x 512 133 / 177
+// against 131 / 170 for 4 x 512.
 template <int kBand, int kVoteThreads>
 __global__ void __launch_bounds__(kVoteThreads) k_hough_vote(int H, int W, int C, float inlier, HoughWs ws,
                                                               int32_t* __restrict__ counts_out) {
