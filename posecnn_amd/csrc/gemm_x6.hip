@@ -236,8 +236,12 @@ __global__ void __launch_bounds__(X6Tile<T>::threads, T == 256 ? 1 : 2) k_gemm_x
       // step is one basic block: per accumulator row twelve MFMAs, then its
       // share of the four staging parts.  Products are accumulated smallest
       // first (lo*hi, hi*lo, mid*mid, mid*hi, hi*mid, hi*hi).
-      auto kloop = [&](auto amw_c) {
+      auto kloop = [&](auto amw_c, auto first_c) {
         constexpr int AMW = decltype(amw_c)::value;
+        // 0: each row's staging share after its MFMAs; 1: before them;
+        // 2: all staging before the rows; 3: all staging after the rows
+        constexpr int MODE = decltype(first_c)::value;
+        constexpr bool STAGE_FIRST = MODE == 1;
         for (int s = 0; s < nsteps; s++) {
           const char* cur = xl + (s & 1) * STAGE;
           char* nxt = xl + ((s + 1) & 1) * STAGE;
@@ -253,6 +257,10 @@ __global__ void __launch_bounds__(X6Tile<T>::threads, T == 256 ? 1 : 2) k_gemm_x
               bm[j] = *(const bf16x8*)(cur + 4 * PART + b_off[j]);
               bl[j] = *(const bf16x8*)(cur + 5 * PART + b_off[j]);
             }
+            if constexpr (MODE == 2) {
+#pragma unroll
+              for (int p = 0; p < 4; p++) stage_part(p, nxt, kn);
+            }
             bf16x8 ah[2], am[2], al[2];
             ah[0] = *(const bf16x8*)(cur + a_off[0]);
             am[0] = *(const bf16x8*)(cur + PART + a_off[0]);
@@ -265,6 +273,10 @@ __global__ void __launch_bounds__(X6Tile<T>::threads, T == 256 ? 1 : 2) k_gemm_x
                 al[(i + 1) & 1] = *(const bf16x8*)(cur + 2 * PART + a_off[i + 1]);
               }
               const int c = i & 1;
+              if constexpr (STAGE_FIRST) {
+#pragma unroll
+                for (int p = i * 4 / AMW; p < (i + 1) * 4 / AMW; p++) stage_part(p, nxt, kn);
+              }
 #pragma unroll
               for (int j = 0; j < 2; j++) {
                 acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[c], bh[j], acc[i][j], 0, 0, 0);
@@ -274,19 +286,45 @@ __global__ void __launch_bounds__(X6Tile<T>::threads, T == 256 ? 1 : 2) k_gemm_x
                 acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[c], bm[j], acc[i][j], 0, 0, 0);
                 acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[c], bh[j], acc[i][j], 0, 0, 0);
               }
+              if constexpr (MODE == 0) {
 #pragma unroll
-              for (int p = i * 4 / AMW; p < (i + 1) * 4 / AMW; p++) stage_part(p, nxt, kn);
+                for (int p = i * 4 / AMW; p < (i + 1) * 4 / AMW; p++) stage_part(p, nxt, kn);
+              }
+            }
+            if constexpr (MODE == 3) {
+#pragma unroll
+              for (int p = 0; p < 4; p++) stage_part(p, nxt, kn);
             }
           }
           __syncthreads();
         }
       };
-      if (amw == AM) kloop(IC<AM>{});
-      else if (amw == 0) kloop(IC<0>{});
-      else if (amw == 1) kloop(IC<1>{});
+      // stagger: the two waves of a SIMD (wave w and w + 4: wm = 0 and 1) run
+      // the same K step, so without an offset they reach their MFMAs and their
+      // staging together (MI355X_MICROARCH.md, two waves per SIMD, item 9).
+      // The wm = 1 waves stage first: all four parts before the rows where A
+      // is k-contiguous (forward / dX shapes: half a step of offset), each
+      // row's share before that row for the weight-gradient shapes, whose
+      // row-contiguous operands take the longer offset badly.  Same-box A/B
+      // (scripts/gemm_bench.py, nine GEMMs; the whole step 4007-4012 ->
+      // 4156-4175 frames/s per-row, 4188-4198 half-step for every shape):
+      // half-step fc6 fwd 494-503 -> 480-485, fc6 dX 471-473 -> 450, fc7 dX
+      // 90 -> 82 us but fc6 dW 453 -> 477; per-row fc6 dW 453 -> 446 us.
+      auto kloop_w = [&](auto amw_c) {
+        if constexpr (A_T) {
+          if (wm == 1) kloop(amw_c, IC<1>{});
+          else kloop(amw_c, IC<0>{});
+        } else {
+          if (wm == 1) kloop(amw_c, IC<2>{});
+          else kloop(amw_c, IC<3>{});
+        }
+      };
+      if (amw == AM) kloop_w(IC<AM>{});
+      else if (amw == 0) kloop_w(IC<0>{});
+      else if (amw == 1) kloop_w(IC<1>{});
       else if constexpr (AM >= 4) {
-        if (amw == 2) kloop(IC<2>{});
-        else kloop(IC<3>{});
+        if (amw == 2) kloop_w(IC<2>{});
+        else kloop_w(IC<3>{});
       }
     }
     x_epilogue<T, AM>(g, pl, acc, m0, n0, rl, z, wm, wn, r, hsel);
