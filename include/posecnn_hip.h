@@ -247,6 +247,35 @@ int pcnn_gemm(int M, int N, int K, const float* A, const float* A2, int lda, int
               const int32_t* M_dev, const int32_t* K_dev, int precision, void* workspace, size_t workspace_bytes,
               void* stream);
 
+/* pcnn_gemm plus the pose head's dropout (drop6 / drop7, vgg16_convs.py:189,191;
+ * Network.dropout = tf.nn.dropout, network.py:574-577; keep_prob 0.5 in
+ * training, lib/fcn/train.py:421, 1.0 at test time, test.py:173):
+ *  drop (optional, uint8 (M, ldd >= N), 0 / 1): forward, applied after bias / act
+ *       as tf.nn.dropout computes it: C = (v / keep_prob) * drop
+ *  mask (optional): backward of relu + dropout, with mask = the dropped
+ *       forward activation: C = mask > 0 ? v / keep_prob : 0
+ *       (TF: ReluGrad(features) of (grad * binary) / keep_prob)
+ *  keep_prob in (0, 1]; 1 with drop == NULL is exactly pcnn_gemm. */
+int pcnn_gemm_drop(int M, int N, int K, const float* A, const float* A2, int lda, int a_trans, const float* B,
+                   int ldb, int b_trans, float* Cm, int ldc, const float* bias, int act, const float* mask, int ldm,
+                   const uint8_t* drop, int ldd, float keep_prob, const int32_t* M_dev, const int32_t* K_dev,
+                   int precision, void* workspace, size_t workspace_bytes, void* stream);
+
+/* Dropout keep masks (the binary tensor of tf.nn.dropout: floor(keep_prob + U[0,1))):
+ * mask[r, c] for r < min(*rows_dev, rows) (rows_dev may be NULL), c < cols, row
+ * pitch ld >= cols bytes.  U comes from Philox4x32-10 (key = seed, counter =
+ * (element quad index, *step_dev)) in TF's uint32 -> float construction
+ * ((x & 0x7fffff) | 0x3f800000 as a float, minus 1).  The draw is keyed on the
+ * device-side step counter, so a captured HIP graph draws new masks on every
+ * replay.  TF's own stream assignment is not reproducible (parity unpinned:
+ * the masks are i.i.d. Bernoulli(keep_prob) either way); several masks of one
+ * step take distinct `stream_id`s.  cols % 4 == 0 and ld % 4 == 0. */
+int pcnn_dropout_mask(uint8_t* mask, int rows, int cols, int ld, const int32_t* rows_dev, uint64_t seed,
+                      const int64_t* step_dev, int stream_id, float keep_prob, void* stream);
+
+/* Philox4x32-10 self-check (test infrastructure): out[4 i .. 4 i + 3] = philox(ctr[4 i .. 4 i + 3], key[2 i .. 2 i + 1]). */
+int pcnn_philox_check(const uint32_t* ctr, const uint32_t* key, int n, uint32_t* out, void* stream);
+
 /* Column sums over the first min(*M_dev, M) rows: out[n] = sum_m X[m, n] (bias gradients). */
 int pcnn_colsum(const float* X, int M, int N, int ldx, const int32_t* M_dev, float* out, void* stream);
 

@@ -72,6 +72,12 @@ _SIGS = {
     "pcnn_gemm": (c_int, [c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p,
                           c_int, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_size_t,
                           c_void_p]),
+    "pcnn_gemm_drop": (c_int, [c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_int,
+                               c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_float, c_void_p,
+                               c_void_p, c_int, c_void_p, c_size_t, c_void_p]),
+    "pcnn_dropout_mask": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, ctypes.c_uint64, c_void_p, c_int, c_float,
+                                  c_void_p]),
+    "pcnn_philox_check": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
     "pcnn_colsum": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     "pcnn_box_nms": (c_int, [c_void_p, c_int, c_int, c_void_p, c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
                              c_void_p, c_void_p, c_void_p]),
@@ -166,6 +172,10 @@ def workspace(nbytes, device, tag="default", stream=None):
     key = (str(device), tag, s.cuda_stream)
     buf = _ws.get(key)
     if buf is None or buf.numel() < nbytes:
-        buf = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)
+        # allocated under the launch stream: when a grown buffer replaces the
+        # old one, the caching allocator hands the old block out again only in
+        # order with that stream, whose kernels are the old block's users
+        with torch.cuda.stream(s):
+            buf = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)
         _ws[key] = buf
     return buf

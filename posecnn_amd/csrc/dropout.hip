@@ -1,0 +1,107 @@
+// Dropout keep masks of the pose head (drop6 / drop7, vgg16_convs.py:189,191;
+// Network.dropout -> tf.nn.dropout, network.py:574-577).  tf.nn.dropout draws
+// U ~ [0, 1) per element, keeps floor(keep_prob + U) (the "binary tensor")
+// and returns (x / keep_prob) * binary; the GEMM epilogues of fc6 / fc7 apply
+// that product (gemm_common.h drop_epi), so this kernel only writes the
+// binary tensor, one byte per element.
+//
+// The uniform draw is Philox4x32-10 (Salmon et al., SC'11 -- the generator TF
+// uses for random_uniform on the GPU) with TF's uint32 -> float construction.
+// Key = the caller's 64-bit seed; counter = (element quad index: 2 words,
+// stream id, device-side step counter).  Each lane turns one Philox block into
+// the 4 bytes of one element quad (one 32-bit store).  The step counter lives
+// in device memory so that a captured HIP graph draws fresh masks on every
+// replay (the caller bumps it once per step).
+#include "pcnn_common.h"
+
+namespace {
+
+struct U4 {
+  uint32_t x, y, z, w;
+};
+
+__host__ __device__ __forceinline__ void mulhilo(uint32_t a, uint32_t b, uint32_t& hi, uint32_t& lo) {
+  const uint64_t p = (uint64_t)a * b;
+  hi = (uint32_t)(p >> 32);
+  lo = (uint32_t)p;
+}
+
+// Philox4x32 with 10 rounds (Random123 constants)
+__host__ __device__ __forceinline__ U4 philox4x32_10(U4 c, uint32_t k0, uint32_t k1) {
+  constexpr uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u, W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
+#pragma unroll
+  for (int r = 0; r < 10; r++) {
+    uint32_t h0, l0, h1, l1;
+    mulhilo(M0, c.x, h0, l0);
+    mulhilo(M1, c.z, h1, l1);
+    c = U4{h1 ^ c.y ^ k0, l1, h0 ^ c.w ^ k1, l0};
+    k0 += W0;
+    k1 += W1;
+  }
+  return c;
+}
+
+// TF's Uint32ToFloat (random_distributions.h): 23 random mantissa bits -> [1, 2) - 1
+__device__ __forceinline__ float u01(uint32_t x) { return __uint_as_float((x & 0x7fffffu) | 0x3f800000u) - 1.0f; }
+
+__device__ __forceinline__ uint32_t keep_bit(uint32_t x, float keep) {
+  return floorf(keep + u01(x)) >= 1.0f ? 1u : 0u;
+}
+
+__global__ void __launch_bounds__(256) k_dropout_mask(uint8_t* __restrict__ mask, int rows, int cols, int ld,
+                                                      const int32_t* __restrict__ rows_dev, uint32_t k0, uint32_t k1,
+                                                      const int64_t* __restrict__ step_dev, uint32_t stream_id,
+                                                      float keep) {
+  int R = rows;
+  if (rows_dev) {
+    const int v = *rows_dev;
+    R = v < rows ? (v < 0 ? 0 : v) : rows;
+  }
+  const uint64_t step = step_dev ? (uint64_t)*step_dev : 0;
+  const int q4 = cols >> 2;
+  const long quads = (long)R * q4;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < quads; i += (long)gridDim.x * blockDim.x) {
+    const int r = (int)(i / q4), c = (int)(i - (long)r * q4) * 4;
+    const uint64_t e = (uint64_t)r * (uint64_t)q4 + (uint64_t)(c >> 2);  // element quad of a dense (rows, cols) mask
+    const U4 o = philox4x32_10(U4{(uint32_t)e, (uint32_t)(e >> 32), stream_id, (uint32_t)step}, k0, k1);
+    const uint32_t b = keep_bit(o.x, keep) | keep_bit(o.y, keep) << 8 | keep_bit(o.z, keep) << 16 |
+                       keep_bit(o.w, keep) << 24;
+    *(uint32_t*)(mask + (size_t)r * ld + c) = b;
+  }
+}
+
+__global__ void k_philox_check(const uint32_t* __restrict__ ctr, const uint32_t* __restrict__ key, int n,
+                               uint32_t* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const U4 o = philox4x32_10(U4{ctr[4 * i], ctr[4 * i + 1], ctr[4 * i + 2], ctr[4 * i + 3]}, key[2 * i],
+                             key[2 * i + 1]);
+  out[4 * i] = o.x;
+  out[4 * i + 1] = o.y;
+  out[4 * i + 2] = o.z;
+  out[4 * i + 3] = o.w;
+}
+
+}  // namespace
+
+extern "C" int pcnn_dropout_mask(uint8_t* mask, int rows, int cols, int ld, const int32_t* rows_dev, uint64_t seed,
+                                 const int64_t* step_dev, int stream_id, float keep_prob, void* stream) {
+  PCNN_REQUIRE(mask && rows >= 0 && cols > 0 && cols % 4 == 0 && ld >= cols && ld % 4 == 0 && ((uintptr_t)mask & 3) == 0);
+  PCNN_REQUIRE(keep_prob > 0.f && keep_prob <= 1.f && stream_id >= 0);
+  if (rows == 0) return PCNN_OK;
+  const long quads = (long)rows * (cols / 4);
+  long grid = (quads + 255) / 256;
+  if (grid > 2048) grid = 2048;
+  hipLaunchKernelGGL(k_dropout_mask, dim3((unsigned)grid), dim3(256), 0, (hipStream_t)stream, mask, rows, cols, ld,
+                     rows_dev, (uint32_t)seed, (uint32_t)(seed >> 32), step_dev, (uint32_t)stream_id, keep_prob);
+  PCNN_CHECK_LAUNCH();
+  return PCNN_OK;
+}
+
+extern "C" int pcnn_philox_check(const uint32_t* ctr, const uint32_t* key, int n, uint32_t* out, void* stream) {
+  PCNN_REQUIRE(ctr && key && out && n >= 0);
+  if (n == 0) return PCNN_OK;
+  hipLaunchKernelGGL(k_philox_check, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, ctr, key, n, out);
+  PCNN_CHECK_LAUNCH();
+  return PCNN_OK;
+}

@@ -36,7 +36,21 @@ struct GemmArgs {
   int tile;     // split kernels: tile edge (256 or 128), chosen on the host
   int xgrid;    // split kernels: launch grid (the plan depends on it; k_gemm_reduce re-derives the plan)
   int c_stream; // split kernels: store C non-temporally (outputs far beyond the caches, e.g. the fc6 weight gradient)
+  // dropout (pose_head.hip k_gemm_reduce applies it; the GEMM kernels' own
+  // epilogues never do): C = (v / keep) * drop[m, n] in the forward; with a
+  // mask (the relu + dropout backward) C = (mask > 0 ? v : 0) / keep
+  const uint8_t* drop;
+  int ldd;
+  float keep;  // keep_prob; 1 = no dropout
 };
+
+// The dropout part of the epilogue, after bias / act / mask: tf.nn.dropout's
+// (x / keep_prob) * binary (keep == 1: v / 1 == v, the division is skipped).
+__device__ __forceinline__ float drop_epi(float v, const GemmArgs& g, int m, int n) {
+  if (g.keep != 1.f) v = v / g.keep;
+  if (g.drop) v = v * (float)g.drop[(size_t)m * g.ldd + n];
+  return v;
+}
 
 __device__ __forceinline__ int eff_dim(int full, const int32_t* dev) {
   if (!dev) return full;
@@ -111,6 +125,16 @@ __host__ __device__ __forceinline__ XPlan x_plan(int Meff, int N, int Keff, int 
     }
   }
   return p;
+}
+
+// XCD-aware item order: the dispatcher deals workgroup b to XCD b % 8, so a
+// bijective remap gives each XCD one contiguous run of items (neighbouring
+// tiles share an operand panel through that XCD's L2).  Also for counts that
+// are not a multiple of 8 (fc6 dX: 196 tiles, whose two M tiles per N column
+// used to land on different XCDs and fetch the same W6 panel twice).
+__device__ __forceinline__ int xcd_remap(int b, int n) {
+  const int q = n / 8, r = n % 8, x = b % 8;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
 }
 
 // Operand view for buffer loads: SGPR descriptor + the extent in bytes.  All

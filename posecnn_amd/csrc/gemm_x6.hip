@@ -162,7 +162,11 @@ __global__ void __launch_bounds__(X6Tile<T>::threads, T == 256 ? 1 : 2) k_gemm_x
   // XCD-aware order (as k_gemm_x3): the workgroups of one XCD take consecutive items
   int wg = blockIdx.x;
   if (wg >= active) return;
+#ifndef PCNN_OLD_XCD_MAP
+  wg = xcd_remap(wg, active);
+#else
   if (active % 8 == 0) wg = (wg % 8) * (active / 8) + wg / 8;
+#endif
   const int lane = pcnn::lane_id(), wave = threadIdx.x >> 6;
   const int wm = wave / X::wn, wn = wave % X::wn;
   const int r = lane & 31, hsel = lane >> 5;
@@ -340,11 +344,14 @@ __global__ void __launch_bounds__(X6Tile<T>::threads, T == 256 ? 1 : 2) k_gemm_x
 
 template <int T, bool AT, bool BT, bool RG, bool S2, bool GN>
 void launch_one(const GemmArgs& g, int grid, hipStream_t st) {
-  static bool attr_set = false;
-  if (!attr_set) {
+  // the attribute is per device: one flag per device ordinal
+  static bool attr_set[pcnn::kMaxDevices] = {};
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (dev < 0 || dev >= pcnn::kMaxDevices || !attr_set[dev]) {
     (void)hipFuncSetAttribute((const void*)k_gemm_x6<T, AT, BT, RG, S2, GN>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, X6Tile<T>::lds);
-    attr_set = true;
+    if (dev >= 0 && dev < pcnn::kMaxDevices) attr_set[dev] = true;
   }
   hipLaunchKernelGGL((k_gemm_x6<T, AT, BT, RG, S2, GN>), dim3(grid), dim3(X6Tile<T>::threads), X6Tile<T>::lds, st,
                      g);

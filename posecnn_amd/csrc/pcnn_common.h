@@ -23,6 +23,9 @@
 
 namespace pcnn {
 
+// per-device once-only host state (kernel attributes are set per device)
+constexpr int kMaxDevices = 64;
+
 __device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
 
 __device__ __forceinline__ uint64_t lanemask_lt() {

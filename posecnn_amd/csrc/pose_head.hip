@@ -406,7 +406,11 @@ __global__ void __launch_bounds__(XTile<T>::threads, T == 256 ? 1 : 2) k_gemm_x3
   // shared operand rows meet in one L2
   int wg = blockIdx.x;
   if (wg >= active) return;
+#ifndef PCNN_OLD_XCD_MAP
+  wg = xcd_remap(wg, active);
+#else
   if (active % 8 == 0) wg = (wg % 8) * (active / 8) + wg / 8;
+#endif
   const int lane = pcnn::lane_id(), wave = threadIdx.x >> 6;
   const int wm = wave / X::wn, wn = wave % X::wn;
   const int r = lane & 31, hsel = lane >> 5;
@@ -564,11 +568,24 @@ __global__ void __launch_bounds__(256) k_gemm_reduce(GemmArgs g) {
   const int Meff = eff_dim(g.M, g.M_dev);
   const int Keff = eff_dim(g.K, g.K_dev);
   const int S = g.prec ? x_plan(Meff, g.N, Keff, g.tile, g.xgrid, split_bk(g.prec)).S : split_for(Meff, g.N, Keff);
-  if (S == 1) return;
+  const bool dr = g.drop || g.keep != 1.f;
+  if (S == 1) {
+    // whole tiles: the GEMM's own epilogue wrote bias / act / mask; dropout
+    // (or the backward's 1 / keep) is applied here, in place
+    if (!dr) return;
+    const long total = (long)Meff * g.N;
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+      const int m = (int)(i / g.N), n = (int)(i % g.N);
+      float* c = g.C + (size_t)m * g.ldc + n;
+      *c = drop_epi(*c, g, m, n);
+    }
+    return;
+  }
   // slab sums in slice order z = 0, 1, ... (0 + s0 == s0, so starting from
   // s0 is the same fp32 sum); float4 along N when rows stay 16-B aligned
   const size_t slab_stride = (size_t)g.M * g.N;
   const bool vec = (long)g.M * g.N < (1l << 31) && (g.N & 3) == 0 && (g.ldc & 3) == 0 && (!g.mask || (g.ldm & 3) == 0) &&
+                   (!g.drop || (g.ldd & 3) == 0) &&
                    ((((uintptr_t)g.slab) | ((uintptr_t)g.C) | ((uintptr_t)g.mask) | ((uintptr_t)g.bias)) & 15) == 0;
   if (vec) {
     const int n4 = g.N >> 2;
@@ -581,8 +598,11 @@ __global__ void __launch_bounds__(256) k_gemm_reduce(GemmArgs g) {
         const float4 t = sp[z * (slab_stride >> 2)];
         v.x += t.x; v.y += t.y; v.z += t.z; v.w += t.w;
       }
-      *(float4*)(g.C + (size_t)m * g.ldc + n) = make_float4(epilogue(v.x, g, m, n), epilogue(v.y, g, m, n + 1),
-                                                            epilogue(v.z, g, m, n + 2), epilogue(v.w, g, m, n + 3));
+      float4 o = make_float4(epilogue(v.x, g, m, n), epilogue(v.y, g, m, n + 1), epilogue(v.z, g, m, n + 2),
+                             epilogue(v.w, g, m, n + 3));
+      if (dr) o = make_float4(drop_epi(o.x, g, m, n), drop_epi(o.y, g, m, n + 1), drop_epi(o.z, g, m, n + 2),
+                              drop_epi(o.w, g, m, n + 3));
+      *(float4*)(g.C + (size_t)m * g.ldc + n) = o;
     }
     return;
   }
@@ -591,7 +611,8 @@ __global__ void __launch_bounds__(256) k_gemm_reduce(GemmArgs g) {
     const int m = (int)(i / g.N), n = (int)(i % g.N);
     float v = 0.f;
     for (int z = 0; z < S; z++) v += g.slab[((size_t)z * g.M + m) * g.N + n];
-    g.C[(size_t)m * g.ldc + n] = epilogue(v, g, m, n);
+    v = epilogue(v, g, m, n);
+    g.C[(size_t)m * g.ldc + n] = dr ? drop_epi(v, g, m, n) : v;
   }
 }
 
@@ -707,7 +728,18 @@ extern "C" int pcnn_gemm(int M, int N, int K, const float* A, const float* A2, i
                          int ldb, int b_trans, float* Cm, int ldc, const float* bias, int act, const float* mask,
                          int ldm, const int32_t* M_dev, const int32_t* K_dev, int precision, void* workspace,
                          size_t workspace_bytes, void* stream) {
+  return pcnn_gemm_drop(M, N, K, A, A2, lda, a_trans, B, ldb, b_trans, Cm, ldc, bias, act, mask, ldm, nullptr, 0, 1.f,
+                        M_dev, K_dev, precision, workspace, workspace_bytes, stream);
+}
+
+extern "C" int pcnn_gemm_drop(int M, int N, int K, const float* A, const float* A2, int lda, int a_trans,
+                              const float* B, int ldb, int b_trans, float* Cm, int ldc, const float* bias, int act,
+                              const float* mask, int ldm, const uint8_t* drop, int ldd, float keep_prob,
+                              const int32_t* M_dev, const int32_t* K_dev, int precision, void* workspace,
+                              size_t workspace_bytes, void* stream) {
   PCNN_REQUIRE(M >= 0 && N > 0 && K >= 0 && A && B && Cm);
+  PCNN_REQUIRE(keep_prob > 0.f && keep_prob <= 1.f);
+  PCNN_REQUIRE(!drop || (ldd >= N && (long)M * ldd < (1l << 31)));
   PCNN_REQUIRE(precision >= 0 && precision <= 2);
   PCNN_REQUIRE(lda >= (a_trans ? M : K) && ldb >= (b_trans ? K : N) && ldc >= N);
   PCNN_REQUIRE(!mask || ldm >= N);
@@ -721,7 +753,7 @@ extern "C" int pcnn_gemm(int M, int N, int K, const float* A, const float* A2, i
   if (workspace_bytes < pcnn_gemm_workspace_size(M, N, K, M_dev != nullptr, precision) || !workspace)
     return PCNN_ECAPACITY;
   GemmArgs g{M, N, K, A, A2, lda, B, ldb, Cm, ldc, bias, act, mask, ldm, M_dev, K_dev, (float*)workspace, precision,
-             tile_x3(M, N, K), 0, 0};
+             tile_x3(M, N, K), 0, 0, drop, ldd, keep_prob};
   hipStream_t st = (hipStream_t)stream;
   if (precision == 1 || precision == 2) {
     // ragged edges: a KC operand whose K (or device-side K) is not a multiple of
@@ -756,11 +788,13 @@ extern "C" int pcnn_gemm(int M, int N, int K, const float* A, const float* A2, i
     g.c_stream = (long)M * N * 4 > (256l << 20);
 #define PCNN_X3_LAUNCH_G(TT, AT, BT, RG, S2, GN)                                                              \
   do {                                                                                                          \
-    static bool attr_set = false;                                                                               \
-    if (!attr_set) {                                                                                            \
+    static bool attr_set[pcnn::kMaxDevices] = {};                                                               \
+    int dev_ = 0;                                                                                               \
+    (void)hipGetDevice(&dev_);                                                                                  \
+    if (dev_ < 0 || dev_ >= pcnn::kMaxDevices || !attr_set[dev_]) {                                             \
       (void)hipFuncSetAttribute((const void*)k_gemm_x3<TT, AT, BT, RG, S2, GN>,                                 \
                                 hipFuncAttributeMaxDynamicSharedMemorySize, XTile<TT>::lds);                    \
-      attr_set = true;                                                                                          \
+      if (dev_ >= 0 && dev_ < pcnn::kMaxDevices) attr_set[dev_] = true;                                         \
     }                                                                                                           \
     hipLaunchKernelGGL((k_gemm_x3<TT, AT, BT, RG, S2, GN>), dim3(grid), dim3(XTile<TT>::threads), XTile<TT>::lds, \
                        st, g);                                                                                  \
@@ -789,7 +823,7 @@ extern "C" int pcnn_gemm(int M, int N, int K, const float* A, const float* A2, i
     // split-K slab reduction when the plan can split (a no-op launch is not
     // free: queued behind a persistent GEMM on another stream it holds back
     // everything after it on its own stream)
-    if (may_split) hipLaunchKernelGGL(k_gemm_reduce, dim3(1024), dim3(256), 0, st, g);
+    if (may_split || drop || keep_prob != 1.f) hipLaunchKernelGGL(k_gemm_reduce, dim3(1024), dim3(256), 0, st, g);
     PCNN_CHECK_LAUNCH();
     return PCNN_OK;
   }
@@ -806,7 +840,7 @@ extern "C" int pcnn_gemm(int M, int N, int K, const float* A, const float* A2, i
   // (a static M whose tile count already fills the grid: split 1 for every K).
   // A no-op launch is not free: queued behind a persistent GEMM on another
   // stream it holds back everything after it on its own stream.
-  const bool may_split = M_dev || ((M + BM - 1) / BM) * ((N + BN - 1) / BN) < 256;
+  const bool may_split = M_dev || ((M + BM - 1) / BM) * ((N + BN - 1) / BN) < 256 || drop || keep_prob != 1.f;
   if (may_split) hipLaunchKernelGGL(k_gemm_reduce, dim3(1024), dim3(256), 0, st, g);
   PCNN_CHECK_LAUNCH();
   return PCNN_OK;

@@ -33,15 +33,29 @@ class RoiExchange:
         idx = torch.arange(self.ws * cap, device=device)
         self._rank = idx // cap
         self._local = (idx % cap).to(torch.int32)
+        self._pending = []
 
     def __call__(self, box, pose, num_rois):
         """box (cap,7), pose (cap,7), num_rois (2,) int32 [rows, max(rows,1)].
         Returns (rows (ws*cap, 14) with the global rows first, total (1,) int32)."""
+        self.start(box, pose, num_rois)
+        return self.finish()
+
+    def start(self, box, pose, num_rois):
+        """Issue the two all-gathers asynchronously (the pose step starts them
+        right after the vote; they overlap the rest of the step)."""
         d = self.dist
         self.l_rows[:, :7].copy_(box)
         self.l_rows[:, 7:].copy_(pose)
-        d.all_gather_into_tensor(self.g_counts, num_rois)
-        d.all_gather_into_tensor(self.g_rows, self.l_rows)
+        self._pending = [d.all_gather_into_tensor(self.g_counts, num_rois, async_op=True),
+                         d.all_gather_into_tensor(self.g_rows, self.l_rows, async_op=True)]
+
+    def finish(self):
+        """Join the all-gathers and compact the live rows rank-major on the device."""
+        for w in self._pending:
+            if w is not None:
+                w.wait()
+        self._pending = []
         counts = self.g_counts.view(self.ws, 2)[:, 0]
         offs = torch.cumsum(counts, 0, dtype=torch.int32) - counts  # exclusive scan
         live = self._local < counts[self._rank]

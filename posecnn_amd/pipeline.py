@@ -18,8 +18,11 @@ global row count, so per-rank losses sum to the single-device loss); the
 pose-head weight gradients are reduced by row block through their factors
 (posecnn_amd/exchange.py GradShard: rank r ends with rows_r of the global
 dW6/dW7/dW8 and the full bias gradients); the loss scalar is all-reduced.
-`gather_detections()` all-gathers the detected RoIs + initial poses in
-single-device row order (exchange.RoiExchange).
+The detected RoIs + initial poses are all-gathered in single-device row
+order (exchange.RoiExchange; BASELINE.json configs[3] "RCCL all-gather of
+RoIs/poses"): step() starts the gather right after the vote, it overlaps the
+rest of the step and is joined at the step's end (`self.detections`);
+`gather_detections()` runs the same exchange on its own.
 """
 import torch
 
@@ -37,7 +40,7 @@ class PoseStep:
     def __init__(self, B, H, W, num_classes, device, conv4_hw=None, conv5_hw=None, channels=512, units=4096,
                  is_train=1, skip_pixels=10, vote_threshold=-1.0, vote_percentage=0.02, margin=0.01,
                  global_batch=None, batch_base=0, weights=None, dist=None, backward=True, precision=2,
-                 overlap_weight_grads=True, pixel_argmax=True):
+                 overlap_weight_grads=True, pixel_argmax=True, keep_prob=None, drop_seed=0x5EED):
         self.B, self.H, self.W, self.C = B, H, W, num_classes
         self.dev = device
         self.is_train, self.skip, self.vthr, self.vper, self.margin = is_train, skip_pixels, vote_threshold, \
@@ -93,6 +96,23 @@ class PoseStep:
         if self.gshard is not None:  # this rank's row block of each weight gradient
             for k in ("w6", "w7", "w8"):
                 self.grads[k] = self.grads[k][self.gshard.rows(k)].contiguous()
+        # drop6 / drop7 (vgg16_convs.py:189,191): keep_prob 0.5 in training
+        # (train.py:421), 1 at test time (test.py:173); fused into the fc6 / fc7
+        # epilogues (forward) and the relu-mask epilogues of fc8 / fc7 dX
+        self.keep = float(keep_prob if keep_prob is not None else (0.5 if is_train else 1.0))
+        if not 0.0 < self.keep <= 1.0:
+            raise ValueError("keep_prob must be in (0, 1]")
+        self.drop6 = self.drop7 = None
+        self._drop_external = False
+        if self.keep < 1.0:
+            u8 = dict(dtype=torch.uint8, device=device)
+            self.drop6 = torch.zeros((CAP, units), **u8)
+            self.drop7 = torch.zeros((CAP, units), **u8)
+            self.drop_step = torch.zeros((1,), dtype=torch.int64, device=device)  # Philox counter word, bumped per step
+            rank = dist.get_rank() if dist is not None else 0  # independent masks per rank
+            self.drop_seed = (int(drop_seed) + rank * 0x9E3779B97F4A7C15) & ((1 << 64) - 1)
+            self._drop_ready = None
+            self._drop_ev = torch.cuda.Event()
         self.dconv4 = torch.zeros((B, self.h4, self.w4, channels), **f32)
         self.dconv5 = torch.zeros((B, self.h5, self.w5, channels), **f32)
         self.norm_rows = torch.zeros((1,), **i32)
@@ -100,7 +120,8 @@ class PoseStep:
         # optional {gemm name: [(start_event, end_event), ...]}: HIP events around each FC GEMM on the
         # stream it runs on, with the step's stream overlap left on (the in-step kernel times, bench.py)
         self.gemm_timer = None
-        self.xchg = None  # RoiExchange, built on the first gather_detections()
+        self.xchg = None  # RoiExchange, built on the first sharded step / gather_detections()
+        self.detections = None  # sharded step: (global rows (ws*CAP, 14) = [box | pose], total (1,)) of the last step
         self._pending = {}  # async collectives of the current step
         self._in_step = False  # forward() inside step(): the loss all-reduce is joined at the step's end
         # weight-gradient branch of the backward (None: everything on the caller's stream)
@@ -145,6 +166,34 @@ class PoseStep:
                                            num_rois=h["num_rois"][1:2])
         self._prepped = True
 
+    def set_drop_masks(self, m6, m7):
+        """Use fixed dropout keep masks ((rows, units) 0/1, copied into the
+        capacity buffers) instead of drawing new ones every step (tests)."""
+        if self.keep >= 1.0:
+            raise ValueError("set_drop_masks: the step has keep_prob 1 (no dropout)")
+        for dst, m in ((self.drop6, m6), (self.drop7, m7)):
+            dst.zero_()
+            dst[:m.shape[0]].copy_(m.to(torch.uint8))
+        self._drop_external = True
+
+    def draw_drop_masks(self):
+        """This step's drop6 / drop7 keep masks (Philox, keyed on the device
+        step counter so graph replays draw new ones), on the side stream; the
+        fc6 forward waits for them."""
+        if self.keep >= 1.0 or self._drop_external:
+            return
+        nr = self.hough["num_rois"][1:2]
+        side = self.side_stream if self.timer is None else None
+        if side is not None:
+            side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side or torch.cuda.current_stream()):
+            ph.dropout_mask(self.drop6, self.keep, self.drop_seed, self.drop_step, 6, rows_dev=nr)
+            ph.dropout_mask(self.drop7, self.keep, self.drop_seed, self.drop_step, 7, rows_dev=nr)
+            self.drop_step.add_(1)
+            if side is not None:
+                self._drop_ev.record(side)
+                self._drop_ready = self._drop_ev
+
     def exchange(self):
         """Global ADD-loss normaliser = max(sum of per-rank rows, 1): an
         all-reduce of one int (async; the loss kernel waits for it)."""
@@ -169,9 +218,12 @@ class PoseStep:
         h = self.hough
         if self.dist is None:
             return torch.cat([h["box"], h["pose"]], 1), h["num_rois"][0:1]
+        return self._exchange_rows()(h["box"], h["pose"], h["num_rois"])
+
+    def _exchange_rows(self):
         if self.xchg is None:
             self.xchg = RoiExchange(self.dist, CAP, self.dev)
-        return self.xchg(h["box"], h["pose"], h["num_rois"])
+        return self.xchg
 
     def forward(self, conv4, conv5, points, symmetry):
         h = self.hough
@@ -185,12 +237,16 @@ class PoseStep:
         gs = self.gshard if self.backward else None
         if gs is not None:  # fc6 input column blocks to their owners (overlaps the forward)
             gs.send_input("w6", x)
+        dk = dict(keep_prob=self.keep) if self.keep < 1.0 else {}
+        if self.keep < 1.0 and getattr(self, "_drop_ready", None) is not None:
+            torch.cuda.current_stream().wait_event(self._drop_ready)  # this step's keep masks (side stream)
+            self._drop_ready = None
         with self._t("gemm_fc6_fwd"):
-            self._g("fc6_fwd", x, w.w6, self.y6, bias=w.b6, act=1, M_dev=nr)
+            self._g("fc6_fwd", x, w.w6, self.y6, bias=w.b6, act=1, M_dev=nr, drop=self.drop6, **dk)
         if gs is not None:
             gs.send_input("w7", self.y6)
         with self._t("gemm_fc7_fc8_fwd"):
-            self._g("fc7_fwd", self.y6, w.w7, self.y7, bias=w.b7, act=1, M_dev=nr)
+            self._g("fc7_fwd", self.y6, w.w7, self.y7, bias=w.b7, act=1, M_dev=nr, drop=self.drop7, **dk)
             if gs is not None:
                 gs.send_input("w8", self.y7)
             self._g("fc8_fwd", self.y7, w.w8, self.y8, bias=w.b8, act=0, M_dev=nr)
@@ -255,12 +311,13 @@ class PoseStep:
             ph.head_bwd(self.diff, self.t8, h["weight"], self.pred, self.dy8, num_rois=nr, d_pred_scale=self.one)
         with self._t("gemm_fc8_fc7_dw_bias"):  # fc8 weight / bias gradients
             weight_grads("w8", self.y7, self.dy8, CAP, w.units, self.D)
+        dk = dict(keep_prob=self.keep) if self.keep < 1.0 else {}  # relu + dropout backward: kept grads / keep_prob
         with self._t("gemm_fc8_fc7_dx"):
-            self._g("fc8_dx", self.dy8, w.w8, self.dy7, b_trans=1, mask=self.y7, M_dev=nr)
+            self._g("fc8_dx", self.dy8, w.w8, self.dy7, b_trans=1, mask=self.y7, M_dev=nr, **dk)
         with self._t("gemm_fc8_fc7_dw_bias"):  # fc7 weight / bias gradients
             weight_grads("w7", self.y6, self.dy7, CAP, w.units, w.units)
         with self._t("gemm_fc8_fc7_dx"):
-            self._g("fc7_dx", self.dy7, w.w7, self.dy6, b_trans=1, mask=self.y6, M_dev=nr)
+            self._g("fc7_dx", self.dy7, w.w7, self.dy6, b_trans=1, mask=self.y6, M_dev=nr, **dk)
         with self._t("gemm_fc6_dw"):  # fc6 weight / bias gradients (A = pool5 + pool4)
             weight_grads("w6", x, self.dy6, CAP, K6, w.units)
         with self._t("gemm_fc6_dx"):
@@ -291,8 +348,13 @@ class PoseStep:
 
     def step(self, inputs):
         self.vote(inputs["label"], inputs["vertex"], inputs["extents"], inputs["meta"], inputs["gt"])
+        self.draw_drop_masks()
         self.add_prep(inputs["points"], inputs["symmetry"])
         self.exchange()
+        if self.dist is not None:  # the RoI / pose all-gather: started here, joined at the end of the step
+            with self._t("allgather_rois"):
+                h = self.hough
+                self._exchange_rows().start(h["box"], h["pose"], h["num_rois"])
         self._in_step = True
         try:
             loss = self.forward(inputs["conv4"], inputs["conv5"], inputs["points"], inputs["symmetry"])
@@ -301,4 +363,6 @@ class PoseStep:
         finally:
             self._in_step = False
         self._wait("loss")
+        if self.dist is not None:
+            self.detections = self.xchg.finish()
         return loss

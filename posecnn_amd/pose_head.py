@@ -6,7 +6,9 @@ read on the device (capacity-sized RoI buffers, no host sync).
 Weights follow Network.fc (network.py:393-423): `weights` [in, out] with
 truncated-normal(0, 0.001) init (network.py:415), `biases` [out] zero; the
 reshape of the (R,7,7,512) pooled features is NHWC-flat ((h*7+w)*512+c).
-Dropout is the identity (keep_prob = 1, the test-time graph).
+drop6 / drop7 (vgg16_convs.py:189,191, tf.nn.dropout) are fused into the fc6 /
+fc7 forward epilogues and the relu-mask epilogues of the backward (keep_prob
+0.5 in training, train.py:421; 1, the identity, at test time).
 """
 import torch
 
@@ -14,12 +16,17 @@ from . import _lib
 
 
 def gemm(A, B, C, a_trans=0, b_trans=0, A2=None, bias=None, act=0, mask=None, M_dev=None, K_dev=None, M=None,
-         N=None, K=None, precision=2, stream=None):
-    """C[M,N] = epilogue(op(A) (+ op(A2)) @ op(B)); see pcnn_gemm in include/posecnn_hip.h."""
+         N=None, K=None, precision=2, drop=None, keep_prob=1.0, stream=None):
+    """C[M,N] = epilogue(op(A) (+ op(A2)) @ op(B)); see pcnn_gemm / pcnn_gemm_drop in
+    include/posecnn_hip.h.  drop (uint8 (M, >=N) 0/1) applies tf.nn.dropout after
+    the activation, (v / keep_prob) * drop; with mask, keep_prob scales the kept
+    gradient (v / keep_prob: the backward of relu + dropout)."""
     _lib.require_gpu(A, B, C)
     for t in (A, B, C, A2, bias, mask):
         if t is not None and (t.dtype != torch.float32 or t.stride(-1) != 1):
             raise ValueError("gemm operands must be fp32 with unit inner stride")
+    if drop is not None and (drop.dtype != torch.uint8 or drop.stride(-1) != 1 or not drop.is_cuda):
+        raise ValueError("gemm: drop must be a uint8 device tensor with unit inner stride")
     if M is None:
         M = A.shape[1] if a_trans else A.shape[0]
     if K is None:
@@ -29,12 +36,35 @@ def gemm(A, B, C, a_trans=0, b_trans=0, A2=None, bias=None, act=0, mask=None, M_
     lib = _lib.load()
     ws = _lib.workspace(lib.pcnn_gemm_workspace_size(M, N, K, int(M_dev is not None), precision), C.device, "gemm",
                         stream)
-    rc = lib.pcnn_gemm(M, N, K, _lib.ptr(A), _lib.ptr(A2), A.stride(0), int(a_trans), _lib.ptr(B), B.stride(0),
-                       int(b_trans), _lib.ptr(C), C.stride(0), _lib.ptr(bias), int(act), _lib.ptr(mask),
-                       mask.stride(0) if mask is not None else 0, _lib.ptr(M_dev), _lib.ptr(K_dev), int(precision),
-                       _lib.ptr(ws), ws.numel(), _lib.stream_ptr(stream))
+    if drop is None and keep_prob == 1.0:
+        rc = lib.pcnn_gemm(M, N, K, _lib.ptr(A), _lib.ptr(A2), A.stride(0), int(a_trans), _lib.ptr(B), B.stride(0),
+                           int(b_trans), _lib.ptr(C), C.stride(0), _lib.ptr(bias), int(act), _lib.ptr(mask),
+                           mask.stride(0) if mask is not None else 0, _lib.ptr(M_dev), _lib.ptr(K_dev),
+                           int(precision), _lib.ptr(ws), ws.numel(), _lib.stream_ptr(stream))
+    else:
+        rc = lib.pcnn_gemm_drop(M, N, K, _lib.ptr(A), _lib.ptr(A2), A.stride(0), int(a_trans), _lib.ptr(B),
+                                B.stride(0), int(b_trans), _lib.ptr(C), C.stride(0), _lib.ptr(bias), int(act),
+                                _lib.ptr(mask), mask.stride(0) if mask is not None else 0, _lib.ptr(drop),
+                                drop.stride(0) if drop is not None else 0, float(keep_prob), _lib.ptr(M_dev),
+                                _lib.ptr(K_dev), int(precision), _lib.ptr(ws), ws.numel(), _lib.stream_ptr(stream))
     _lib.check(rc, "gemm")
     return C
+
+
+def dropout_mask(mask, keep_prob, seed, step_dev=None, stream_id=0, rows_dev=None, stream=None):
+    """The binary tensor of tf.nn.dropout, floor(keep_prob + U[0,1)), into the
+    uint8 (rows, cols) `mask` (Philox4x32-10 keyed on seed, the device step
+    counter step_dev (int64 (1,)) and stream_id; rows past *rows_dev untouched)."""
+    _lib.require_gpu(mask)
+    if mask.dtype != torch.uint8 or mask.dim() != 2 or mask.stride(1) != 1:
+        raise ValueError("dropout_mask: uint8 (rows, cols) mask with unit inner stride")
+    if step_dev is not None and (step_dev.dtype != torch.int64 or not step_dev.is_cuda):
+        raise ValueError("dropout_mask: step_dev must be an int64 device tensor")
+    rc = _lib.load().pcnn_dropout_mask(_lib.ptr(mask), mask.shape[0], mask.shape[1], mask.stride(0),
+                                       _lib.ptr(rows_dev), int(seed) & ((1 << 64) - 1), _lib.ptr(step_dev),
+                                       int(stream_id), float(keep_prob), _lib.stream_ptr(stream))
+    _lib.check(rc, "dropout_mask")
+    return mask
 
 
 def colsum(X, out, M_dev=None, stream=None):

@@ -60,6 +60,8 @@ def icp(live, pred_vertices, pred_normals, camera, depth_range=(0.25, 6.0), max_
     dev = pv.device
     update = torch.empty((N, 7), dtype=torch.float32, device=dev)
     pin = _f(pose_in) if pose_in is not None else None
+    if pin is not None and pin.shape != (N, 7):
+        raise ValueError("icp: pose_in must be (N,7)")
     pout = torch.empty((N, 7), dtype=torch.float32, device=dev) if pin is not None else None
     systems = torch.empty((N, iterations, 28), dtype=torch.float32, device=dev) if return_systems else None
     L = _lib.load()
@@ -86,6 +88,8 @@ def icp_center(live, label, obj_ids, vertmap, pred_vertices, pred_normals, max_e
     dev = lv.device
     out = torch.empty((L_, 4), dtype=torch.float32, device=dev)
     pin = _f(pose_in) if pose_in is not None else None
+    if pin is not None and pin.shape != (L_, 7):
+        raise ValueError("icp_center: pose_in must be (L,7)")
     pout = torch.empty((L_, 7), dtype=torch.float32, device=dev) if pin is not None else None
     lib = _lib.load()
     ws = _lib.workspace(lib.pcnn_icp_reduce_workspace_size(L_, H, W), dev, "icp_red", stream)
@@ -101,6 +105,8 @@ def pose_energy(live, label, obj, pred_vertices, poses, depth_range=(0.25, 6.0),
     _lib.require_gpu(live, label, pred_vertices, poses)
     lv, pv, P = _f(live), _f(pred_vertices), _f(poses)
     H, W = lv.shape[-3], lv.shape[-2]
+    if P.dim() != 2 or P.shape[1] != 7 or pv.shape != (H, W, 4) or label.shape[-2:] != (H, W):
+        raise ValueError("pose_energy: poses (K,7), pred_vertices (H,W,4), label (H,W)")
     K = P.shape[0]
     dev = lv.device
     energy = torch.empty((K,), dtype=torch.float32, device=dev)
@@ -118,6 +124,8 @@ def icp_score(live, label, obj, vertmap, hyps, radius=0.01, stream=None):
     _lib.require_gpu(live, label, vertmap, hyps)
     lv, vm, P = _f(live), _f(vertmap), _f(hyps)
     H, W = lv.shape[-3], lv.shape[-2]
+    if P.dim() != 2 or P.shape[1] != 7 or vm.shape[-3:] != (H, W, 3) or label.shape[-2:] != (H, W):
+        raise ValueError("icp_score: hyps (J,7), vertmap (H,W,3), label (H,W)")
     J = P.shape[0]
     dev = lv.device
     score = torch.empty((J,), dtype=torch.float32, device=dev)

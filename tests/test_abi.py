@@ -97,6 +97,15 @@ def test_argument_validation_without_gpu(lib):
     # split-bf16 GEMM needs 16-B aligned operands
     assert lib.pcnn_gemm(4, 4, 4, ctypes.c_void_p(20), nul, 4, 0, ctypes.c_void_p(16), 4, 0, ctypes.c_void_p(16), 4,
                          nul, 0, nul, 0, nul, nul, 1, nul, 0, nul) == 1
+    # gemm with dropout: keep_prob outside (0, 1]; drop pitch below N
+    assert lib.pcnn_gemm_drop(4, 4, 4, ctypes.c_void_p(16), nul, 4, 0, ctypes.c_void_p(16), 4, 0, ctypes.c_void_p(16),
+                              4, nul, 0, nul, 0, nul, 0, ctypes.c_float(0.0), nul, nul, 2, nul, 0, nul) == 1
+    assert lib.pcnn_gemm_drop(4, 4, 4, ctypes.c_void_p(16), nul, 4, 0, ctypes.c_void_p(16), 4, 0, ctypes.c_void_p(16),
+                              4, nul, 0, nul, 0, ctypes.c_void_p(16), 2, ctypes.c_float(0.5), nul, nul, 2, nul, 0,
+                              nul) == 1
+    # dropout masks: columns not a multiple of 4; keep_prob 0
+    assert lib.pcnn_dropout_mask(ctypes.c_void_p(16), 4, 6, 8, nul, 1, nul, 0, ctypes.c_float(0.5), nul) == 1
+    assert lib.pcnn_dropout_mask(ctypes.c_void_p(16), 4, 8, 8, nul, 1, nul, 0, ctypes.c_float(0.0), nul) == 1
     # roi pool: unknown layout
     assert lib.pcnn_roi_pool_fwd(ctypes.c_void_p(16), 1, 8, 8, 4, 7, ctypes.c_void_p(16), 1, 5, 0, nul, 1.0, 7, 7, 0,
                                  ctypes.c_void_p(16), ctypes.c_void_p(16), nul) == 1

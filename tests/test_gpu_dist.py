@@ -120,7 +120,7 @@ def _run(fr, sl, global_batch, batch_base, d):
     inputs.update(extents=t(fr["extents"]), gt=t(fr["gt"]), points=t(fr["points"]), symmetry=t(fr["symmetry"]))
     nb = inputs["label"].shape[0]
     step = PoseStep(nb, H, W, C, dev, channels=CH, units=UNITS, is_train=1, skip_pixels=3,
-                    global_batch=global_batch, batch_base=batch_base, dist=d)
+                    global_batch=global_batch, batch_base=batch_base, dist=d, keep_prob=1.0)
     for _ in range(2):  # second step: stale rows of the first must not leak into the gradients
         step.step(inputs)
     torch.cuda.synchronize()

@@ -29,7 +29,13 @@ def _close(a, ref, rt=1e-4):
     np.testing.assert_allclose(a, ref, rtol=rt, atol=rt * float(np.abs(ref).max()))
 
 
-def test_pose_step_vs_fp64_autograd(hip, orc):
+@pytest.mark.parametrize("drop", ["none", "philox", "external"])
+def test_pose_step_vs_fp64_autograd(hip, orc, drop):
+    """drop: "none" = keep_prob 1 (the test-time graph); "philox" = keep_prob
+    0.5 with the step's own drawn masks; "external" = keep_prob 0.5 with masks
+    supplied through set_drop_masks.  The fp64 graph applies drop6 / drop7 as
+    tf.nn.dropout does, (x / keep_prob) * binary (vgg16_convs.py:189,191), and
+    autograd gives TF's backward of it."""
     fr = synth.make_frames(B, H=H, W=W, num_classes=C, objects_per_image=4, seed=91)
     g = torch.Generator().manual_seed(3)
     conv4 = torch.randn((B, H // 8, W // 8, CH), generator=g)
@@ -38,7 +44,13 @@ def test_pose_step_vs_fp64_autograd(hip, orc):
     t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(D)
     inputs = dict(label=t(fr["label"]), vertex=t(fr["vertex"]), extents=t(fr["extents"]), meta=t(fr["meta"]),
                   gt=t(fr["gt"]), conv4=conv4.to(D), conv5=conv5.to(D), points=t(pts), symmetry=t(sym))
-    step = PoseStep(B, H, W, C, D, channels=CH, units=UNITS, is_train=1, skip_pixels=3)
+    keep = 1.0 if drop == "none" else 0.5
+    step = PoseStep(B, H, W, C, D, channels=CH, units=UNITS, is_train=1, skip_pixels=3, keep_prob=keep)
+    if drop == "external":
+        gm = torch.Generator().manual_seed(11)
+        cap = step.drop6.shape[0]
+        step.set_drop_masks((torch.rand((cap, UNITS), generator=gm) < 0.5).to(D),
+                            (torch.rand((cap, UNITS), generator=gm) < 0.5).to(D))
     # non-zero biases so the bias epilogues and column sums are exercised
     w = step.weights
     for b in (w.b6, w.b7, w.b8):
@@ -53,8 +65,18 @@ def test_pose_step_vs_fp64_autograd(hip, orc):
     W6, W7, W8 = (f64(v).requires_grad_() for v in (w.w6, w.w7, w.w8))
     b6, b7, b8 = (f64(v).requires_grad_() for v in (w.b6, w.b7, w.b8))
     x.requires_grad_()
-    y6 = torch.relu(x @ W6 + b6)
-    y7 = torch.relu(y6 @ W7 + b7)
+    if keep < 1.0:
+        m6, m7 = f64(step.drop6[:n]), f64(step.drop7[:n])
+        for m_ in (m6, m7):  # Bernoulli(keep_prob) masks
+            assert set(np.unique(m_.numpy())) <= {0.0, 1.0}
+            assert abs(float(m_.mean()) - keep) < 0.03
+        if drop == "philox":
+            assert not torch.equal(m6, m7)
+    else:
+        m6 = m7 = None
+    dropout = lambda y, m_: y if m_ is None else (y / keep) * m_  # tf.nn.dropout
+    y6 = dropout(torch.relu(x @ W6 + b6), m6)
+    y7 = dropout(torch.relu(y6 @ W7 + b7), m7)
     y8 = y7 @ W8 + b8
     pw = f64(step.hough["weight"][:n])
     m = torch.tanh(y8) * pw

@@ -6,7 +6,8 @@ conv5_3 with 512 channels, 4096-unit fc6 / fc7 (vgg16_convs.py:167-200), the
 default fp32-faithful GEMMs.  Checked, on the step's own intermediate values:
   * the Hough rows against the oracle (bit-exact);
   * pool5 + pool4 against the oracle's two RoI pools (bit-exact sum);
-  * each layer of the head (y6, y7, y8, pred; dy8, dy7, dy6, dX and every
+  * each layer of the head with drop6 / drop7 at keep_prob 0.5 on
+    externally supplied masks (y6, y7, y8, pred; dy8, dy7, dy6, dX and every
     weight / bias gradient) against float64 (torch on the GPU) of that
     layer on the step's own fp32 inputs, at fp32-GEMM tolerance (2e-5 of the
     tensor's scale); the ADD loss / gradient against the oracle (1e-4, its
@@ -51,7 +52,15 @@ def test_configs2_full_step(hip, orc):
     fr = synth.make_frames(B, H, W, num_classes=C, objects_per_image=6, seed=3)
     pts, sym = synth.rescaled_points(C)
     inp = _inputs(fr, (60, 80), (30, 40), pts, sym, 1234)
-    step = PoseStep(B, H, W, C, D, is_train=1, skip_pixels=10)
+    step = PoseStep(B, H, W, C, D, is_train=1, skip_pixels=10)  # train: drop6 / drop7 at keep_prob 0.5
+    keep = step.keep
+    assert keep == 0.5
+    # externally supplied dropout keep masks (the step's Philox draw is checked in test_gpu_step.py)
+    gm = torch.Generator(device=D)
+    gm.manual_seed(17)
+    m6 = torch.rand((step.drop6.shape[0], 4096), generator=gm, device=D) < keep
+    m7 = torch.rand((step.drop7.shape[0], 4096), generator=gm, device=D) < keep
+    step.set_drop_masks(m6, m7)
     w = step.weights
     gb = torch.Generator(device=D)
     gb.manual_seed(5)
@@ -67,6 +76,7 @@ def test_configs2_full_step(hip, orc):
                                               -1.0, 0.02, 10)
     assert on == n
     np.testing.assert_array_equal(step.hough["box"][:n].cpu().numpy(), ob)
+    np.testing.assert_array_equal(step.hough["pose"][:n].cpu().numpy(), op)
     np.testing.assert_array_equal(step.hough["target"][:n].cpu().numpy(), ot)
     np.testing.assert_array_equal(step.hough["weight"][:n].cpu().numpy(), ow)
 
@@ -82,8 +92,10 @@ def test_configs2_full_step(hip, orc):
     f = lambda t_: t_[:n].double()
     x = step.pool[:n].reshape(n, -1).double()
     W6, W7, W8 = (v.double() for v in (w.w6, w.w7, w.w8))
-    _close(step.y6[:n], torch.relu(x @ W6 + w.b6.double()), 2e-5)
-    _close(step.y7[:n], torch.relu(f(step.y6) @ W7 + w.b7.double()), 2e-5)
+    d6, d7 = m6[:n].double(), m7[:n].double()
+    dropout = lambda y, m_: (y / keep) * m_  # tf.nn.dropout (network.py:574-577)
+    _close(step.y6[:n], dropout(torch.relu(x @ W6 + w.b6.double()), d6), 2e-5)
+    _close(step.y7[:n], dropout(torch.relu(f(step.y6) @ W7 + w.b7.double()), d7), 2e-5)
     _close(step.y8[:n], f(step.y7) @ W8 + w.b8.double(), 2e-5)
     y8 = f(step.y8).requires_grad_()
     pw = step.hough["weight"][:n].double()
@@ -101,10 +113,11 @@ def test_configs2_full_step(hip, orc):
     dy8, dy7, dy6 = f(step.dy8), f(step.dy7), f(step.dy6)
     _close(gr["w8"], f(step.y7).T @ dy8, 2e-5)
     _close(gr["b8"], dy8.sum(0), 2e-5)
-    _close(step.dy7[:n], (dy8 @ W8.T) * (step.y7[:n] > 0), 2e-5)
+    # TF's backward of relu -> dropout: ReluGrad((g * binary) / keep_prob); y7 is the dropped activation
+    _close(step.dy7[:n], (dy8 @ W8.T) * d7 / keep * (step.y7[:n] > 0), 2e-5)
     _close(gr["w7"], f(step.y6).T @ dy7, 2e-5)
     _close(gr["b7"], dy7.sum(0), 2e-5)
-    _close(step.dy6[:n], (dy7 @ W7.T) * (step.y6[:n] > 0), 2e-5)
+    _close(step.dy6[:n], (dy7 @ W7.T) * d6 / keep * (step.y6[:n] > 0), 2e-5)
     _close(gr["w6"], x.T @ dy6, 2e-5)
     _close(gr["b6"], dy6.sum(0), 2e-5)
     _close(step.dx[:n], dy6 @ W6.T, 2e-5)
