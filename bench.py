@@ -88,9 +88,12 @@ def main():
     t0 = time.time()
     if linemod:
         G_BP, CH_BP = 64, 64
-        voxel = ([2.0 / G_BP, 1.5 / G_BP, 1.7 / G_BP], [-1.0, -0.75, 0.4])
+        # the voxel grid spans the camera frustum over the scene's 0.9-2.1 m depth range
+        voxel = ([1.2 / G_BP, 0.9 / G_BP, 1.2 / G_BP], [-0.6, -0.45, 0.9])
+        # RGB-D frames: depth at every pixel (objects over a floor plane), so surfaces cross the voxel grid
         fr = synth.make_frames(B, H, W, num_classes=C, objects_per_image=4, seed=seed, image_offset=rank * B,
-                               extents=synth.models()["linemod_extents"], with_depth=True, voxel=voxel)
+                               extents=synth.models()["linemod_extents"], with_depth=True, voxel=voxel,
+                               depth_background=(1.0, 2.0))
     else:
         fr = synth.make_frames(B, H, W, num_classes=C, objects_per_image=6, seed=seed, image_offset=rank * B)
     log(f"[rank {rank}] synthetic frames in {time.time() - t0:.1f}s")
@@ -359,7 +362,7 @@ def main():
                          "fp32-faithful)",
                       1: "f32 (FC GEMMs split-bf16x3 MFMA, fp32 accumulate)", 0: "f32"}[args.precision],
             "data": "synthetic (seeded label/vertex maps per minibatch.py:517-575; random conv4_3/conv5_3; "
-                    "random-init FC weights" + ("; LINEMOD box-surface model points, rendered box depth, random "
+                    "random-init FC weights" + ("; LINEMOD box-surface model points, rendered box depth over a floor plane, random "
                                                 "backprojection features" if linemod else "") + ")",
             "config": {
                 "workload": ("configs[4]: LINEMOD 15-class hough_voting_gpu(train) + roi_pool x2 + fc6/7/8 + "

@@ -364,3 +364,26 @@ def icp_score(live, label, obj, vertmap, hyps, radius=0.01):
     lib().orc_icp_score(lp, labp, int(obj), vmp, H, W, Pp, P.shape[0], ctypes.c_float(radius),
                         sc.ctypes.data_as(F32P), ch.ctypes.data_as(I32P))
     return sc, int(ch[0])
+
+
+def pose2d(label, vertmap, extents, fx, fy, px, py, seed=1305, n_hyp=256, max_iter=100000):
+    """Synthesizer::estimatePose2D restated (orc_pose2d.cpp).  Returns dict:
+    poses (3, 4, C) in the reference's output layout, hyps (n_hyp, 13)
+    [objID | R | t], hyp_px (n_hyp, 4) sampled pixels, inliers (n_hyp, 8)
+    per preemptive round, final (C, 3) [h, inliers, hypotheses], n_obj."""
+    label, lp = _i(label)
+    vertmap, vp = _f(vertmap)
+    extents, ep = _f(extents)
+    H, W = label.shape
+    C = extents.shape[0]
+    poses = np.zeros((3, 4, C), np.float32)
+    hyps = np.zeros((n_hyp, 13), np.float32)
+    hpx = np.zeros((n_hyp, 4), np.int32)
+    inl = np.zeros((n_hyp, 8), np.int32)
+    fin = np.zeros((C, 3), np.int32)
+    lib().orc_pose2d.restype = ctypes.c_int
+    n = lib().orc_pose2d(lp, vp, ep, H, W, C, ctypes.c_float(fx), ctypes.c_float(fy), ctypes.c_float(px),
+                         ctypes.c_float(py), ctypes.c_uint64(seed), n_hyp, max_iter, poses.ctypes.data_as(F32P),
+                         hyps.ctypes.data_as(F32P), hpx.ctypes.data_as(I32P), inl.ctypes.data_as(I32P),
+                         fin.ctypes.data_as(I32P))
+    return dict(poses=poses, hyps=hyps, hyp_px=hpx, inliers=inl, final=fin, n_obj=n)

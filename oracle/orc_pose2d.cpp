@@ -1,0 +1,403 @@
+// ORACLE — TEST INFRASTRUCTURE ONLY (see orc_common.h).
+//
+// RGB-only pose estimation of the reference's test-time path (SURVEY.md §8(f)
+// row 4, RANSAC half): Synthesizer::estimatePose2D
+// (lib/synthesize/synthesize.cpp:1571-1766), reached through
+// synthesizer.pyx:74-82 estimate_poses_2d from lib/fcn/test.py:1364
+// (cfg.TEST.VERTEX_REG_3D: the vertex map holds object coordinates scaled to
+// [0, 1] by the class extents).  Restated pieces:
+//   getLabels (:1010-1031, column-major traversal, > minArea = 400 px),
+//   getBb3Ds / getBB3D (:1035-1048, detection.h:45-64),
+//   getMode3D (:1052-1071), pointLineDistance (:1074-1080),
+//   samplePoint2D (:1084-1104), hypothesis sampling (:1616-1688),
+//   getBB2D (detection.h:78-109), the preemptive loop (:1693-1727) with
+//   countInliers2D (:1171-1214; std::mt19937 default seed and
+//   std::negative_binomial_distribution<int>(1, maxPixels / N) pixel skips),
+//   getWorkingQueue (:1150-1160), and the output layout (:1729-1764).
+// Deliberate, documented choices (parity unpinned: OpenCV, NLopt absent):
+//   * RNG: hypothesis h draws from its own Philox4x32-10 stream (key = seed,
+//     counter = (draw, h, 'P2D', 0)), uniform ints by rejection; the
+//     reference's per-thread mt19937 streams (thread_rand.cpp) are assigned
+//     to hypotheses by the OpenMP schedule, i.e. nondeterministically.
+//   * Hypotheses are stored in ascending h (the reference appends in
+//     completion order under omp critical); the per-round sort is stable
+//     (inliers descending, then h): one legal order of std::sort's ties.
+//   * cv::solvePnP(CV_P3P) is restated as Grunert's P3P (distance ratios
+//     u = s2/s1, v = s3/s1; the quartic in v from eliminating u, its roots by
+//     Durand-Kerner iteration polished by Newton steps), the camera-frame
+//     triangle aligned to the model triangle by orthonormal triads, and the
+//     solution whose reprojection of the 4th point is closest kept -- as
+//     OpenCV's p3p.cpp selects it.
+//   * The preemptive "refinement" in estimatePose2D calls updateHyp3D
+//     (:1722), which returns at once in the 2-D path (inlierPts -- the 3-D
+//     correspondences -- stay empty, :1374), and refineWithOpt's optEnergy2D
+//     divides by that empty list's size (:1457): every energy is inf or NaN,
+//     so NLopt keeps the start point.  The final pose is therefore the winning
+//     hypothesis's P3P pose; both steps are restated as the identity.
+//   * The sampling loop is capped at max_iter draws per hypothesis (the
+//     reference: 10,000,000).
+#include "orc_common.h"
+#include <algorithm>
+#include <complex>
+#include <random>
+#include <vector>
+
+namespace {
+
+// ---- Philox4x32-10 (Salmon et al., SC'11; Random123 constants) -------------
+struct U4 { uint32_t v[4]; };
+U4 philox(U4 c, uint32_t k0, uint32_t k1) {
+  for (int r = 0; r < 10; r++) {
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c.v[0], p1 = (uint64_t)0xCD9E8D57u * c.v[2];
+    U4 o;
+    o.v[0] = (uint32_t)(p1 >> 32) ^ c.v[1] ^ k0;
+    o.v[1] = (uint32_t)p1;
+    o.v[2] = (uint32_t)(p0 >> 32) ^ c.v[3] ^ k1;
+    o.v[3] = (uint32_t)p0;
+    c = o;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return c;
+}
+
+struct Stream {
+  uint32_t k0, k1, h, ctr = 0;
+  int word = 4;
+  U4 buf;
+  Stream(uint64_t seed, uint32_t hyp) : k0((uint32_t)seed), k1((uint32_t)(seed >> 32)), h(hyp) {}
+  uint32_t next() {
+    if (word == 4) {
+      buf = philox(U4{{ctr++, h, 0x50324400u, 0u}}, k0, k1);
+      word = 0;
+    }
+    return buf.v[word++];
+  }
+  // uniform in [0, n): reject the top 2^32 mod n values
+  int uniform(int n) {
+    const uint32_t un = (uint32_t)n;
+    const uint32_t lim = (uint32_t)(0x100000000ull - (0x100000000ull % un));
+    uint32_t x;
+    do { x = next(); } while (lim != 0 && x >= lim);
+    return (int)(x % un);
+  }
+};
+
+struct V3 { double x, y, z; };
+V3 operator-(V3 a, V3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+V3 operator+(V3 a, V3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+V3 operator*(double s, V3 a) { return {s * a.x, s * a.y, s * a.z}; }
+double dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+V3 cross(V3 a, V3 b) { return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x}; }
+double nrm(V3 a) { return std::sqrt(dot(a, a)); }
+
+struct F3 { float x, y, z; };  // cv::Point3f
+
+struct Pose { double R[9]; double t[3]; };
+
+struct Cam { double fx, fy, px, py; };
+
+// cv::projectPoints without distortion (OpenCV's cvProjectPoints2 order)
+void project(const Pose& P, V3 X, const Cam& k, double& u, double& v) {
+  const double* R = P.R;
+  const double x = R[0] * X.x + R[1] * X.y + R[2] * X.z + P.t[0];
+  const double y = R[3] * X.x + R[4] * X.y + R[5] * X.z + P.t[1];
+  double z = R[6] * X.x + R[7] * X.y + R[8] * X.z + P.t[2];
+  z = z != 0.0 ? 1.0 / z : 1.0;
+  u = x * z * k.fx + k.px;
+  v = y * z * k.fy + k.py;
+}
+
+// getMode3D (synthesize.cpp:1052-1071): the object coordinate of pixel p
+F3 mode3d(const float* vertmap, const float* extents, int C, int objID, int p) {
+  const float* m = vertmap + (size_t)p * 3 * C + 3 * objID;
+  float o[3];
+  for (int i = 0; i < 3; i++) {
+    const float vmin = -extents[objID * 3 + i] / 2, vmax = extents[objID * 3 + i] / 2;
+    const float a = (float)(1.0 / (double)(vmax - vmin));
+    const float b = (float)(-1.0 * (double)vmin / (double)(vmax - vmin));
+    o[i] = (m[i] - b) / a;
+  }
+  return {o[0], o[1], o[2]};
+}
+
+double norm3f(F3 a, F3 b) {  // cv::norm(Point3f - Point3f)
+  const float dx = a.x - b.x, dy = a.y - b.y, dz = a.z - b.z;
+  return std::sqrt((double)dx * dx + (double)dy * dy + (double)dz * dz);
+}
+
+double point_line(F3 p1, F3 p2, F3 p3) {  // :1074-1080, float vector ops, double norms
+  const F3 a{p2.x - p1.x, p2.y - p1.y, p2.z - p1.z}, b{p3.x - p1.x, p3.y - p1.y, p3.z - p1.z};
+  const F3 c{a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
+  const double nc = std::sqrt((double)c.x * c.x + (double)c.y * c.y + (double)c.z * c.z);
+  const double na = std::sqrt((double)a.x * a.x + (double)a.y * a.y + (double)a.z * a.z);
+  return nc / na;
+}
+
+// ---- Grunert's P3P ----------------------------------------------------------
+// real roots of c[4] v^4 + ... + c[0]
+int quartic_roots(const double* c, double* out) {
+  const double a4 = c[4];
+  double mx = 0;
+  for (int i = 0; i < 4; i++) mx = std::max(mx, std::fabs(c[i]));
+  if (!(std::fabs(a4) > 1e-12 * mx)) return 0;
+  double a[4];
+  for (int i = 0; i < 4; i++) a[i] = c[i] / a4;
+  double bound = 1;
+  for (int i = 0; i < 4; i++) bound = std::max(bound, 1 + std::fabs(a[i]));
+  typedef std::complex<double> cd;
+  cd z[4];
+  const cd seed(0.4, 0.9);
+  cd w(1, 0);
+  for (int k = 0; k < 4; k++) { z[k] = w * bound; w *= seed; }
+  auto pe = [&](cd x) { return (((x + a[3]) * x + a[2]) * x + a[1]) * x + a[0]; };
+  for (int it = 0; it < 200; it++)
+    for (int k = 0; k < 4; k++) {
+      cd den(1, 0);
+      for (int j = 0; j < 4; j++)
+        if (j != k) den *= (z[k] - z[j]);
+      if (den == cd(0, 0)) continue;
+      z[k] -= pe(z[k]) / den;
+    }
+  int n = 0;
+  for (int k = 0; k < 4; k++) {
+    if (!(std::fabs(z[k].imag()) <= 1e-6 * (1 + std::abs(z[k])))) continue;
+    double x = z[k].real();
+    for (int it = 0; it < 4; it++) {  // Newton polish on the real quartic
+      const double p = (((x + a[3]) * x + a[2]) * x + a[1]) * x + a[0];
+      const double dp = ((4 * x + 3 * a[3]) * x + 2 * a[2]) * x + a[1];
+      if (dp == 0) break;
+      x -= p / dp;
+    }
+    out[n++] = x;
+  }
+  return n;
+}
+
+void polymul(const double* a, int na, const double* b, int nb, double* out) {  // coefficient arrays, low first
+  for (int i = 0; i < na + nb - 1; i++) out[i] = 0;
+  for (int i = 0; i < na; i++)
+    for (int j = 0; j < nb; j++) out[i + j] += a[i] * b[j];
+}
+
+// Triad alignment of the model triangle P onto the camera-frame triangle Q
+Pose triad(const V3* P, const V3* Q) {
+  auto frame = [](const V3* X, V3* e) {
+    e[0] = (1.0 / nrm(X[1] - X[0])) * (X[1] - X[0]);
+    V3 w = X[2] - X[0];
+    w = w - dot(w, e[0]) * e[0];
+    e[1] = (1.0 / nrm(w)) * w;
+    e[2] = cross(e[0], e[1]);
+  };
+  V3 e[3], f[3];
+  frame(P, e);
+  frame(Q, f);
+  Pose o;
+  const double fe[3][3] = {{f[0].x, f[1].x, f[2].x}, {f[0].y, f[1].y, f[2].y}, {f[0].z, f[1].z, f[2].z}};
+  const double ee[3][3] = {{e[0].x, e[1].x, e[2].x}, {e[0].y, e[1].y, e[2].y}, {e[0].z, e[1].z, e[2].z}};
+  for (int r = 0; r < 3; r++)
+    for (int c = 0; c < 3; c++) o.R[3 * r + c] = fe[r][0] * ee[c][0] + fe[r][1] * ee[c][1] + fe[r][2] * ee[c][2];
+  const V3 RP{o.R[0] * P[0].x + o.R[1] * P[0].y + o.R[2] * P[0].z, o.R[3] * P[0].x + o.R[4] * P[0].y + o.R[5] * P[0].z,
+              o.R[6] * P[0].x + o.R[7] * P[0].y + o.R[8] * P[0].z};
+  o.t[0] = Q[0].x - RP.x;
+  o.t[1] = Q[0].y - RP.y;
+  o.t[2] = Q[0].z - RP.z;
+  return o;
+}
+
+// solvePnP(..., CV_P3P) on 4 correspondences: solve with points 0-2, keep the
+// solution whose reprojection of point 3 is closest
+bool p3p(const F3* X, const float (*m)[2], const Cam& k, Pose& best) {
+  V3 P[4], j[4];
+  for (int i = 0; i < 4; i++) {
+    P[i] = {X[i].x, X[i].y, X[i].z};
+    const V3 r{((double)m[i][0] - k.px) / k.fx, ((double)m[i][1] - k.py) / k.fy, 1.0};
+    j[i] = (1.0 / nrm(r)) * r;
+  }
+  const double a = nrm(P[1] - P[2]), b = nrm(P[0] - P[2]), c = nrm(P[0] - P[1]);
+  const double ca = dot(j[1], j[2]), cb = dot(j[0], j[2]), cg = dot(j[0], j[1]);
+  const double a2 = a * a, b2 = b * b, c2 = c * c;
+  if (!(b2 > 0)) return false;
+  const double K1 = (a2 - c2) / b2, Kc = c2 / b2;
+  const double Nv[3] = {1 + K1, -2 * K1 * cb, K1 - 1};  // u * D(v) = N(v)
+  const double Dv[2] = {2 * cg, -2 * ca};
+  const double qv[3] = {1 - Kc, 2 * Kc * cb, -Kc};       // 1 - (c^2/b^2)(1 + v^2 - 2 v cos b)
+  double NN[5], ND[4], DD[3], qDD[5];
+  polymul(Nv, 3, Nv, 3, NN);
+  polymul(Nv, 3, Dv, 2, ND);
+  polymul(Dv, 2, Dv, 2, DD);
+  polymul(qv, 3, DD, 3, qDD);
+  double poly[5];
+  for (int i = 0; i < 5; i++) poly[i] = NN[i] - 2 * cg * (i < 4 ? ND[i] : 0) + qDD[i];
+  double roots[4];
+  const int nr = quartic_roots(poly, roots);
+  double best_err = -1;
+  for (int r = 0; r < nr; r++) {
+    const double v = roots[r];
+    const double D = 2 * (cg - v * ca);
+    if (std::fabs(D) < 1e-12) continue;
+    const double u = ((K1 - 1) * v * v - 2 * K1 * cb * v + 1 + K1) / D;
+    const double q = 1 + v * v - 2 * v * cb;
+    if (!(q > 0) || !(u > 0) || !(v > 0)) continue;
+    const double s1 = std::sqrt(b2 / q);
+    const V3 Q[3] = {s1 * j[0], (u * s1) * j[1], (v * s1) * j[2]};
+    const Pose cand = triad(P, Q);
+    double pu, pv;
+    project(cand, P[3], k, pu, pv);
+    const double e = (pu - m[3][0]) * (pu - m[3][0]) + (pv - m[3][1]) * (pv - m[3][1]);
+    if (!(e == e)) continue;
+    if (best_err < 0 || e < best_err) { best_err = e; best = cand; }
+  }
+  return best_err >= 0;
+}
+
+// getBB2D (detection.h:78-109) area: float projections, int truncation, clamp
+int bb_area(const Pose& P, const F3* bb3, const Cam& k, int W, int H) {
+  int minX = W - 1, maxX = 0, minY = H - 1, maxY = 0;
+  for (int i = 0; i < 8; i++) {
+    double u, v;
+    project(P, {bb3[i].x, bb3[i].y, bb3[i].z}, k, u, v);
+    const float fu = (float)u, fv = (float)v;
+    minX = orc::f2i_sat(std::min((float)minX, fu));
+    minY = orc::f2i_sat(std::min((float)minY, fv));
+    maxX = orc::f2i_sat(std::max((float)maxX, fu));
+    maxY = orc::f2i_sat(std::max((float)maxY, fv));
+  }
+  auto cl = [](int x, int lo, int hi) { return x < lo ? lo : (x > hi ? hi : x); };
+  minX = cl(minX, 0, W - 1); maxX = cl(maxX, 0, W - 1);
+  minY = cl(minY, 0, H - 1); maxY = cl(maxY, 0, H - 1);
+  return (maxX - minX + 1) * (maxY - minY + 1);
+}
+
+struct Hyp { int h, obj, inliers = 0; Pose pose; };
+
+}  // namespace
+
+// hyps_out (n_hyp, 13): [objID (or -1), R (9, row-major), t (3)]; hyp_px (n_hyp, 4)
+// sampled pixel indices; inl_out (n_hyp, 8) inlier count of each preemptive
+// round (-1 when the hypothesis was no longer in the queue); final_out (C, 3)
+// [h, inliers, hypotheses of the class] of the surviving hypothesis (-1 when
+// none); poses_out (3, 4, C) the reference's output layout.  Returns the
+// number of classes that took part (object_ids).
+ORC_API int orc_pose2d(const int* label, const float* vertmap, const float* extents, int H, int W, int C, float fx,
+                       float fy, float px, float py, uint64_t seed, int n_hyp, int max_iter, float* poses_out,
+                       float* hyps_out, int* hyp_px, int* inl_out, int* final_out) {
+  const Cam k{fx, fy, px, py};
+  std::vector<std::vector<int>> labels(C);
+  for (int x = 0; x < W; x++)
+    for (int y = 0; y < H; y++) labels[label[y * W + x]].push_back(y * W + x);
+  std::vector<int> objs;
+  for (int c = 1; c < C; c++)
+    if ((float)labels[c].size() > 400.0f) objs.push_back(c);
+  for (int i = 0; i < n_hyp * 13; i++) hyps_out[i] = 0;
+  for (int i = 0; i < n_hyp; i++) hyps_out[i * 13] = -1;
+  for (int i = 0; i < n_hyp * 4; i++) hyp_px[i] = -1;
+  for (int i = 0; i < n_hyp * 8; i++) inl_out[i] = -1;
+  for (int i = 0; i < C * 3; i++) final_out[i] = -1;
+  if (objs.empty()) return 0;
+  std::vector<std::vector<Hyp>> hypmap(C);
+  for (int h = 0; h < n_hyp; h++) {
+    Stream rs(seed, (uint32_t)h);
+    for (int it = 0; it < max_iter; it++) {
+      const int obj = objs[rs.uniform((int)objs.size())];
+      const auto& L = labels[obj];
+      float m[4][2];
+      F3 X[4];
+      int px4[4], n = 0;
+      bool ok = true;
+      for (int s = 0; s < 4 && ok; s++) {  // samplePoint2D x 4
+        const int idx = L[rs.uniform((int)L.size())];
+        const float u = (float)(idx % W), v = (float)(idx / W);
+        double md = -1;
+        for (int q = 0; q < n; q++) {
+          const float dx = m[q][0] - u, dy = m[q][1] - v;
+          const double d = std::sqrt((double)dx * dx + (double)dy * dy);
+          md = md < 0 ? d : std::min(md, d);
+        }
+        if (md > 0 && md < 10) { ok = false; break; }
+        const F3 o = mode3d(vertmap, extents, C, obj, idx);
+        if (o.x == 0 && o.y == 0 && o.z == 0) { ok = false; break; }
+        md = -1;
+        for (int q = 0; q < n; q++) {
+          const double d = norm3f(X[q], o);
+          md = md < 0 ? d : std::min(md, d);
+        }
+        if (md > 0 && md < 0.01) { ok = false; break; }
+        m[n][0] = u; m[n][1] = v; X[n] = o; px4[n] = idx; n++;
+      }
+      if (!ok) continue;
+      if (point_line(X[0], X[1], X[2]) < 0.01 || point_line(X[0], X[1], X[3]) < 0.01 ||
+          point_line(X[0], X[2], X[3]) < 0.01 || point_line(X[1], X[2], X[3]) < 0.01)
+        continue;
+      Pose P;
+      if (!p3p(X, m, k, P)) continue;
+      bool out = false;
+      for (int q = 0; q < 4 && !out; q++) {
+        double u, v;
+        project(P, {X[q].x, X[q].y, X[q].z}, k, u, v);
+        const float du = m[q][0] - (float)u, dv = m[q][1] - (float)v;  // Point2f difference
+        if (!(std::sqrt((double)du * du + (double)dv * dv) < 10)) out = true;
+      }
+      if (out) continue;
+      const float e0 = extents[obj * 3] * 0.5f, e1 = extents[obj * 3 + 1] * 0.5f, e2 = extents[obj * 3 + 2] * 0.5f;
+      const F3 bb3[8] = {{e0, e1, e2}, {-e0, e1, e2}, {e0, -e1, e2}, {-e0, -e1, e2},
+                         {e0, e1, -e2}, {-e0, e1, -e2}, {e0, -e1, -e2}, {-e0, -e1, -e2}};
+      if ((float)bb_area(P, bb3, k, W, H) < 400.0f) continue;
+      Hyp hy;
+      hy.h = h; hy.obj = obj; hy.pose = P;
+      hypmap[obj].push_back(hy);
+      hyps_out[h * 13] = (float)obj;
+      for (int i = 0; i < 9; i++) hyps_out[h * 13 + 1 + i] = (float)P.R[i];
+      for (int i = 0; i < 3; i++) hyps_out[h * 13 + 10 + i] = (float)P.t[i];
+      for (int i = 0; i < 4; i++) hyp_px[h * 4 + i] = px4[i];
+      break;
+    }
+  }
+  // preemptive loop: every class runs 8 rounds (<= 256 hypotheses halve to
+  // one in at most 8; a lone hypothesis is counted until refSteps reaches 8)
+  for (int c = 0; c < C; c++) {
+    auto& hs = hypmap[c];
+    if (hs.empty()) continue;
+    const auto& L = labels[c];
+    const int N = (int)L.size();
+    for (int round = 1; round <= 8; round++) {
+      const int maxPixels = 1000 * round;
+      const float rate = maxPixels / (float)N;
+      std::vector<int> sub;
+      std::mt19937 gen;
+      std::negative_binomial_distribution<int> nb(1, rate < 1 ? rate : 0.5f);
+      for (int i = 0; i < N;) {
+        sub.push_back(i);
+        if (rate < 1) i += std::max(1, nb(gen));
+        else i++;
+      }
+      for (auto& hy : hs) {
+        int cnt = 0;
+        for (int i : sub) {
+          const int idx = L[i];
+          const double u0 = idx % W, v0 = idx / W;
+          const F3 o = mode3d(vertmap, extents, C, c, idx);
+          double u, v;
+          project(hy.pose, {o.x, o.y, o.z}, k, u, v);
+          if (std::sqrt((u0 - u) * (u0 - u) + (v0 - v) * (v0 - v)) < 10.0f) cnt++;
+        }
+        hy.inliers = cnt;
+        inl_out[hy.h * 8 + round - 1] = cnt;
+      }
+      if (hs.size() > 1) {
+        std::stable_sort(hs.begin(), hs.end(), [](const Hyp& a, const Hyp& b) { return a.inliers > b.inliers; });
+        hs.erase(hs.begin() + hs.size() / 2, hs.end());
+      }
+    }
+    const Hyp& w = hs[0];
+    final_out[c * 3] = w.h;
+    final_out[c * 3 + 1] = w.inliers;
+    int nh = 0;
+    for (int h = 0; h < n_hyp; h++) nh += hyps_out[h * 13] == (float)c;
+    final_out[c * 3 + 2] = nh;
+    for (int y = 0; y < 3; y++)
+      for (int x = 0; x < 4; x++)
+        poses_out[c + C * (y * 4 + x)] = x < 3 ? (float)w.pose.R[y * 3 + x] : (float)w.pose.t[y];
+  }
+  return (int)objs.size();
+}

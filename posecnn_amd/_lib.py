@@ -78,6 +78,10 @@ _SIGS = {
     "pcnn_dropout_mask": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, ctypes.c_uint64, c_void_p, c_int, c_float,
                                   c_void_p]),
     "pcnn_philox_check": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
+    "pcnn_pose2d_workspace_size": (c_size_t, [c_int, c_int, c_int, c_int]),
+    "pcnn_pose2d": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_float, c_float, c_float,
+                            ctypes.c_uint64, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                            c_size_t, c_void_p]),
     "pcnn_colsum": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     "pcnn_box_nms": (c_int, [c_void_p, c_int, c_int, c_void_p, c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
                              c_void_p, c_void_p, c_void_p]),

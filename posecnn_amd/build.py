@@ -13,7 +13,7 @@ OBJ = os.path.join(HERE, "build")
 OUT = os.path.join(HERE, "libposecnn_hip.so")
 SOURCES = ["capi.hip", "hough_compact.hip", "hough_vote.hip", "hough_peak.hip", "hough_emit.hip", "roi_pooling.hip",
            "average_distance.hip", "backprojecting.hip", "pose_head.hip", "gemm_x6.hip", "box_nms.hip",
-           "label_producer.hip", "icp.hip", "dropout.hip"]
+           "label_producer.hip", "icp.hip", "dropout.hip", "pose2d.hip"]
 HEADERS = [os.path.join(CSRC, "pcnn_common.h"), os.path.join(CSRC, "hough_common.h"), os.path.join(CSRC, "gemm_common.h"),
            os.path.join(HERE, "..", "include", "posecnn_hip.h")]
 # -ffp-contract=off: the parity arithmetic rounds every float op separately

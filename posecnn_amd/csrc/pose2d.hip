@@ -1,0 +1,622 @@
+// RGB-only pose estimation: Synthesizer::estimatePose2D
+// (lib/synthesize/synthesize.cpp:1571-1766, synthesizer.pyx:74-82, called from
+// lib/fcn/test.py:1364 under cfg.TEST.VERTEX_REG_3D) -- preemptive RANSAC
+// over 2-D / 3-D correspondences from an object-coordinate vertex map.
+//
+// The reference runs it on the host: 256 hypotheses sampled by OpenMP threads
+// (4 random pixels of one object, P3P, a reprojection and box-area check),
+// then 8 preemptive rounds of inlier counting over a growing random subset of
+// the object's pixels (std::mt19937 + negative_binomial skips), each round
+// keeping the better half.  Here:
+//   k_p2d_colcount / k_p2d_scan / k_p2d_scatter  the per-class pixel lists in
+//       the reference's column-major order (getLabels, :1010-1031): per-column
+//       class counts, a per-class scan over columns, an ordered scatter;
+//   host: the class counts come back once (object_ids need > 400 pixels), and
+//       the 8 rounds' pixel subsets of each object are drawn with the
+//       reference's own generator (a default-seeded std::mt19937 and
+//       std::negative_binomial_distribution<int>(1, maxPixels / N) per round,
+//       :1183-1213 -- identical for every hypothesis of the round) and copied
+//       up once;
+//   k_p2d_hyps: one lane per hypothesis runs the rejection-sampling loop
+//       (samplePoint2D x 4, degeneracy tests, Grunert P3P in double, the
+//       reprojection and getBB2D area checks) on its own Philox stream;
+//   k_p2d_ransac: one workgroup per object runs the 8 rounds: its waves count
+//       inliers of the surviving hypotheses over the round's subset (double
+//       projections, one hypothesis per wave at a time), a stable rank sort
+//       keeps the better half, and the survivor's pose is written in the
+//       reference's (3, 4, C) layout.
+// The reference's refinement steps are inert in this path (updateHyp3D on an
+// empty 3-D inlier list, optEnergy2D divided by that list's size: NLopt keeps
+// the start point) and are not run; the oracle (oracle/orc_pose2d.cpp)
+// documents the same reading.
+#include "pcnn_common.h"
+#include <climits>
+#include <algorithm>
+#include <random>
+#include <vector>
+
+namespace {
+
+constexpr int kRounds = 8;       // <= 256 hypotheses halve to one in <= 8 rounds; refIt = 8 (:1601)
+constexpr int kRansacThreads = 256;
+constexpr int kMaxHypBlock = 1024;
+
+struct U4 { uint32_t x, y, z, w; };
+
+__device__ __forceinline__ U4 philox(U4 c, uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; r++) {
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c.x, p1 = (uint64_t)0xCD9E8D57u * c.z;
+    c = U4{(uint32_t)(p1 >> 32) ^ c.y ^ k0, (uint32_t)p1, (uint32_t)(p0 >> 32) ^ c.w ^ k1, (uint32_t)p0};
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return c;
+}
+
+// hypothesis h's draws: Philox4x32-10 block (draw / 4, h, 'P2D', 0), words in order
+struct Stream {
+  uint32_t k0, k1, h, ctr;
+  int word;
+  U4 buf;
+  __device__ Stream(uint64_t seed, uint32_t hyp) : k0((uint32_t)seed), k1((uint32_t)(seed >> 32)), h(hyp), ctr(0),
+                                                   word(4), buf{0, 0, 0, 0} {}
+  __device__ uint32_t next() {
+    if (word == 4) {
+      buf = philox(U4{ctr++, h, 0x50324400u, 0u}, k0, k1);
+      word = 0;
+    }
+    const uint32_t v = word == 0 ? buf.x : word == 1 ? buf.y : word == 2 ? buf.z : buf.w;
+    word++;
+    return v;
+  }
+  __device__ int uniform(int n) {  // [0, n) by rejection of the top 2^32 mod n values
+    const uint32_t un = (uint32_t)n;
+    const uint32_t lim = (uint32_t)(0x100000000ull - (0x100000000ull % un));
+    uint32_t x;
+    do { x = next(); } while (lim != 0 && x >= lim);
+    return (int)(x % un);
+  }
+};
+
+struct D3 { double x, y, z; };
+__device__ __forceinline__ D3 sub(D3 a, D3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+__device__ __forceinline__ D3 scl(double s, D3 a) { return {s * a.x, s * a.y, s * a.z}; }
+__device__ __forceinline__ double dot(D3 a, D3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+__device__ __forceinline__ D3 cross(D3 a, D3 b) {
+  return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
+}
+__device__ __forceinline__ double nrm(D3 a) { return sqrt(dot(a, a)); }
+
+struct F3 { float x, y, z; };
+struct Pose { double R[9], t[3]; };
+struct Cam { double fx, fy, px, py; };
+
+// cv::projectPoints, no distortion (cvProjectPoints2's operation order)
+__device__ __forceinline__ void project(const Pose& P, D3 X, const Cam& k, double& u, double& v) {
+  const double x = P.R[0] * X.x + P.R[1] * X.y + P.R[2] * X.z + P.t[0];
+  const double y = P.R[3] * X.x + P.R[4] * X.y + P.R[5] * X.z + P.t[1];
+  double z = P.R[6] * X.x + P.R[7] * X.y + P.R[8] * X.z + P.t[2];
+  z = z != 0.0 ? 1.0 / z : 1.0;
+  u = x * z * k.fx + k.px;
+  v = y * z * k.fy + k.py;
+}
+
+// getMode3D (:1052-1071): undo the [0, 1] extent scaling of the object coordinate
+__device__ __forceinline__ F3 mode3d(const float* __restrict__ vm, const float* __restrict__ ext, int C, int obj, int p) {
+  const float* m = vm + (size_t)p * 3 * C + 3 * obj;
+  float o[3];
+#pragma unroll
+  for (int i = 0; i < 3; i++) {
+    const float vmin = -ext[obj * 3 + i] / 2, vmax = ext[obj * 3 + i] / 2;
+    const float a = (float)(1.0 / (double)(vmax - vmin));
+    const float b = (float)(-1.0 * (double)vmin / (double)(vmax - vmin));
+    o[i] = (m[i] - b) / a;
+  }
+  return {o[0], o[1], o[2]};
+}
+
+__device__ __forceinline__ double norm3f(F3 a, F3 b) {
+  const float dx = a.x - b.x, dy = a.y - b.y, dz = a.z - b.z;
+  return sqrt((double)dx * dx + (double)dy * dy + (double)dz * dz);
+}
+
+__device__ __forceinline__ double point_line(F3 p1, F3 p2, F3 p3) {  // :1074-1080
+  const F3 a{p2.x - p1.x, p2.y - p1.y, p2.z - p1.z}, b{p3.x - p1.x, p3.y - p1.y, p3.z - p1.z};
+  const F3 c{a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
+  return sqrt((double)c.x * c.x + (double)c.y * c.y + (double)c.z * c.z) /
+         sqrt((double)a.x * a.x + (double)a.y * a.y + (double)a.z * a.z);
+}
+
+// complex helpers for the Durand-Kerner iteration
+struct Cx { double re, im; };
+__device__ __forceinline__ Cx cadd(Cx a, Cx b) { return {a.re + b.re, a.im + b.im}; }
+__device__ __forceinline__ Cx csub(Cx a, Cx b) { return {a.re - b.re, a.im - b.im}; }
+__device__ __forceinline__ Cx cmul(Cx a, Cx b) { return {a.re * b.re - a.im * b.im, a.re * b.im + a.im * b.re}; }
+__device__ __forceinline__ Cx cdiv(Cx a, Cx b) {
+  const double d = b.re * b.re + b.im * b.im;
+  return {(a.re * b.re + a.im * b.im) / d, (a.im * b.re - a.re * b.im) / d};
+}
+
+// real roots of c4 v^4 + ... + c0 (Durand-Kerner, then Newton polish)
+__device__ int quartic_roots(const double* c, double* out) {
+  double mx = 0;
+  for (int i = 0; i < 4; i++) mx = fmax(mx, fabs(c[i]));
+  if (!(fabs(c[4]) > 1e-12 * mx)) return 0;
+  double a[4];
+  for (int i = 0; i < 4; i++) a[i] = c[i] / c[4];
+  double bound = 1;
+  for (int i = 0; i < 4; i++) bound = fmax(bound, 1 + fabs(a[i]));
+  Cx z[4];
+  Cx w{1, 0};
+  const Cx sd{0.4, 0.9};
+  for (int k = 0; k < 4; k++) {
+    z[k] = {w.re * bound, w.im * bound};
+    w = cmul(w, sd);
+  }
+  for (int it = 0; it < 200; it++)
+    for (int k = 0; k < 4; k++) {
+      Cx den{1, 0};
+      for (int j = 0; j < 4; j++)
+        if (j != k) den = cmul(den, csub(z[k], z[j]));
+      if (den.re == 0 && den.im == 0) continue;
+      Cx p = cadd(z[k], Cx{a[3], 0});
+      p = cadd(cmul(p, z[k]), Cx{a[2], 0});
+      p = cadd(cmul(p, z[k]), Cx{a[1], 0});
+      p = cadd(cmul(p, z[k]), Cx{a[0], 0});
+      z[k] = csub(z[k], cdiv(p, den));
+    }
+  int n = 0;
+  for (int k = 0; k < 4; k++) {
+    const double az = sqrt(z[k].re * z[k].re + z[k].im * z[k].im);
+    if (!(fabs(z[k].im) <= 1e-6 * (1 + az))) continue;
+    double x = z[k].re;
+    for (int it = 0; it < 4; it++) {
+      const double p = (((x + a[3]) * x + a[2]) * x + a[1]) * x + a[0];
+      const double dp = ((4 * x + 3 * a[3]) * x + 2 * a[2]) * x + a[1];
+      if (dp == 0) break;
+      x -= p / dp;
+    }
+    out[n++] = x;
+  }
+  return n;
+}
+
+__device__ Pose triad(const D3* P, const D3* Q) {
+  D3 e[3], f[3];
+  {
+    e[0] = scl(1.0 / nrm(sub(P[1], P[0])), sub(P[1], P[0]));
+    D3 w = sub(P[2], P[0]);
+    w = sub(w, scl(dot(w, e[0]), e[0]));
+    e[1] = scl(1.0 / nrm(w), w);
+    e[2] = cross(e[0], e[1]);
+  }
+  {
+    f[0] = scl(1.0 / nrm(sub(Q[1], Q[0])), sub(Q[1], Q[0]));
+    D3 w = sub(Q[2], Q[0]);
+    w = sub(w, scl(dot(w, f[0]), f[0]));
+    f[1] = scl(1.0 / nrm(w), w);
+    f[2] = cross(f[0], f[1]);
+  }
+  Pose o;
+  const double fe[3][3] = {{f[0].x, f[1].x, f[2].x}, {f[0].y, f[1].y, f[2].y}, {f[0].z, f[1].z, f[2].z}};
+  const double ee[3][3] = {{e[0].x, e[1].x, e[2].x}, {e[0].y, e[1].y, e[2].y}, {e[0].z, e[1].z, e[2].z}};
+  for (int r = 0; r < 3; r++)
+    for (int c = 0; c < 3; c++) o.R[3 * r + c] = fe[r][0] * ee[c][0] + fe[r][1] * ee[c][1] + fe[r][2] * ee[c][2];
+  const double rp0 = o.R[0] * P[0].x + o.R[1] * P[0].y + o.R[2] * P[0].z;
+  const double rp1 = o.R[3] * P[0].x + o.R[4] * P[0].y + o.R[5] * P[0].z;
+  const double rp2 = o.R[6] * P[0].x + o.R[7] * P[0].y + o.R[8] * P[0].z;
+  o.t[0] = Q[0].x - rp0;
+  o.t[1] = Q[0].y - rp1;
+  o.t[2] = Q[0].z - rp2;
+  return o;
+}
+
+__device__ void polymul(const double* a, int na, const double* b, int nb, double* out) {
+  for (int i = 0; i < na + nb - 1; i++) out[i] = 0;
+  for (int i = 0; i < na; i++)
+    for (int j = 0; j < nb; j++) out[i + j] += a[i] * b[j];
+}
+
+// solvePnP(CV_P3P) on 4 correspondences (Grunert's P3P with points 0-2, the
+// solution reprojecting point 3 closest), as the oracle restates it
+__device__ bool p3p(const F3* X, const float (*m)[2], const Cam& k, Pose& best) {
+  D3 P[4], j[4];
+  for (int i = 0; i < 4; i++) {
+    P[i] = {X[i].x, X[i].y, X[i].z};
+    const D3 r{((double)m[i][0] - k.px) / k.fx, ((double)m[i][1] - k.py) / k.fy, 1.0};
+    j[i] = scl(1.0 / nrm(r), r);
+  }
+  const double a = nrm(sub(P[1], P[2])), b = nrm(sub(P[0], P[2])), c = nrm(sub(P[0], P[1]));
+  const double ca = dot(j[1], j[2]), cb = dot(j[0], j[2]), cg = dot(j[0], j[1]);
+  const double a2 = a * a, b2 = b * b, c2 = c * c;
+  if (!(b2 > 0)) return false;
+  const double K1 = (a2 - c2) / b2, Kc = c2 / b2;
+  const double Nv[3] = {1 + K1, -2 * K1 * cb, K1 - 1};
+  const double Dv[2] = {2 * cg, -2 * ca};
+  const double qv[3] = {1 - Kc, 2 * Kc * cb, -Kc};
+  double NN[5], ND[4], DD[3], qDD[5];
+  polymul(Nv, 3, Nv, 3, NN);
+  polymul(Nv, 3, Dv, 2, ND);
+  polymul(Dv, 2, Dv, 2, DD);
+  polymul(qv, 3, DD, 3, qDD);
+  double poly[5];
+  for (int i = 0; i < 5; i++) poly[i] = NN[i] - 2 * cg * (i < 4 ? ND[i] : 0) + qDD[i];
+  double roots[4];
+  const int nr = quartic_roots(poly, roots);
+  double best_err = -1;
+  for (int r = 0; r < nr; r++) {
+    const double v = roots[r];
+    const double D = 2 * (cg - v * ca);
+    if (fabs(D) < 1e-12) continue;
+    const double u = ((K1 - 1) * v * v - 2 * K1 * cb * v + 1 + K1) / D;
+    const double q = 1 + v * v - 2 * v * cb;
+    if (!(q > 0) || !(u > 0) || !(v > 0)) continue;
+    const double s1 = sqrt(b2 / q);
+    const D3 Q[3] = {scl(s1, j[0]), scl(u * s1, j[1]), scl(v * s1, j[2])};
+    const Pose cand = triad(P, Q);
+    double pu, pv;
+    project(cand, P[3], k, pu, pv);
+    const double e = (pu - m[3][0]) * (pu - m[3][0]) + (pv - m[3][1]) * (pv - m[3][1]);
+    if (!(e == e)) continue;
+    if (best_err < 0 || e < best_err) {
+      best_err = e;
+      best = cand;
+    }
+  }
+  return best_err >= 0;
+}
+
+__device__ __forceinline__ int f2i_sat(float f) {  // C++ float -> int, defined for every input
+  if (f != f) return 0;
+  if (f >= 2147483648.0f) return INT_MAX;
+  if (f <= -2147483648.0f) return INT_MIN;
+  return (int)f;
+}
+
+// getBB2D (detection.h:78-109) area
+__device__ int bb_area(const Pose& P, const float* ext, int obj, const Cam& k, int W, int H) {
+  const float e0 = ext[obj * 3] * 0.5f, e1 = ext[obj * 3 + 1] * 0.5f, e2 = ext[obj * 3 + 2] * 0.5f;
+  int minX = W - 1, maxX = 0, minY = H - 1, maxY = 0;
+  for (int i = 0; i < 8; i++) {  // getBB3D corner order (detection.h:53-61)
+    const float cx = (i & 1) ? -e0 : e0, cy = (i & 2) ? -e1 : e1, cz = (i & 4) ? -e2 : e2;
+    double u, v;
+    project(P, D3{cx, cy, cz}, k, u, v);
+    const float fu = (float)u, fv = (float)v;
+    minX = f2i_sat(fminf((float)minX, fu));
+    minY = f2i_sat(fminf((float)minY, fv));
+    maxX = f2i_sat(fmaxf((float)maxX, fu));
+    maxY = f2i_sat(fmaxf((float)maxY, fv));
+  }
+  minX = min(max(minX, 0), W - 1);
+  maxX = min(max(maxX, 0), W - 1);
+  minY = min(max(minY, 0), H - 1);
+  maxY = min(max(maxY, 0), H - 1);
+  return (maxX - minX + 1) * (maxY - minY + 1);
+}
+
+struct P2dWs {
+  int32_t* colcnt;   // (C, W) class pixels per column
+  int32_t* coloff;   // (C, W) exclusive scan over columns
+  int32_t* count;    // (C)
+  int32_t* lists;    // (H W) per-class pixel lists, column-major, classes concatenated
+  int32_t* listoff;  // (C) list offsets (host-computed)
+  int32_t* objs;     // (C) object ids (host-computed)
+  int32_t* sub;      // subsets: indices into the class list, rounds concatenated per object
+  int32_t* suboff;   // (n_obj, kRounds + 1)
+  double* hyp;       // (n_hyp, 16): obj, R (9), t (3)
+};
+
+__global__ void k_p2d_colcount(const int32_t* __restrict__ label, int H, int W, int C, int32_t* colcnt) {
+  const int x = blockIdx.x * blockDim.x + threadIdx.x;
+  if (x >= W) return;
+  for (int y = 0; y < H; y++) {
+    const int c = label[y * W + x];
+    if (c >= 0 && c < C) colcnt[c * W + x]++;  // one thread per column: no contention
+  }
+}
+
+__global__ void __launch_bounds__(1024) k_p2d_scan(const int32_t* __restrict__ colcnt, int W, int32_t* coloff,
+                                                   int32_t* count) {
+  __shared__ int part[1024];
+  const int c = blockIdx.x;
+  int carry = 0;
+  for (int base = 0; base < W; base += 1024) {
+    const int x = base + threadIdx.x;
+    const int v = x < W ? colcnt[c * W + x] : 0;
+    part[threadIdx.x] = v;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {  // Hillis-Steele inclusive scan
+      const int add = threadIdx.x >= o ? part[threadIdx.x - o] : 0;
+      __syncthreads();
+      part[threadIdx.x] += add;
+      __syncthreads();
+    }
+    if (x < W) coloff[c * W + x] = carry + part[threadIdx.x] - v;
+    carry += part[1023];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) count[c] = carry;
+}
+
+__global__ void __launch_bounds__(64) k_p2d_scatter(const int32_t* __restrict__ label, int H, int W, int C, P2dWs ws) {
+  extern __shared__ int run[];  // [C][64] running counts of this block's columns
+  const int x = blockIdx.x * 64 + threadIdx.x;
+  for (int c = 0; c < C; c++) run[c * 64 + threadIdx.x] = 0;
+  if (x >= W) return;
+  for (int y = 0; y < H; y++) {
+    const int c = label[y * W + x];
+    if (c < 0 || c >= C) continue;
+    const int r = run[c * 64 + threadIdx.x]++;
+    ws.lists[ws.listoff[c] + ws.coloff[c * W + x] + r] = y * W + x;
+  }
+}
+
+// One lane per hypothesis: the sampling loop of :1616-1688
+__global__ void __launch_bounds__(64) k_p2d_hyps(const float* __restrict__ vm, const float* __restrict__ ext, int H,
+                                                 int W, int C, Cam k, uint64_t seed, int n_hyp, int n_obj,
+                                                 int max_iter, P2dWs ws, float* __restrict__ hyps_out,
+                                                 int32_t* __restrict__ hyp_px) {
+  const int h = blockIdx.x * blockDim.x + threadIdx.x;
+  if (h >= n_hyp) return;
+  double* hr = ws.hyp + (size_t)h * 16;
+  hr[0] = -1;
+  hyps_out[(size_t)h * 13] = -1.f;
+  for (int i = 1; i < 13; i++) hyps_out[(size_t)h * 13 + i] = 0.f;
+  for (int i = 0; i < 4; i++) hyp_px[h * 4 + i] = -1;
+  Stream rs(seed, (uint32_t)h);
+  for (int it = 0; it < max_iter; it++) {
+    const int obj = ws.objs[rs.uniform(n_obj)];
+    const int* L = ws.lists + ws.listoff[obj];
+    const int N = ws.count[obj];
+    float m[4][2];
+    F3 X[4];
+    int px4[4], n = 0;
+    bool ok = true;
+    for (int s = 0; s < 4 && ok; s++) {  // samplePoint2D (:1084-1104)
+      const int idx = L[rs.uniform(N)];
+      const float u = (float)(idx % W), v = (float)(idx / W);
+      double md = -1;
+      for (int q = 0; q < n; q++) {
+        const float dx = m[q][0] - u, dy = m[q][1] - v;
+        const double d = sqrt((double)dx * dx + (double)dy * dy);
+        md = md < 0 ? d : fmin(md, d);
+      }
+      if (md > 0 && md < 10) { ok = false; break; }
+      const F3 o = mode3d(vm, ext, C, obj, idx);
+      if (o.x == 0 && o.y == 0 && o.z == 0) { ok = false; break; }
+      md = -1;
+      for (int q = 0; q < n; q++) {
+        const double d = norm3f(X[q], o);
+        md = md < 0 ? d : fmin(md, d);
+      }
+      if (md > 0 && md < 0.01) { ok = false; break; }
+      m[n][0] = u;
+      m[n][1] = v;
+      X[n] = o;
+      px4[n] = idx;
+      n++;
+    }
+    if (!ok) continue;
+    if (point_line(X[0], X[1], X[2]) < 0.01 || point_line(X[0], X[1], X[3]) < 0.01 ||
+        point_line(X[0], X[2], X[3]) < 0.01 || point_line(X[1], X[2], X[3]) < 0.01)
+      continue;
+    Pose P;
+    if (!p3p(X, m, k, P)) continue;
+    bool out = false;
+    for (int q = 0; q < 4 && !out; q++) {  // the 4 samples must reproject within 10 px (:1664-1672)
+      double u, v;
+      project(P, D3{X[q].x, X[q].y, X[q].z}, k, u, v);
+      const float du = m[q][0] - (float)u, dv = m[q][1] - (float)v;
+      if (!(sqrt((double)du * du + (double)dv * dv) < 10)) out = true;
+    }
+    if (out) continue;
+    if ((float)bb_area(P, ext, obj, k, W, H) < 400.0f) continue;  // :1678-1680
+    hr[0] = obj;
+    for (int i = 0; i < 9; i++) hr[1 + i] = P.R[i];
+    for (int i = 0; i < 3; i++) hr[10 + i] = P.t[i];
+    hyps_out[(size_t)h * 13] = (float)obj;
+    for (int i = 0; i < 9; i++) hyps_out[(size_t)h * 13 + 1 + i] = (float)P.R[i];
+    for (int i = 0; i < 3; i++) hyps_out[(size_t)h * 13 + 10 + i] = (float)P.t[i];
+    for (int i = 0; i < 4; i++) hyp_px[h * 4 + i] = px4[i];
+    return;
+  }
+}
+
+// One workgroup per object: the preemptive rounds of :1693-1727 and the output of :1729-1764
+__global__ void __launch_bounds__(kRansacThreads) k_p2d_ransac(const float* __restrict__ vm, const float* __restrict__ ext,
+                                                               int W, int C, Cam k, int n_hyp, P2dWs ws,
+                                                               int32_t* __restrict__ inl_out,
+                                                               int32_t* __restrict__ final_out,
+                                                               float* __restrict__ poses_out) {
+  __shared__ int hl[kMaxHypBlock], hcnt[kMaxHypBlock], tmp[kMaxHypBlock];
+  __shared__ int s_m;
+  const int oi = blockIdx.x;
+  const int obj = ws.objs[oi];
+  const int* L = ws.lists + ws.listoff[obj];
+  const int lane = pcnn::lane_id(), wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  // this object's hypotheses in ascending h (stored order, see the oracle)
+  if (threadIdx.x == 0) {
+    int m = 0;
+    for (int h = 0; h < n_hyp; h++)
+      if (ws.hyp[(size_t)h * 16] == (double)obj && m < kMaxHypBlock) hl[m++] = h;
+    s_m = m;
+  }
+  __syncthreads();
+  int m = s_m;
+  if (m == 0) return;
+  for (int r = 0; r < kRounds; r++) {
+    const int* S = ws.sub + ws.suboff[oi * (kRounds + 1) + r];
+    const int ns = ws.suboff[oi * (kRounds + 1) + r + 1] - ws.suboff[oi * (kRounds + 1) + r];
+    for (int j = wave; j < m; j += nw) {  // countInliers2D (:1171-1214) of hypothesis hl[j]
+      const double* hr = ws.hyp + (size_t)hl[j] * 16;
+      Pose P;
+      for (int i = 0; i < 9; i++) P.R[i] = hr[1 + i];
+      for (int i = 0; i < 3; i++) P.t[i] = hr[10 + i];
+      int cnt = 0;
+      for (int i = lane; i < ns; i += 64) {
+        const int idx = L[S[i]];
+        const double u0 = idx % W, v0 = idx / W;
+        const F3 o = mode3d(vm, ext, C, obj, idx);
+        double u, v;
+        project(P, D3{o.x, o.y, o.z}, k, u, v);
+        if (sqrt((u0 - u) * (u0 - u) + (v0 - v) * (v0 - v)) < 10.0f) cnt++;
+      }
+      cnt = pcnn::wave_sum(cnt);
+      if (lane == 0) {
+        hcnt[j] = cnt;
+        inl_out[hl[j] * kRounds + r] = cnt;
+      }
+    }
+    __syncthreads();
+    if (m > 1) {  // stable sort by inliers (descending), keep the better half
+      for (int j = threadIdx.x; j < m; j += blockDim.x) {
+        int rank = 0;
+        for (int q = 0; q < m; q++) rank += hcnt[q] > hcnt[j] || (hcnt[q] == hcnt[j] && q < j);
+        tmp[rank] = j;
+      }
+      __syncthreads();
+      const int keep = m / 2;
+      int nh = 0, nc = 0;
+      if (threadIdx.x < keep) {
+        nh = hl[tmp[threadIdx.x]];
+        nc = hcnt[tmp[threadIdx.x]];
+      }
+      int nh2 = 0, nc2 = 0;  // keep <= 512: a second element per thread
+      if (threadIdx.x + blockDim.x < keep) {
+        nh2 = hl[tmp[threadIdx.x + blockDim.x]];
+        nc2 = hcnt[tmp[threadIdx.x + blockDim.x]];
+      }
+      __syncthreads();
+      if (threadIdx.x < keep) { hl[threadIdx.x] = nh; hcnt[threadIdx.x] = nc; }
+      if (threadIdx.x + blockDim.x < keep) { hl[threadIdx.x + blockDim.x] = nh2; hcnt[threadIdx.x + blockDim.x] = nc2; }
+      m = keep;
+      __syncthreads();
+    }
+  }
+  if (threadIdx.x == 0) {
+    const int h = hl[0];
+    int nh = 0;
+    for (int q = 0; q < n_hyp; q++) nh += ws.hyp[(size_t)q * 16] == (double)obj;
+    final_out[obj * 3] = h;
+    final_out[obj * 3 + 1] = hcnt[0];
+    final_out[obj * 3 + 2] = nh;
+    const double* hr = ws.hyp + (size_t)h * 16;
+    for (int y = 0; y < 3; y++)
+      for (int x = 0; x < 4; x++) poses_out[obj + C * (y * 4 + x)] = x < 3 ? (float)hr[1 + y * 3 + x] : (float)hr[10 + y];
+  }
+}
+
+struct Layout {
+  size_t colcnt, coloff, count, lists, listoff, objs, suboff, hyp, sub, total;
+};
+
+Layout layout(int H, int W, int C, int n_hyp) {
+  pcnn::Carve cv(nullptr);
+  Layout l;
+  l.colcnt = (size_t)(uintptr_t)cv.take<int32_t>((size_t)C * W);
+  l.coloff = (size_t)(uintptr_t)cv.take<int32_t>((size_t)C * W);
+  l.count = (size_t)(uintptr_t)cv.take<int32_t>(C);
+  l.lists = (size_t)(uintptr_t)cv.take<int32_t>((size_t)H * W);
+  l.listoff = (size_t)(uintptr_t)cv.take<int32_t>(C);
+  l.objs = (size_t)(uintptr_t)cv.take<int32_t>(C);
+  l.suboff = (size_t)(uintptr_t)cv.take<int32_t>((size_t)C * (kRounds + 1));
+  l.hyp = (size_t)(uintptr_t)cv.take<double>((size_t)n_hyp * 16);
+  // subsets: a round visits at most every pixel of the class once
+  l.sub = (size_t)(uintptr_t)cv.take<int32_t>((size_t)kRounds * H * W);
+  l.total = cv.off + 256;
+  return l;
+}
+
+}  // namespace
+
+extern "C" size_t pcnn_pose2d_workspace_size(int H, int W, int C, int n_hyp) {
+  if (H <= 0 || W <= 0 || C <= 0 || n_hyp <= 0) return 256;
+  return layout(H, W, C, n_hyp).total;
+}
+
+extern "C" int pcnn_pose2d(const int32_t* label, const float* vertmap, const float* extents, int H, int W, int C,
+                           float fx, float fy, float px, float py, uint64_t seed, int n_hyp, int max_iter,
+                           float* poses_out, float* hyps_out, int32_t* hyp_px, int32_t* inl_out, int32_t* final_out,
+                           void* workspace, size_t workspace_bytes, void* stream) {
+  PCNN_REQUIRE(label && vertmap && extents && poses_out && hyps_out && hyp_px && inl_out && final_out);
+  PCNN_REQUIRE(H > 0 && W > 0 && C > 1 && C <= 64 && n_hyp > 0 && n_hyp <= kMaxHypBlock && max_iter > 0);
+  PCNN_REQUIRE((long)H * W < (1l << 28));
+  const Layout l = layout(H, W, C, n_hyp);
+  if (!workspace || workspace_bytes < l.total) return PCNN_ECAPACITY;
+  char* base = (char*)workspace;
+  P2dWs ws;
+  ws.colcnt = (int32_t*)(base + l.colcnt);
+  ws.coloff = (int32_t*)(base + l.coloff);
+  ws.count = (int32_t*)(base + l.count);
+  ws.lists = (int32_t*)(base + l.lists);
+  ws.listoff = (int32_t*)(base + l.listoff);
+  ws.objs = (int32_t*)(base + l.objs);
+  ws.suboff = (int32_t*)(base + l.suboff);
+  ws.hyp = (double*)(base + l.hyp);
+  ws.sub = (int32_t*)(base + l.sub);
+  hipStream_t st = (hipStream_t)stream;
+  if (hipMemsetAsync(ws.colcnt, 0, (size_t)C * W * sizeof(int32_t), st) != hipSuccess) return PCNN_EHIP;
+  if (hipMemsetAsync(poses_out, 0, (size_t)12 * C * sizeof(float), st) != hipSuccess) return PCNN_EHIP;
+  if (hipMemsetAsync(inl_out, 0xFF, (size_t)n_hyp * kRounds * sizeof(int32_t), st) != hipSuccess) return PCNN_EHIP;
+  if (hipMemsetAsync(final_out, 0xFF, (size_t)C * 3 * sizeof(int32_t), st) != hipSuccess) return PCNN_EHIP;
+  hipLaunchKernelGGL(k_p2d_colcount, dim3((W + 255) / 256), dim3(256), 0, st, label, H, W, C, ws.colcnt);
+  hipLaunchKernelGGL(k_p2d_scan, dim3(C), dim3(1024), 0, st, ws.colcnt, W, ws.coloff, ws.count);
+  PCNN_CHECK_LAUNCH();
+  // the class sizes decide object_ids (> minArea = 400, :1027) and the
+  // subsets: one host round trip, as the reference is host code throughout
+  std::vector<int32_t> cnt(C);
+  if (hipMemcpyAsync(cnt.data(), ws.count, C * sizeof(int32_t), hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess)
+    return PCNN_EHIP;
+  std::vector<int32_t> listoff(C), objs;
+  int acc = 0;
+  for (int c = 0; c < C; c++) {
+    listoff[c] = acc;
+    acc += cnt[c];
+    if (c >= 1 && (float)cnt[c] > 400.0f) objs.push_back(c);
+  }
+  const int n_obj = (int)objs.size();
+  if (n_obj == 0) {  // no object: hypotheses stay empty (:1586-1587)
+    hipLaunchKernelGGL(k_p2d_hyps, dim3((n_hyp + 63) / 64), dim3(64), 0, st, vertmap, extents, H, W, C,
+                       Cam{fx, fy, px, py}, seed, n_hyp, 0, 0, ws, hyps_out, hyp_px);
+    PCNN_CHECK_LAUNCH();
+    return PCNN_OK;
+  }
+  // countInliers2D's pixel subsets of the 8 rounds (the same for every
+  // hypothesis of a round: a fresh default-seeded std::mt19937 per call)
+  std::vector<int32_t> sub, suboff;
+  for (int oi = 0; oi < n_obj; oi++) {
+    const int N = cnt[objs[oi]];
+    for (int r = 1; r <= kRounds; r++) {
+      suboff.push_back((int32_t)sub.size());
+      const int maxPixels = 1000 * r;
+      const float rate = maxPixels / (float)N;
+      std::mt19937 gen;
+      std::negative_binomial_distribution<int> nb(1, rate < 1 ? rate : 0.5f);
+      for (int i = 0; i < N;) {
+        sub.push_back(i);
+        if (rate < 1) i += std::max(1, nb(gen));
+        else i++;
+      }
+    }
+    suboff.push_back((int32_t)sub.size());
+  }
+  if (sub.size() > (size_t)kRounds * H * W) return PCNN_ECAPACITY;
+  if (hipMemcpyAsync(ws.listoff, listoff.data(), C * sizeof(int32_t), hipMemcpyHostToDevice, st) != hipSuccess ||
+      hipMemcpyAsync(ws.objs, objs.data(), n_obj * sizeof(int32_t), hipMemcpyHostToDevice, st) != hipSuccess ||
+      hipMemcpyAsync(ws.suboff, suboff.data(), suboff.size() * sizeof(int32_t), hipMemcpyHostToDevice, st) !=
+          hipSuccess ||
+      hipMemcpyAsync(ws.sub, sub.data(), sub.size() * sizeof(int32_t), hipMemcpyHostToDevice, st) != hipSuccess)
+    return PCNN_EHIP;
+  const Cam k{fx, fy, px, py};
+  hipLaunchKernelGGL(k_p2d_scatter, dim3((W + 63) / 64), dim3(64), C * 64 * sizeof(int), st, label, H, W, C, ws);
+  hipLaunchKernelGGL(k_p2d_hyps, dim3((n_hyp + 63) / 64), dim3(64), 0, st, vertmap, extents, H, W, C, k, seed, n_hyp,
+                     n_obj, max_iter, ws, hyps_out, hyp_px);
+  hipLaunchKernelGGL(k_p2d_ransac, dim3(n_obj), dim3(kRansacThreads), 0, st, vertmap, extents, W, C, k, n_hyp, ws,
+                     inl_out, final_out, poses_out);
+  PCNN_CHECK_LAUNCH();
+  // the host vectors above are the sources of the async copies
+  if (hipStreamSynchronize(st) != hipSuccess) return PCNN_EHIP;
+  return PCNN_OK;
+}

@@ -90,8 +90,14 @@ def make_meta(K, B, voxel=None):
 
 
 def make_frames(B, H=480, W=640, num_classes=22, objects_per_image=6, seed=0, image_offset=0,
-                extents=None, K=None, dir_noise=0.05, depth_noise=0.01, with_depth=False, voxel=None):
-    """Generate B synthetic frames; image i uses rng seed (seed*1000 + image_offset + i)."""
+                extents=None, K=None, dir_noise=0.05, depth_noise=0.01, with_depth=False, voxel=None,
+                depth_background=None):
+    """Generate B synthetic frames; image i uses rng seed (seed*1000 + image_offset + i).
+    depth_background = (z_top, z_bottom): with_depth frames also get a scene
+    behind the objects -- a plane whose depth runs linearly from z_top at the
+    top image row to z_bottom at the bottom one (a floor / table seen at an
+    angle), as an RGB-D sensor reports depth at every pixel; None leaves the
+    pixels outside the objects at depth 0 (holes)."""
     mdl = models()
     if extents is None:
         extents = mdl["lov_extents"][:num_classes]
@@ -108,6 +114,9 @@ def make_frames(B, H=480, W=640, num_classes=22, objects_per_image=6, seed=0, im
     label = np.zeros((B, H, W), np.int32)
     vertex = np.empty((B, H, W, 3 * C), np.float32)
     depth = np.zeros((B, H, W, 1), np.float32) if with_depth else None
+    if depth is not None and depth_background is not None:
+        zt, zb = depth_background
+        depth[:] = (zt + (zb - zt) * np.arange(H, dtype=np.float64) / max(H - 1, 1)).astype(np.float32)[None, :, None, None]
     gts = []
     margin = max(4, int(round(40 * W / 640)))
     for i in range(B):

@@ -109,3 +109,32 @@ def test_fc7_forward_relu(hip, ops):
     c32 = torch.relu(y6[:R] @ w7)
     _check("fc7 fwd", C[:R], ref, c32)
     assert not C[R:].any()
+
+
+def test_x6_edge_semantics(hip):
+    """x6's stated operand range: finite |x| <= 3.3895314e38 (the largest
+    bf16, 0x7F7F) -- there it tracks fp32 (values up to 1e38 here).  A larger
+    finite fp32 rounds its hi plane to inf, and an inf / NaN operand makes its
+    mid plane NaN: the output elements that operand reaches are NaN (fp32 gives
+    +-inf for inf * finite, a finite value for the near-FLT_MAX case), and every
+    other element is unaffected (a row of A reaches only its own output row)."""
+    g = torch.Generator(device=D)
+    g.manual_seed(3)
+    M, K, N = 64, 256, 128
+    A = torch.randn((M, K), generator=g, device=D)
+    B = torch.randn((K, N), generator=g, device=D) * 1e-3
+    A[1, 5] = 1e38                      # in range: finite, fp32-faithful
+    A[2, 7] = float("inf")
+    A[3, 9] = float("nan")
+    A[4, 11] = 3.4e38                   # finite fp32, above the largest bf16
+    C = torch.zeros((M, N), device=D)
+    ph.gemm(A, B, C, precision=2)
+    ref = A.double() @ B.double()
+    fin = torch.ones(M, dtype=torch.bool, device=D)
+    fin[2:5] = False
+    ok = (C[fin].double() - ref[fin]).abs() <= 2e-5 * ref[fin].abs() + 2e-5 * ref[fin].abs().max()
+    assert bool(ok.all())
+    assert torch.isfinite(C[1]).all() and abs(float(C[1, 0]) / float(ref[1, 0]) - 1) < 1e-6
+    for r in (2, 3, 4):
+        assert bool(torch.isnan(C[r]).all()), r
+    assert bool(torch.isfinite((A[4:5] @ B)).all())  # the fp32 matmul stays finite there

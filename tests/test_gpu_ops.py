@@ -302,16 +302,20 @@ def test_backproject(hip, orc, Ch, NC, ks):
     np.testing.assert_array_equal(gd.cpu().numpy(), orc.backproject_bwd(g, depth, meta, H, W, G))
 
 
-def test_backproject_linemod_config(hip, orc):
+@pytest.mark.parametrize("background", [None, (1.0, 2.0)])
+def test_backproject_linemod_config(hip, orc, background):
     """configs[4] sizes for one image: 640x480 LINEMOD frame (15 objects' extents,
-    4 objects, rendered depth), G = 64, Ch = 64, NC = 16, kernel_size 1,
-    threshold 0.02, forward and backward bit-exact."""
+    4 objects, rendered depth; with a floor plane behind them, the bench's
+    workload, or depth holes around them), G = 64, Ch = 64, NC = 16,
+    kernel_size 1, threshold 0.02, forward and backward
+    bit-exact."""
     rng = np.random.default_rng(45)
     mdl = synth.models()
     G, Ch, NC = 64, 64, 16
-    voxel = ([2.0 / G, 1.5 / G, 1.7 / G], [-1.0, -0.75, 0.4])
+    voxel = ([1.2 / G, 0.9 / G, 1.2 / G], [-0.6, -0.45, 0.9])  # the camera frustum at 0.9-2.1 m (bench.py)
     fr = synth.make_frames(1, 480, 640, num_classes=16, objects_per_image=4, seed=5,
-                           extents=mdl["linemod_extents"], with_depth=True, voxel=voxel)
+                           extents=mdl["linemod_extents"], with_depth=True, voxel=voxel,
+                           depth_background=background)
     depth = fr["depth"]
     data = rng.normal(size=(1, 480, 640, Ch)).astype(np.float32)
     label = rng.uniform(size=(1, 480, 640, NC)).astype(np.float32)
@@ -322,6 +326,8 @@ def test_backproject_linemod_config(hip, orc):
     np.testing.assert_array_equal(tl.cpu().numpy(), ol)
     np.testing.assert_array_equal(tf.cpu().numpy(), of)
     assert of.any() and not of.all()
+    if background is not None:  # the scene's surfaces cross the grid: percent-level hits
+        assert (of[..., 0] > 0).mean() > 0.01
     g = rng.normal(size=od.shape).astype(np.float32)
     gd = bp.backproject_grad(T(data), T(depth), T(fr["meta"]), T(g), G, 1, 0.02)
     np.testing.assert_array_equal(gd.cpu().numpy(), orc.backproject_bwd(g, depth, fr["meta"], 480, 640, G))
