@@ -419,6 +419,16 @@ int pcnn_pose_energy(const float* live, const int32_t* label, int obj, const flo
                      float znear, float zfar, const float* poses, int K, float* energy, void* workspace,
                      size_t workspace_bytes, void* stream);
 
+/* Batched optEnergy: pose k (of K) is scored for object pose_obj[k] against live
+ * map pose_live[k] (of n_live, (H,W,3) each) and rendered vertices pose_pv[k]
+ * (of n_pv, (H,W,4) each) -- one launch for the Nelder-Mead simplices of every
+ * RoI of solveICP (synthesize.cpp:2529-2573), which the reference evaluates one
+ * pose at a time.  workspace: pcnn_icp_reduce_workspace_size(K, H, W). */
+int pcnn_pose_energy_batch(const float* live, int n_live, const int32_t* label, const float* pred_vertices, int n_pv,
+                           int H, int W, float znear, float zfar, const float* poses, int K, const int32_t* pose_obj,
+                           const int32_t* pose_live, const int32_t* pose_pv, float* energy, void* workspace,
+                           size_t workspace_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

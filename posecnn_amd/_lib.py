@@ -105,6 +105,9 @@ _SIGS = {
     "pcnn_icp_score_workspace_size": (c_size_t, [c_int, c_int, c_int]),
     "pcnn_icp_score": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_float, c_void_p,
                                c_void_p, c_void_p, c_size_t, c_void_p]),
+    "pcnn_pose_energy_batch": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_float,
+                                       c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t,
+                                       c_void_p]),
     "pcnn_pose_energy": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_float, c_float, c_void_p, c_int,
                                  c_void_p, c_void_p, c_size_t, c_void_p]),
 }

@@ -630,14 +630,22 @@ __global__ void __launch_bounds__(kBlk) k_icp_center(const float* __restrict__ l
 }
 
 // optEnergy for K poses over the object's pixels (grid: segments x poses)
-__global__ void __launch_bounds__(kBlk) k_pose_energy(const float* __restrict__ live, const int32_t* __restrict__ label,
-                                                      int obj, const float* __restrict__ pred_v, int HW, float znear,
+// (batched form: pose k belongs to problem (pose_obj[k], live map pose_live[k],
+// rendered vertices pose_pv[k]); NULL index arrays = one problem for all K)
+__global__ void __launch_bounds__(kBlk) k_pose_energy(const float* __restrict__ live_all,
+                                                      const int32_t* __restrict__ label, int obj0,
+                                                      const float* __restrict__ pv_all, int HW, float znear,
                                                       float zfar, const float* __restrict__ poses,
                                                       float* __restrict__ partial, unsigned* __restrict__ tickets,
-                                                      float* __restrict__ energy) {
+                                                      float* __restrict__ energy, const int32_t* __restrict__ pose_obj,
+                                                      const int32_t* __restrict__ pose_live,
+                                                      const int32_t* __restrict__ pose_pv) {
   __shared__ float sh[(kBlk / 64) * 2];
   __shared__ int flag;
   const int k = blockIdx.y, seg = blockIdx.x, nblk = gridDim.x;
+  const int obj = pose_obj ? pose_obj[k] : obj0;
+  const float* __restrict__ live = live_all + (pose_live ? (size_t)pose_live[k] * HW * 3 : 0);
+  const float* __restrict__ pred_v = pv_all + (pose_pv ? (size_t)pose_pv[k] * HW * 4 : 0);
   const float* P = poses + (size_t)k * 7;
   const float qn = sqrtf(P[0] * P[0] + P[1] * P[1] + P[2] * P[2] + P[3] * P[3]);
   const Quat q = {P[0] / qn, P[1] / qn, P[2] / qn, P[3] / qn};
@@ -925,7 +933,29 @@ extern "C" int pcnn_pose_energy(const float* live, const int32_t* label, int obj
   if (hipMemsetAsync(tickets, 0, (size_t)K * sizeof(unsigned), st) != hipSuccess) return PCNN_EHIP;
   const int HW = H * W, nseg = (HW + kSeg - 1) / kSeg;
   hipLaunchKernelGGL(k_pose_energy, dim3(nseg, K), dim3(kBlk), 0, st, live, label, obj, pred_vertices, HW, znear,
-                     zfar, poses, partial, tickets, energy);
+                     zfar, poses, partial, tickets, energy, (const int32_t*)nullptr, (const int32_t*)nullptr,
+                     (const int32_t*)nullptr);
+  PCNN_CHECK_LAUNCH();
+  return PCNN_OK;
+}
+
+extern "C" int pcnn_pose_energy_batch(const float* live, int n_live, const int32_t* label, const float* pred_vertices,
+                                      int n_pv, int H, int W, float znear, float zfar, const float* poses, int K,
+                                      const int32_t* pose_obj, const int32_t* pose_live, const int32_t* pose_pv,
+                                      float* energy, void* workspace, size_t workspace_bytes, void* stream) {
+  PCNN_REQUIRE(live && label && pred_vertices && poses && energy && workspace && pose_obj && pose_live && pose_pv &&
+               K > 0 && H > 0 && W > 0 && n_live > 0 && n_pv > 0);
+  size_t need = 0;
+  float* partial;
+  unsigned* tickets;
+  carve_red(nullptr, K, H * W, 4, &partial, &tickets, &need);
+  if (workspace_bytes < need) return PCNN_ECAPACITY;
+  carve_red(workspace, K, H * W, 4, &partial, &tickets, nullptr);
+  hipStream_t st = (hipStream_t)stream;
+  if (hipMemsetAsync(tickets, 0, (size_t)K * sizeof(unsigned), st) != hipSuccess) return PCNN_EHIP;
+  const int HW = H * W, nseg = (HW + kSeg - 1) / kSeg;
+  hipLaunchKernelGGL(k_pose_energy, dim3(nseg, K), dim3(kBlk), 0, st, live, label, 0, pred_vertices, HW, znear, zfar,
+                     poses, partial, tickets, energy, pose_obj, pose_live, pose_pv);
   PCNN_CHECK_LAUNCH();
   return PCNN_OK;
 }

@@ -119,6 +119,39 @@ def pose_energy(live, label, obj, pred_vertices, poses, depth_range=(0.25, 6.0),
     return energy
 
 
+def pose_energy_batch(live, label, pose_obj, pose_live, pred_vertices, pose_pv, poses, depth_range=(0.25, 6.0),
+                      stream=None):
+    """optEnergy of K poses in one launch: pose k (poses (K,7)) is scored for
+    object pose_obj[k] against live[pose_live[k]] (live (L,H,W,3)) and
+    pred_vertices[pose_pv[k]] (pred_vertices (P,H,W,4)).  Index arrays are
+    device int32 (K,), validated here on the host side when given as CPU data."""
+    _lib.require_gpu(live, label, pred_vertices, poses)
+    lv, pv, P = _f(live), _f(pred_vertices), _f(poses)
+    if lv.dim() != 4 or pv.dim() != 4 or P.dim() != 2 or P.shape[1] != 7:
+        raise ValueError("pose_energy_batch: live (L,H,W,3), pred_vertices (P,H,W,4), poses (K,7)")
+    L_, H, W = lv.shape[0], lv.shape[1], lv.shape[2]
+    K = P.shape[0]
+    if pv.shape[1:] != (H, W, 4) or lv.shape[3] != 3 or label.shape[-2:] != (H, W):
+        raise ValueError("pose_energy_batch: map shapes disagree")
+    idx = []
+    for a, n in ((pose_obj, None), (pose_live, L_), (pose_pv, pv.shape[0])):
+        t = torch.as_tensor(a)
+        if t.numel() != K:
+            raise ValueError("pose_energy_batch: one index per pose")
+        if not t.is_cuda and n is not None and K and (int(t.min()) < 0 or int(t.max()) >= n):
+            raise ValueError("pose_energy_batch: index out of range")
+        idx.append(t.to(device=lv.device, dtype=torch.int32).contiguous())
+    energy = torch.empty((K,), dtype=torch.float32, device=lv.device)
+    lib = _lib.load()
+    ws = _lib.workspace(lib.pcnn_icp_reduce_workspace_size(K, H, W), lv.device, "icp_energy", stream)
+    rc = lib.pcnn_pose_energy_batch(_lib.ptr(lv), L_, _lib.ptr(label.contiguous().to(torch.int32)), _lib.ptr(pv),
+                                    pv.shape[0], H, W, float(depth_range[0]), float(depth_range[1]), _lib.ptr(P), K,
+                                    _lib.ptr(idx[0]), _lib.ptr(idx[1]), _lib.ptr(idx[2]), _lib.ptr(energy),
+                                    _lib.ptr(ws), ws.numel(), _lib.stream_ptr(stream))
+    _lib.check(rc, "pose_energy_batch")
+    return energy
+
+
 def icp_score(live, label, obj, vertmap, hyps, radius=0.01, stream=None):
     """SegICP score of J hypotheses (synthesize.cpp:2288-2330) -> (score (J,), choose (1,) int32)."""
     _lib.require_gpu(live, label, vertmap, hyps)
@@ -153,57 +186,99 @@ def _se3_mul(a, b):
     return np.concatenate([q / np.linalg.norm(q), t])
 
 
-def nelder_mead(f, x0, lb, ub, max_eval):
+def nelder_mead_steps(x0, lb, ub, max_eval):
     """Bounded Nelder-Mead (NLopt LN_NELDERMEAD's role in poseWithOpt,
-    synthesize.cpp:2529-2573): initial steps NLopt's default (a quarter of the
-    bound range, 0.75 of the distance to a nearer bound), reflection 1,
-    expansion 2, contraction 1/2, shrink 1/2, trial points clamped to the
-    bounds, at most max_eval evaluations of f.  NLopt is absent here: the
-    search's exact trajectory is unpinned."""
+    synthesize.cpp:2529-2573) as a generator: it yields (m, n) arrays of points
+    to evaluate and receives their m values (send), and returns (x, f).  The
+    initial simplex and a shrink step are asked for as one batch; otherwise one
+    point at a time, in the same order and count as the sequential search.
+    Initial steps NLopt's default (a quarter of the bound range, 0.75 of the
+    distance to a nearer bound), reflection 1, expansion 2, contraction 1/2,
+    shrink 1/2, trial points clamped to the bounds, at most max_eval
+    evaluations.  NLopt is absent here: the search's exact trajectory is
+    unpinned."""
     import numpy as np
     x0 = np.asarray(x0, np.float64)
     n = x0.size
     lb, ub = np.asarray(lb, np.float64), np.asarray(ub, np.float64)
     step = np.minimum(0.25 * (ub - lb), np.minimum(0.75 * (ub - x0), 0.75 * (x0 - lb)))
     pts = [x0] + [x0 + step[i] * np.eye(n)[i] for i in range(n)]
-    vals = [f(p) for p in pts]
+    vals = list((yield np.stack(pts)))
     nev = len(pts)
     clamp = lambda p: np.minimum(np.maximum(p, lb), ub)
+    one = lambda p: float((yield p[None])[0])  # noqa: E731 (a one-point request)
     while nev < max_eval:
         order = np.argsort(vals, kind="stable")
         pts = [pts[i] for i in order]
         vals = [vals[i] for i in order]
         c = np.mean(pts[:-1], axis=0)
         xr = clamp(c + (c - pts[-1]))
-        fr = f(xr)
+        fr = yield from one(xr)
         nev += 1
         if fr < vals[0] and nev < max_eval:
             xe = clamp(c + 2 * (c - pts[-1]))
-            fe = f(xe)
+            fe = yield from one(xe)
             nev += 1
             pts[-1], vals[-1] = (xe, fe) if fe < fr else (xr, fr)
         elif fr < vals[-2]:
             pts[-1], vals[-1] = xr, fr
         elif nev < max_eval:
             xc = clamp(c + 0.5 * (pts[-1] - c)) if fr >= vals[-1] else clamp(c + 0.5 * (xr - c))
-            fc = f(xc)
+            fc = yield from one(xc)
             nev += 1
             if fc < min(fr, vals[-1]):
                 pts[-1], vals[-1] = xc, fc
             else:
-                for i in range(1, n + 1):
-                    if nev >= max_eval:
-                        break
-                    pts[i] = clamp(pts[0] + 0.5 * (pts[i] - pts[0]))
-                    vals[i] = f(pts[i])
-                    nev += 1
+                m = min(n, max_eval - nev)
+                if m > 0:
+                    new = [clamp(pts[0] + 0.5 * (pts[i] - pts[0])) for i in range(1, m + 1)]
+                    fv = list((yield np.stack(new)))
+                    for i in range(1, m + 1):
+                        pts[i], vals[i] = new[i - 1], fv[i - 1]
+                    nev += m
     i = int(np.argmin(vals))
     return pts[i], vals[i]
 
 
+def nelder_mead(f, x0, lb, ub, max_eval):
+    """The search of nelder_mead_steps driven by a scalar function f."""
+    import numpy as np
+    gen = nelder_mead_steps(x0, lb, ub, max_eval)
+    try:
+        req = next(gen)
+        while True:
+            req = gen.send(np.array([f(p) for p in req]))
+    except StopIteration as e:
+        return e.value
+
+
+def nelder_mead_batch(fbatch, starts, lb, ub, max_eval):
+    """Lock-step Nelder-Mead searches, one per start: every round collects the
+    pending requests of all live searches and evaluates them with ONE call
+    fbatch(list of (search, points)) -> list of value arrays (solve_icp: one
+    batched optEnergy launch for every RoI's simplex)."""
+    gens = [nelder_mead_steps(x0, l, u, max_eval) for x0, l, u in zip(starts, lb, ub)]
+    res = [None] * len(gens)
+    reqs = {}
+    for i, g in enumerate(gens):
+        reqs[i] = next(g)
+    while reqs:
+        items = sorted(reqs.items())
+        vals = fbatch(items)
+        reqs = {}
+        for (i, _), v in zip(items, vals):
+            try:
+                reqs[i] = gens[i].send(v)
+            except StopIteration as e:
+                res[i] = e.value
+    return res
+
+
 def solve_icp(labelmap, depth, parameters, rois, poses, render, max_error=0.01, nm_evals=50, icp_iterations=8,
               min_pixels=400, stream=None):
-    """Synthesizer::solveICP (synthesize.cpp:2052-2395) on the GPU ops above.
+    """Synthesizer::solveICP (synthesize.cpp:2052-2395) on the GPU ops above,
+    batched over the RoIs (the reference refines them one after another; no
+    state passes between RoIs, :2090-2392).
 
     labelmap (H,W) int32, depth (H,W) uint16, parameters = (fx, fy, px, py,
     znear, zfar, factor) (icp_python's meta, synthesize.cpp:2031-2049), rois
@@ -211,10 +286,13 @@ def solve_icp(labelmap, depth, parameters, rois, poses, render, max_error=0.01, 
     -> (vertmap (H,W,3), pred_vertices (H,W,4), pred_normals (H,W,4)) device
     tensors stands in for the reference's OpenGL pass.  Returns (poses_new,
     poses_icp) (R,7) as the reference fills `outputs` / `outputs_icp`: rows of
-    skipped RoIs stay zero.  Per RoI: live vertices, translation re-centring,
-    the Nelder-Mead search on optEnergy (nm_evals evaluations; 0 skips it),
-    eight depth hypotheses refined by one batched 8-iteration ICP launch, and
-    the SegICP score picks one."""
+    skipped RoIs stay zero.  The steps, each one launch for all RoIs: live
+    vertices of every RoI's object; the >= min_pixels test (one host read);
+    the translation re-centring (one host read); the Nelder-Mead search on
+    optEnergy in lock step (nm_evals evaluations each, 0 skips it: every round
+    of requests is one batched energy launch and one host read); the eight
+    depth hypotheses of every RoI refined by one 8-iteration ICP launch; the
+    SegICP score per RoI, its choice read once at the end."""
     import numpy as np
     fx, fy, px, py, znear, zfar, factor = (float(v) for v in parameters)
     cam = (fx, fy, px, py)
@@ -225,44 +303,69 @@ def solve_icp(labelmap, depth, parameters, rois, poses, render, max_error=0.01, 
     rois_h = rois.detach().cpu().numpy() if torch.is_tensor(rois) else np.asarray(rois)
     poses_h = poses.detach().cpu().numpy() if torch.is_tensor(poses) else np.asarray(poses, np.float32)
     dz = [0.0, -0.02, -0.01, 0.01, 0.02, 0.03, 0.04, 0.05]  # synthesize.cpp:2255-2280
-    for i in range(R_):
-        obj = int(rois_h[i, 1])
-        if obj <= 0:
-            continue
+    lab = labelmap.contiguous().to(torch.int32)
+    cand = [i for i in range(R_) if int(rois_h[i, 1]) > 0]
+    if not cand:
+        return poses_new, poses_icp
+    objs = [int(rois_h[i, 1]) for i in cand]
+    # the object's pixel count (:2152-2160, >= 400 to go on): one histogram, one host read
+    counts = torch.bincount(lab.reshape(-1).long(), minlength=max(objs) + 1).cpu().numpy()
+    keep = [k for k, o in enumerate(objs) if counts[o] >= min_pixels]
+    if not keep:
+        return poses_new, poses_icp
+    rows = [cand[k] for k in keep]
+    objs = [objs[k] for k in keep]
+    n = len(rows)
+    objt = torch.tensor(objs, dtype=torch.int32, device=dev)
+    live = live_vertices(depth, lab, objt, factor, cam, stream)          # (n, H, W, 3)
+    T = []
+    for i in rows:
         p = poses_h[i].astype(np.float64)
-        T = np.concatenate([p[:4] / np.linalg.norm(p[:4]), p[4:7]]).astype(np.float32)
-        vm, pv, pn = render(obj, T)
-        objt = torch.tensor([obj], dtype=torch.int32, device=dev)
-        live = live_vertices(depth, labelmap, objt, factor, cam, stream)
-        if int((labelmap == obj).sum()) < min_pixels:
-            continue
-        out, Tc = icp_center(live, labelmap, objt, vm[None], pv[None], pn[None], max_error,
-                             pose_in=torch.from_numpy(T).to(dev)[None], stream=stream)
-        c = float(out[0, 3])
-        if c > 0:
-            T = Tc[0].cpu().numpy()
-            if nm_evals > 0:  # refinePose(..., 0): optEnergy over a correction of the re-rendered pose
-                _, pv0, _ = render(obj, T)
+        T.append(np.concatenate([p[:4] / np.linalg.norm(p[:4]), p[4:7]]).astype(np.float32))
+    maps = [render(o, Ti) for o, Ti in zip(objs, T)]
+    vm = torch.stack([m[0] for m in maps])
+    out, Tc = icp_center(live, lab, objt, vm, torch.stack([m[1] for m in maps]), torch.stack([m[2] for m in maps]),
+                         max_error, pose_in=torch.from_numpy(np.stack(T)).to(dev), stream=stream)
+    c_h, Tc_h = out[:, 3].cpu().numpy(), Tc.cpu().numpy()
+    for k in range(n):
+        if c_h[k] > 0:
+            T[k] = Tc_h[k]
+    nm = [k for k in range(n) if c_h[k] > 0] if nm_evals > 0 else []
+    if nm:  # refinePose(..., 0): optEnergy over a correction of each re-rendered pose, in lock step
+        pv0 = torch.stack([render(objs[k], T[k])[1] for k in nm])
+        x0 = np.array([1, 0, 0, 0, 0, 0, 0], np.float64)
+        r = np.array([0.1, 0.1, 0.1, 0.1, 0.01, 0.01, 0.1])
+        obj_of = torch.tensor([objs[k] for k in nm], dtype=torch.int32)
+        live_of = torch.tensor(nm, dtype=torch.int32)
 
-                def energy(x):
-                    return float(pose_energy(live[0], labelmap, obj, pv0,
-                                             torch.tensor(x, dtype=torch.float32, device=dev)[None], (znear, zfar),
-                                             stream)[0])
-
-                x0 = np.array([1, 0, 0, 0, 0, 0, 0], np.float64)
-                r = np.array([0.1, 0.1, 0.1, 0.1, 0.01, 0.01, 0.1])
-                x, _ = nelder_mead(energy, x0, x0 - r, x0 + r, nm_evals)
-                T = _se3_mul(np.concatenate([x[:4] / np.linalg.norm(x[:4]), x[4:]]), T).astype(np.float32)
-        Tz = float(T[6])
-        poses_new[i] = T
-        hyps = np.repeat(T[None], len(dz), 0)
-        hyps[1:, 6] = [Tz + d for d in dz[1:]]
-        maps = [render(obj, h) for h in hyps]
-        pvs = torch.stack([m[1] for m in maps])
-        pns = torch.stack([m[2] for m in maps])
-        _, refined = icp(live, pvs, pns, cam, (znear, zfar), max_error, icp_iterations,
-                         live_index=torch.zeros(len(dz), dtype=torch.int32, device=dev),
-                         pose_in=torch.from_numpy(hyps).to(dev), stream=stream)
-        _, choose = icp_score(live[0], labelmap, obj, vm, refined, 0.01, stream)
-        poses_icp[i] = refined[int(choose[0])].cpu().numpy()
+        def energies(items):  # every search's pending points: one launch, one host read
+            P = np.concatenate([pts for _, pts in items]).astype(np.float32)
+            who = np.concatenate([np.full(len(pts), j, np.int64) for j, pts in items])
+            e = pose_energy_batch(live, lab, obj_of[who], live_of[who], pv0, torch.from_numpy(who.astype(np.int32)),
+                                  torch.from_numpy(P).to(dev), (znear, zfar), stream).cpu().numpy()
+            out_, o = [], 0
+            for _, pts in items:
+                out_.append(e[o:o + len(pts)].astype(np.float64))
+                o += len(pts)
+            return out_
+        res = nelder_mead_batch(energies, [x0] * len(nm), [x0 - r] * len(nm), [x0 + r] * len(nm), nm_evals)
+        for j, k in enumerate(nm):
+            x = res[j][0]
+            T[k] = _se3_mul(np.concatenate([x[:4] / np.linalg.norm(x[:4]), x[4:]]), T[k]).astype(np.float32)
+    # eight depth hypotheses per RoI (:2255-2280), all refined by one ICP launch
+    hyps = np.repeat(np.stack(T)[:, None], len(dz), 1)                    # (n, 8, 7)
+    hyps[:, 1:, 6] = np.stack(T)[:, 6:7] + np.array(dz[1:])[None]
+    hmaps = [render(objs[k], hyps[k, h]) for k in range(n) for h in range(len(dz))]
+    pvs = torch.stack([m[1] for m in hmaps])
+    pns = torch.stack([m[2] for m in hmaps])
+    li = torch.arange(n, dtype=torch.int32, device=dev).repeat_interleave(len(dz))
+    _, refined = icp(live, pvs, pns, cam, (znear, zfar), max_error, icp_iterations, live_index=li,
+                     pose_in=torch.from_numpy(hyps.reshape(-1, 7)).to(dev), stream=stream)
+    refined = refined.view(n, len(dz), 7)
+    chosen = [icp_score(live[k], lab, objs[k], vm[k], refined[k], 0.01, stream)[1] for k in range(n)]
+    ch = torch.cat(chosen).cpu().numpy()
+    ref_h = refined.cpu().numpy()
+    for k, i in enumerate(rows):
+        poses_new[i] = T[k]
+        poses_icp[i] = ref_h[k, int(ch[k])]
     return poses_new, poses_icp

@@ -68,6 +68,28 @@ res = {"metric": "refined hypotheses/s (8-iteration df::icp on 640x480 maps)",
                     "bytes_per_iteration": iter_bytes,
                     "note": "step + solve launches per iteration; latency-bound at this size"},
        "data": "synthetic (ray-cast box, tests/refine_scene.py)"}
+# solve_icp end to end (live vertices, re-centring, Nelder-Mead on optEnergy,
+# 8 hypotheses x ICP, SegICP score) for a RoIs of one frame, the renderer a
+# GPU ray-caster standing in for the reference's OpenGL pass
+from refine_scene import render_box_torch  # noqa: E402
+params = list(CAMERA) + [0.25, 6.0, 10000.0]
+half = sc["half"]
+render = lambda o, p: render_box_torch(np.asarray(p, np.float64), half, o)  # noqa: E731
+e2e = {}
+for nroi in (1, 4):
+    rois = np.tile(np.array([[0, sc["cls"], 0, 0, 1, 1]], np.float32), (nroi, 1))
+    poses = np.tile(sc["init"].astype(np.float32)[None], (nroi, 1))
+    for nm in (0, 50):
+        R.solve_icp(lab, depth, params, rois, poses, render, max_error=0.02, nm_evals=nm)  # warm-up
+        torch.cuda.synchronize()
+        reps = 3
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            R.solve_icp(lab, depth, params, rois, poses, render, max_error=0.02, nm_evals=nm)
+        torch.cuda.synchronize()
+        e2e[f"rois{nroi}_nm{nm}_ms"] = round((time.perf_counter() - t0) / reps * 1e3, 2)
+res["solve_icp_end_to_end"] = {**e2e, "note": "wall time per solve_icp call (host orchestration, renders, all "
+                                               "launches and host reads); rois share one frame"}
 if not a.no_cpu:
     from oracle import oracle
     ref_lv = oracle.icp_live_vertices(sc["live"]["depth"], sc["live"]["label"], sc["cls"], 10000.0, CAMERA)

@@ -86,3 +86,39 @@ def scene(seed=0, perturb_deg=3.0, perturb_t=0.01, half=(0.06, 0.045, 0.035), cl
     live = render_box(true, half, cls)
     pred = render_box(init, half, cls)
     return dict(true=true, init=init, live=live, pred=pred, cls=cls, half=half)
+
+
+def render_box_torch(pose, half, cls, H=480, W=640, camera=CAMERA, device="cuda"):
+    """render_box on the GPU (torch), returning the (vertmap, pred_vertices,
+    pred_normals) device maps solve_icp's renderer hands back."""
+    import torch
+    fx, fy, px, py = camera
+    R = torch.tensor(quat_to_R(pose[:4]), dtype=torch.float64, device=device)
+    tt = torch.tensor(np.asarray(pose[4:7], np.float64), device=device)
+    h = torch.tensor(np.asarray(half, np.float64), device=device)
+    ys, xs = torch.meshgrid(torch.arange(H, dtype=torch.float64, device=device),
+                            torch.arange(W, dtype=torch.float64, device=device), indexing="ij")
+    d = torch.stack([(xs - px) / fx, (ys - py) / fy, torch.ones_like(xs)], -1)
+    o = R.T @ (-tt)
+    dd = d @ R
+    t1 = (-h - o) / dd
+    t2 = (h - o) / dd
+    tn = torch.minimum(t1, t2)
+    tf = torch.maximum(t1, t2)
+    tmin = tn.max(-1).values
+    tmax = tf.min(-1).values
+    hit = (tmax >= tmin) & (tmin > 0)
+    axis = tn.argmax(-1)
+    sgn = -torch.sign(torch.gather(dd, -1, axis[..., None])[..., 0])
+    nobj = torch.zeros_like(d).scatter_(-1, axis[..., None], sgn[..., None])
+    P = d * tmin[..., None]
+    N = nobj @ R.T
+    canon = o + dd * tmin[..., None]
+    pv = torch.zeros((H, W, 4), dtype=torch.float32, device=device)
+    pn = torch.zeros((H, W, 4), dtype=torch.float32, device=device)
+    pv[..., :3] = torch.where(hit[..., None], P, torch.zeros_like(P)).float()
+    pv[..., 3] = hit.float()
+    pn[..., :3] = torch.where(hit[..., None], N, torch.zeros_like(N)).float()
+    vm = torch.where(hit[..., None], canon, torch.full_like(canon, float("nan"))).float()
+    vm[..., 0] = torch.where(hit, vm[..., 0] + cls, vm[..., 0])
+    return vm, pv, pn

@@ -168,3 +168,44 @@ def test_icp_edges(hip, orc):
     with pytest.raises(ValueError):  # more than 64 hypotheses
         R.icp_score(lv[0], t(sc["live"]["label"]), sc["cls"], t(sc["pred"]["vertmap"]),
                     torch.zeros((65, 7), device=D))
+
+
+def test_solve_icp_batched_over_rois(hip):
+    """Two boxes of different classes in one frame plus a repeated RoI: the
+    batched solve_icp (one launch per step for all RoIs, Nelder-Mead in lock
+    step) gives each RoI what a call with that RoI alone gives (ICP's
+    workgroup count depends on the batch, so the refined poses agree to float
+    rounding), and both objects land near their true poses."""
+    from posecnn_amd.synthesize import icp as R
+    from refine_scene import axis_angle_quat, quat_mul, render_box
+    rng = np.random.default_rng(11)
+    halves = {3: (0.06, 0.045, 0.035), 5: (0.05, 0.05, 0.03)}
+    trues = {3: np.concatenate([axis_angle_quat([1, 1, 0.3], 0.6), [0.08, -0.02, 0.8]]),
+             5: np.concatenate([axis_angle_quat([0.2, 1, 0.5], 1.1), [-0.1, 0.05, 0.9]])}
+    live = {c: render_box(trues[c], halves[c], c) for c in trues}
+    zs = {c: np.where(live[c]["hit"], live[c]["pred_v"][..., 2], np.inf) for c in trues}
+    front3 = zs[3] <= zs[5]
+    label = np.where(live[3]["hit"] & front3, 3, np.where(live[5]["hit"], 5, 0)).astype(np.int32)
+    depth = np.where(label == 3, live[3]["depth"], np.where(label == 5, live[5]["depth"], 0)).astype(np.uint16)
+
+    def render(obj, pose):
+        m = render_box(np.asarray(pose, np.float64), halves[obj], obj)
+        return t(m["vertmap"]), t(m["pred_v"]), t(m["pred_n"])
+
+    inits = {}
+    for c in trues:
+        dq = axis_angle_quat(rng.normal(size=3), np.deg2rad(2.0))
+        inits[c] = np.concatenate([quat_mul(dq, trues[c][:4]), trues[c][4:] + rng.normal(size=3) * 0.005])
+    rois = np.array([[0, 3, 0, 0, 1, 1], [0, 5, 0, 0, 1, 1], [0, 3, 0, 0, 1, 1]], np.float32)
+    poses = np.stack([inits[3], inits[5], inits[3]]).astype(np.float32)
+    params = list(CAMERA) + [0.25, 6.0, 10000.0]
+    lab_d = t(label)
+    dep_d = t(depth.astype(np.int32)).to(torch.uint16)
+    pnew, picp = R.solve_icp(lab_d, dep_d, params, rois, poses, render, max_error=0.02, nm_evals=20)
+    for i in range(3):
+        a, b = R.solve_icp(lab_d, dep_d, params, rois[i:i + 1], poses[i:i + 1], render, max_error=0.02, nm_evals=20)
+        np.testing.assert_allclose(pnew[i], a[0], atol=1e-6)
+        np.testing.assert_allclose(picp[i], b[0], atol=2e-4)
+    np.testing.assert_array_equal(pnew[0], pnew[2])
+    for i, c in enumerate((3, 5)):
+        assert np.linalg.norm(picp[i, 4:] - trues[c][4:]) < 5e-3
