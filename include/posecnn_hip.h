@@ -261,6 +261,26 @@ int pcnn_gemm_drop(int M, int N, int K, const float* A, const float* A2, int lda
                    const uint8_t* drop, int ldd, float keep_prob, const int32_t* M_dev, const int32_t* K_dev,
                    int precision, void* workspace, size_t workspace_bytes, void* stream);
 
+/* The x6 GEMM on pre-split operands (gemm_tp.hip), bit-identical to pcnn_gemm
+ * precision 2 on the same fp32 values, with no split work in its K loop.
+ * Tiled planes ("TP") of a rows x K operand: block (rb, ks) of 32 rows x 16 k
+ * is 3 KiB at ((rb * ceil(K/16) + ks) * 3) KiB, planes hi / mid / lo (the exact
+ * 3-way bf16 split), lane l of a plane holding row 32 rb + (l & 31),
+ * k 16 ks + 8 (l >> 5) .. + 7 (the MFMA operand fragment).
+ *  pcnn_tp_bytes: storage of one operand.
+ *  pcnn_split_tp: dst <- TP of the fp32 view src[row * row_stride + k * k_stride]
+ *    (rows, K capacities; effective counts from rows_dev / K_dev if non-NULL,
+ *    zeros past them; K steps past ceil(K_eff / 16) are not written).
+ *  pcnn_gemm_tp: C[M,N] = epilogue(A · B) with A_tp = TP of op(A) (M x K) and
+ *    B_tp = TP of op(B)^T (N x K), both stored at capacity K; epilogue, M_dev /
+ *    K_dev, dropout and workspace as pcnn_gemm_drop at precision 2. */
+size_t pcnn_tp_bytes(int rows, int K);
+int pcnn_split_tp(const float* src, long row_stride, long k_stride, int rows, const int32_t* rows_dev, int K,
+                  const int32_t* K_dev, void* dst, size_t dst_bytes, void* stream);
+int pcnn_gemm_tp(int M, int N, int K, const void* A_tp, const void* B_tp, float* Cm, int ldc, const float* bias,
+                 int act, const float* mask, int ldm, const uint8_t* drop, int ldd, float keep_prob,
+                 const int32_t* M_dev, const int32_t* K_dev, void* workspace, size_t workspace_bytes, void* stream);
+
 /* Dropout keep masks (the binary tensor of tf.nn.dropout: floor(keep_prob + U[0,1))):
  * mask[r, c] for r < min(*rows_dev, rows) (rows_dev may be NULL), c < cols, row
  * pitch ld >= cols bytes.  U comes from Philox4x32-10 (key = seed, counter =

@@ -82,6 +82,11 @@ _SIGS = {
     "pcnn_pose2d": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_float, c_float, c_float,
                             ctypes.c_uint64, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                             c_size_t, c_void_p]),
+    "pcnn_tp_bytes": (c_size_t, [c_int, c_int]),
+    "pcnn_split_tp": (c_int, [c_void_p, ctypes.c_long, ctypes.c_long, c_int, c_void_p, c_int, c_void_p, c_void_p,
+                              c_size_t, c_void_p]),
+    "pcnn_gemm_tp": (c_int, [c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p,
+                             c_int, c_void_p, c_int, c_float, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
     "pcnn_colsum": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     "pcnn_box_nms": (c_int, [c_void_p, c_int, c_int, c_void_p, c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
                              c_void_p, c_void_p, c_void_p]),

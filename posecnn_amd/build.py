@@ -13,7 +13,7 @@ OBJ = os.path.join(HERE, "build")
 OUT = os.path.join(HERE, "libposecnn_hip.so")
 SOURCES = ["capi.hip", "hough_compact.hip", "hough_vote.hip", "hough_peak.hip", "hough_emit.hip", "roi_pooling.hip",
            "average_distance.hip", "backprojecting.hip", "pose_head.hip", "gemm_x6.hip", "box_nms.hip",
-           "label_producer.hip", "icp.hip", "dropout.hip", "pose2d.hip"]
+           "label_producer.hip", "icp.hip", "dropout.hip", "pose2d.hip", "gemm_tp.hip"]
 HEADERS = [os.path.join(CSRC, "pcnn_common.h"), os.path.join(CSRC, "hough_common.h"), os.path.join(CSRC, "gemm_common.h"),
            os.path.join(HERE, "..", "include", "posecnn_hip.h")]
 # -ffp-contract=off: the parity arithmetic rounds every float op separately
@@ -23,7 +23,8 @@ FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fP
 # different load tuples into v_pk_add_f32, which forces register copies of the
 # freshly loaded tuples at the loop edge -- each behind a vmcnt wait that
 # exposes the full load latency every K step.
-FILE_FLAGS = {"pose_head.hip": ["-fno-slp-vectorize"], "gemm_x6.hip": ["-fno-slp-vectorize"]}
+FILE_FLAGS = {"pose_head.hip": ["-fno-slp-vectorize"], "gemm_x6.hip": ["-fno-slp-vectorize"],
+              "gemm_tp.hip": ["-fno-slp-vectorize"]}
 
 
 def _obj(src):

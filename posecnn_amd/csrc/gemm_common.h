@@ -162,6 +162,18 @@ __device__ __forceinline__ xf4 x_ld4(const XOp& o, unsigned voff, int soff) {
   return __builtin_bit_cast(xf4, __builtin_amdgcn_raw_buffer_load_b128(o.rs, voff, soff, 0));
 }
 
+// Exact three-way split of two fp32 values into packed bf16 (hi, mid, lo)
+// pairs: one pack-convert per plane; the fp32 value of a packed bf16 half is
+// a shift / mask of the pack; both subtractions are exact.  (gemm_x6.hip
+// splits while staging; gemm_tp.hip's producer splits once into planes.)
+__device__ __forceinline__ void x_split3(float a, float b, unsigned& hi, unsigned& mid, unsigned& lo) {
+  hi = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){a, b}, bf16x2));
+  const float ra = a - __uint_as_float(hi << 16), rb = b - __uint_as_float(hi & 0xffff0000u);
+  mid = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){ra, rb}, bf16x2));
+  const float sa = ra - __uint_as_float(mid << 16), sb = rb - __uint_as_float(mid & 0xffff0000u);
+  lo = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){sa, sb}, bf16x2));
+}
+
 // Epilogue of one tile (or split-K slice) of a split kernel: AM x AN
 // accumulator blocks of 32 x 32 per wave, the wave at rows wm * (T / 2),
 // columns wn * 32 AN of the tile.  One uniform branch (slab or C), otherwise

@@ -103,17 +103,6 @@ __device__ __forceinline__ void x6_load_part(const XOp& P, const XOp& P2, int r0
   v[4 * q + 0] = x[0]; v[4 * q + 1] = x[1]; v[4 * q + 2] = x[2]; v[4 * q + 3] = x[3];
 }
 
-// Exact three-way split of two fp32 values into packed bf16 (hi, mid, lo)
-// pairs: one pack-convert per plane; the fp32 value of a packed bf16 half is
-// a shift / mask of the pack; both subtractions are exact.
-__device__ __forceinline__ void x_split3(float a, float b, unsigned& hi, unsigned& mid, unsigned& lo) {
-  hi = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){a, b}, bf16x2));
-  const float ra = a - __uint_as_float(hi << 16), rb = b - __uint_as_float(hi & 0xffff0000u);
-  mid = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){ra, rb}, bf16x2));
-  const float sa = ra - __uint_as_float(mid << 16), sb = rb - __uint_as_float(mid & 0xffff0000u);
-  lo = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){sa, sb}, bf16x2));
-}
-
 // Part q of the split-and-store of a staged operand into its three planes
 // (pl, pl + part, pl + 2 part).  KC: row x6_kc_row(t) + (T/2) q, 4 k -> one
 // ds_write_b64 per plane.  NC: rows 4 (t >> 3) + 2q + {0, 1}, the k pair

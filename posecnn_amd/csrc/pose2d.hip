@@ -512,19 +512,26 @@ struct Layout {
 };
 
 Layout layout(int H, int W, int C, int n_hyp) {
-  pcnn::Carve cv(nullptr);
+  // byte offsets of the regions (256-B aligned) inside the caller's workspace
+  size_t off = 0;
+  auto take = [&](size_t bytes) {
+    off = pcnn::align_up(off, 256);
+    const size_t o = off;
+    off += bytes;
+    return o;
+  };
   Layout l;
-  l.colcnt = (size_t)(uintptr_t)cv.take<int32_t>((size_t)C * W);
-  l.coloff = (size_t)(uintptr_t)cv.take<int32_t>((size_t)C * W);
-  l.count = (size_t)(uintptr_t)cv.take<int32_t>(C);
-  l.lists = (size_t)(uintptr_t)cv.take<int32_t>((size_t)H * W);
-  l.listoff = (size_t)(uintptr_t)cv.take<int32_t>(C);
-  l.objs = (size_t)(uintptr_t)cv.take<int32_t>(C);
-  l.suboff = (size_t)(uintptr_t)cv.take<int32_t>((size_t)C * (kRounds + 1));
-  l.hyp = (size_t)(uintptr_t)cv.take<double>((size_t)n_hyp * 16);
+  l.colcnt = take((size_t)C * W * sizeof(int32_t));
+  l.coloff = take((size_t)C * W * sizeof(int32_t));
+  l.count = take((size_t)C * sizeof(int32_t));
+  l.lists = take((size_t)H * W * sizeof(int32_t));
+  l.listoff = take((size_t)C * sizeof(int32_t));
+  l.objs = take((size_t)C * sizeof(int32_t));
+  l.suboff = take((size_t)C * (kRounds + 1) * sizeof(int32_t));
+  l.hyp = take((size_t)n_hyp * 16 * sizeof(double));
   // subsets: a round visits at most every pixel of the class once
-  l.sub = (size_t)(uintptr_t)cv.take<int32_t>((size_t)kRounds * H * W);
-  l.total = cv.off + 256;
+  l.sub = take((size_t)kRounds * H * W * sizeof(int32_t));
+  l.total = off + 256;
   return l;
 }
 

@@ -709,6 +709,12 @@ __global__ void __launch_bounds__(256) k_head_bwd(const float* __restrict__ dpre
 
 }  // namespace
 
+namespace pcnn_gk {
+void launch_gemm_reduce(const GemmArgs& g, hipStream_t st) {
+  hipLaunchKernelGGL(k_gemm_reduce, dim3(1024), dim3(256), 0, st, g);
+}
+}  // namespace pcnn_gk
+
 static int x3_max_grid(int T) { return T == 256 ? XTile<256>::grid : XTile<128>::grid; }
 
 extern "C" size_t pcnn_gemm_workspace_size(int M, int N, int K, int m_dynamic, int precision) {

@@ -51,6 +51,44 @@ def gemm(A, B, C, a_trans=0, b_trans=0, A2=None, bias=None, act=0, mask=None, M_
     return C
 
 
+def tp_bytes(rows, K):
+    """Bytes of the tiled three-plane (hi / mid / lo bf16) form of a rows x K operand."""
+    return int(_lib.load().pcnn_tp_bytes(int(rows), int(K)))
+
+
+def split_tp(src, rows, K, out, row_stride, k_stride, rows_dev=None, K_dev=None, stream=None):
+    """out (uint8, >= tp_bytes(rows, K)) <- the tiled planes of the fp32 view
+    src[row * row_stride + k * k_stride] (zeros past rows_dev / K_dev); see
+    pcnn_split_tp in include/posecnn_hip.h."""
+    _lib.require_gpu(src, out)
+    if src.dtype != torch.float32 or out.dtype != torch.uint8 or not out.is_contiguous():
+        raise ValueError("split_tp: fp32 source, contiguous uint8 destination")
+    rc = _lib.load().pcnn_split_tp(_lib.ptr(src), int(row_stride), int(k_stride), int(rows), _lib.ptr(rows_dev),
+                                   int(K), _lib.ptr(K_dev), _lib.ptr(out), out.numel(), _lib.stream_ptr(stream))
+    _lib.check(rc, "split_tp")
+    return out
+
+
+def gemm_tp(A_tp, B_tp, C, M, N, K, bias=None, act=0, mask=None, drop=None, keep_prob=1.0, M_dev=None, K_dev=None,
+            stream=None):
+    """C[M,N] = epilogue(A @ B) from the tiled planes of op(A) (M x K) and of
+    op(B)^T (N x K) (split_tp); bit-identical to gemm(..., precision=2)."""
+    _lib.require_gpu(A_tp, B_tp, C)
+    for t in (C, bias, mask):
+        if t is not None and (t.dtype != torch.float32 or t.stride(-1) != 1):
+            raise ValueError("gemm_tp: fp32 outputs / epilogue operands with unit inner stride")
+    if drop is not None and (drop.dtype != torch.uint8 or drop.stride(-1) != 1):
+        raise ValueError("gemm_tp: drop must be uint8 with unit inner stride")
+    lib = _lib.load()
+    ws = _lib.workspace(lib.pcnn_gemm_workspace_size(M, N, K, int(M_dev is not None), 2), C.device, "gemm", stream)
+    rc = lib.pcnn_gemm_tp(int(M), int(N), int(K), _lib.ptr(A_tp), _lib.ptr(B_tp), _lib.ptr(C), C.stride(0),
+                          _lib.ptr(bias), int(act), _lib.ptr(mask), mask.stride(0) if mask is not None else 0,
+                          _lib.ptr(drop), drop.stride(0) if drop is not None else 0, float(keep_prob),
+                          _lib.ptr(M_dev), _lib.ptr(K_dev), _lib.ptr(ws), ws.numel(), _lib.stream_ptr(stream))
+    _lib.check(rc, "gemm_tp")
+    return C
+
+
 def dropout_mask(mask, keep_prob, seed, step_dev=None, stream_id=0, rows_dev=None, stream=None):
     """The binary tensor of tf.nn.dropout, floor(keep_prob + U[0,1)), into the
     uint8 (rows, cols) `mask` (Philox4x32-10 keyed on seed, the device step

@@ -16,7 +16,7 @@ fi
 pids=""
 for f in $(python3 -c "import sys; sys.path.insert(0, '.'); from posecnn_amd.build import SOURCES; print(' '.join(s[:-4] for s in SOURCES))"); do
   [ -f $C/$f.hip ] || continue  # a source the built revision does not have
-  extra=""; { [ $f = pose_head ] || [ $f = gemm_x6 ]; } && extra="-fno-slp-vectorize"
+  extra=""; { [ $f = pose_head ] || [ $f = gemm_x6 ] || [ $f = gemm_tp ]; } && extra="-fno-slp-vectorize"
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fPIC -Wno-unused-result $extra "$@" \
     -c $C/$f.hip -o scratch/$name.obj/$f.o &
   pids="$pids $!"

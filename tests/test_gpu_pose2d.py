@@ -43,7 +43,9 @@ def test_pose2d_matches_oracle(hip, noise, seed):
         t = poses[:, 3, c]
         got = np.array([fx * t[0] / t[2] + px, fy * t[1] / t[2] + py])
         want = np.array([fx * p["t"][0] / p["t"][2] + px, fy * p["t"][1] / p["t"][2] + py])
-        assert np.abs(got - want).max() < 3.0
+        # the known answer: exact coordinates put the centre on the truth; noisy
+        # ones (a 4-point P3P survivor, no refinement) within a few pixels
+        assert np.abs(got - want).max() < (0.1 if noise == 0.0 else 5.0)
 
 
 def test_pose2d_device_inputs_and_no_object(hip):
