@@ -270,7 +270,8 @@ int pcnn_gemm_drop(int M, int N, int K, const float* A, const float* A2, int lda
  *  pcnn_tp_bytes: storage of one operand.
  *  pcnn_split_tp: dst <- TP of the fp32 view src[row * row_stride + k * k_stride]
  *    (rows, K capacities; effective counts from rows_dev / K_dev if non-NULL,
- *    zeros past them; K steps past ceil(K_eff / 16) are not written).
+ *    zeros past them; row blocks past ceil(rows_eff / 32) and K steps past
+ *    ceil(K_eff / 16) are never multiplied and not written).
  *  pcnn_gemm_tp: C[M,N] = epilogue(A · B) with A_tp = TP of op(A) (M x K) and
  *    B_tp = TP of op(B)^T (N x K), both stored at capacity K; epilogue, M_dev /
  *    K_dev, dropout and workspace as pcnn_gemm_drop at precision 2. */

@@ -94,32 +94,44 @@ __global__ void __launch_bounds__(512, 1) k_gemm_tp(TpArgs p) {
   // the load cursor: (item, step within it), two flat steps ahead of compute
   int l_it = 0, l_s = 0;
   Item LI = item_of(0);
-  auto skip_empty = [&]() {
-    while (l_it < nitems && l_s >= LI.n) {
-      l_it++;
-      l_s = 0;
-      if (l_it < nitems) LI = item_of(l_it);
-    }
-  };
-  skip_empty();
-  // issue this wave's 6 pieces of the cursor's step into stage `st`
-  auto issue = [&](int st) {
+  // the cursor item's 6 source blocks of this wave (row-block base, K steps
+  // stored), refreshed only when the cursor moves to another item
+  const char* lsrc[kPiecesPerWave];
+  auto set_item = [&]() {
     const int m0 = pl.mi_of(LI.t) * pl.Tm, n0 = pl.ni_of(LI.t) * TT;
-    const int ks = LI.kl + l_s;
-    char* sb = xl + st * kStage;
 #pragma unroll
     for (int u = 0; u < kPiecesPerWave; u++) {
       const int q = wave + 8 * u;  // piece 0..47: [A | B] x block x plane
       const int op = q / 24, rem = q % 24, blk = rem / 3, plane = rem % 3;
-      const char* src;
       if (op == 0) {
         const int rb = min(m0 / 32 + blk, p.a_rb - 1);
-        src = p.A + ((size_t)(rb * p.a_ks + ks) * 3 + plane) * kPiece;
+        lsrc[u] = p.A + ((size_t)(rb * p.a_ks + LI.kl) * 3 + plane) * kPiece + lane * 16;
       } else {
         const int rb = min(n0 / 32 + blk, p.b_rb - 1);
-        src = p.B + ((size_t)(rb * p.b_ks + ks) * 3 + plane) * kPiece;
+        lsrc[u] = p.B + ((size_t)(rb * p.b_ks + LI.kl) * 3 + plane) * kPiece + lane * 16;
       }
-      glds16(src + lane * 16, sb + (op * 24 + blk * 3 + plane) * kPiece);
+    }
+  };
+  auto skip_empty = [&]() {
+    while (l_it < nitems && l_s >= LI.n) {
+      l_it++;
+      l_s = 0;
+      if (l_it < nitems) {
+        LI = item_of(l_it);
+        set_item();
+      }
+    }
+  };
+  set_item();
+  skip_empty();
+  // issue this wave's 6 pieces of the cursor's step into stage `st`
+  auto issue = [&](int st) {
+    char* sb = xl + st * kStage;
+#pragma unroll
+    for (int u = 0; u < kPiecesPerWave; u++) {
+      const int q = wave + 8 * u;
+      const int op = q / 24, rem = q % 24, blk = rem / 3, plane = rem % 3;
+      glds16(lsrc[u] + (size_t)l_s * kBlk3, sb + (op * 24 + blk * 3 + plane) * kPiece);
     }
     l_s++;
     skip_empty();
@@ -195,7 +207,8 @@ __global__ void __launch_bounds__(512, 1) k_gemm_tp(TpArgs p) {
 // TP producer: one wave per (32-row block, 16-k step): lane l converts row
 // 32 rb + (l & 31), k 16 ks + 8 (l >> 5) .. + 7 of the fp32 view
 // src[row * rs + k * kst] (zeros past rows_eff / K_eff) into its 16 B of each
-// plane.  K steps at or past ceil(K_eff / 16) are never read and not written.
+// plane.  Row blocks at or past ceil(rows_eff / 32) and K steps at or past
+// ceil(K_eff / 16) are never multiplied and not written.
 __global__ void __launch_bounds__(256) k_split_tp(const float* __restrict__ src, long rs, long kst, int rows,
                                                   const int32_t* __restrict__ rows_dev, int K,
                                                   const int32_t* __restrict__ K_dev, int n_rb, int ks_cap,
@@ -205,7 +218,9 @@ __global__ void __launch_bounds__(256) k_split_tp(const float* __restrict__ src,
   if (chunk >= (long)n_rb * ks_cap) return;
   const int rb = (int)(chunk / ks_cap), ks = (int)(chunk % ks_cap);
   const int Reff = eff_dim(rows, rows_dev), Keff = eff_dim(K, K_dev);
-  if (ks * 16 >= Keff && ks > 0) return;
+  // blocks wholly past the effective rows / K are never multiplied (the GEMM
+  // skips dead row blocks and stops at ceil(K_eff / 16)): not written
+  if ((ks * 16 >= Keff && ks > 0) || (rb * 32 >= Reff && rb > 0)) return;
   const int row = rb * 32 + (lane & 31), k0 = ks * 16 + 8 * (lane >> 5);
   float v[8];
 #pragma unroll

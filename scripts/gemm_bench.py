@@ -1,6 +1,7 @@
 """Time the pose step's nine FC GEMMs (R RoI rows, fp32 in HBM) one by one
 with HIP events; prints us and achieved TFLOP/s per shape.
-    python scripts/gemm_bench.py [--rows 405] [--precision 2[,1,0]] [--iters 20]"""
+    python scripts/gemm_bench.py [--rows 405] [--precision 2[,1,0,-1]] [--iters 20]
+(precision -1: the weight gradients on pre-split tiled planes, csrc/gemm_tp.hip)"""
 import argparse
 import sys
 
@@ -42,10 +43,26 @@ def cases_for(P):
     ]
 
 
+def tp_cases():
+    """The weight gradients on pre-split tiled planes (gemm_tp), the split
+    producers timed on their own."""
+    K6cap = CAP
+    a6, b6 = [torch.empty(ph.tp_bytes(n, K6cap), dtype=torch.uint8, device=D) for n in (K6, U)]
+    a7, b7 = [torch.empty(ph.tp_bytes(n, K6cap), dtype=torch.uint8, device=D) for n in (U, U)]
+    for src, rows, out in ((x5, K6, a6), (dy6, U, b6), (y6, U, a7), (dy7, U, b7)):
+        ph.split_tp(src, rows, CAP, out, 1, rows, K_dev=nr)
+    return [
+        ("split_x6T", 0, lambda: ph.split_tp(x5, K6, CAP, a6, 1, K6, K_dev=nr)),
+        ("split_dy6T", 0, lambda: ph.split_tp(dy6, U, CAP, b6, 1, U, K_dev=nr)),
+        ("fc6_dw_tp", 2 * R * K6 * U, lambda: ph.gemm_tp(a6, b6, gw6, K6, U, CAP, K_dev=nr)),
+        ("fc7_dw_tp", 2 * R * U * U, lambda: ph.gemm_tp(a7, b7, gw7, U, U, CAP, K_dev=nr)),
+    ]
+
+
 for P in [int(v) for v in a.precision.split(",")]:
     print(f"precision {P}", flush=True)
     tot = 0.0
-    for name, flops, fn in cases_for(P):
+    for name, flops, fn in (cases_for(P) if P >= 0 else tp_cases()):
         if a.only and name not in a.only.split(","):
             continue
         for _ in range(3):
@@ -59,5 +76,5 @@ for P in [int(v) for v in a.precision.split(",")]:
         torch.cuda.synchronize()
         us = e0.elapsed_time(e1) / a.iters * 1e3
         tot += us
-        print(f"{name:8s} {us:9.1f} us  {flops / us / 1e6:8.1f} TFLOP/s", flush=True)
+        print(f"{name:10s} {us:9.1f} us  {flops / us / 1e6:8.1f} TFLOP/s", flush=True)
     print(f"total    {tot:9.1f} us", flush=True)

