@@ -267,6 +267,18 @@ def main():
             legs[key] = {"value": round(gB * args.steps / t0_, 2), "unit": "frames/s",
                          "ms_per_step": round(t0_ / args.steps * 1e3, 4), "fc_gemm": desc, "timing": "eager"}
             del step0
+        # the same step without drop6 / drop7 (keep_prob 1, the test-time
+        # graph's pose head): what the reference's training dropout costs
+        step0 = PoseStep(B, H, W, C, dev, is_train=1, skip_pixels=10, global_batch=gB, batch_base=rank * B,
+                         dist=dist, precision=args.precision, weights=step.weights, keep_prob=1.0)
+        run0 = lambda: step0.step(inputs)
+        run0()
+        t0_ = measure(run0)
+        legs["no_dropout_step"] = {"value": round(gB * args.steps / t0_, 2), "unit": "frames/s",
+                                   "ms_per_step": round(t0_ / args.steps * 1e3, 4), "keep_prob": 1.0,
+                                   "timing": "eager",
+                                   "note": "the same step without drop6 / drop7; the line itself trains at 0.5"}
+        del step0
     elapsed = modes[mode]
     frames = gB * args.steps
     # per-step distribution of the reported mode (after the timed region, which

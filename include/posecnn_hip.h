@@ -236,7 +236,13 @@ int pcnn_backproject_bwd(const float* top_diff, const float* depth, const float*
  *             1 = split-bf16 x3 MFMA (hi*hi + hi*lo + lo*hi: ~2^-16 per product),
  *             2 = exact three-way split-bf16 x6 MFMA (hi/mid/lo planes, six
  *                 products: within 2^-24 |a||b| per product, fp32
- *                 accumulation -- fp32-faithful; the pose step's default)
+ *                 accumulation -- fp32-faithful; the pose step's default).
+ *                 Operand range: finite |x| <= 3.3895314e38 (the largest bf16);
+ *                 there results track fp32.  An inf / NaN operand, or a finite
+ *                 one above that bound (its hi plane rounds to inf), makes the
+ *                 output elements it reaches NaN (fp32 would give +-inf or a
+ *                 finite value); every other element is unaffected
+ *                 (tests/test_gpu_gemm_fc6.py::test_x6_edge_semantics).
  *  Deterministic (split-K partials are reduced in fixed order).
  *  workspace: >= pcnn_gemm_workspace_size() bytes, one per stream.
  * ------------------------------------------------------------------------- */
