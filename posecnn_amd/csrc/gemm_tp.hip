@@ -59,6 +59,12 @@ struct Item {
   int t, z, kl, n;
 };
 
+#ifdef PCNN_TP_NOREAD  // timing ablation (wrong results): operands from registers, no LDS fragment reads
+#define TP_FRAG(ptr) (fake)
+#else
+#define TP_FRAG(ptr) (*(const bf16x8*)(ptr))
+#endif
+
 template <bool GEN>
 __global__ void __launch_bounds__(512, 1) k_gemm_tp(TpArgs p) {
   extern __shared__ __attribute__((aligned(16))) char xl[];
@@ -78,6 +84,10 @@ __global__ void __launch_bounds__(512, 1) k_gemm_tp(TpArgs p) {
   const int lane = pcnn::lane_id(), wave = threadIdx.x >> 6;
   const int wm = wave / 4, wn = wave % 4;
   const int r = lane & 31, hsel = lane >> 5;
+#ifdef PCNN_TP_NOREAD
+  bf16x8 fake;
+  for (int e = 0; e < 8; e++) fake[e] = (__bf16)(float)((lane * 7 + e) & 15);
+#endif
   const int kstep = (pl.ns + pl.S - 1) / pl.S;
   auto item_of = [&](int it) {
     Item I;
@@ -158,9 +168,11 @@ __global__ void __launch_bounds__(512, 1) k_gemm_tp(TpArgs p) {
       for (int s = 0; s < I.n; s++, f++) {
         // this wave's pieces of step f landed (step f + 1's may still fly),
         // then every wave's, and every wave is done reading step f - 1's stage
+#ifndef PCNN_TP_NOBAR
         if (issued > f + 1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
+#endif
         if (l_it < nitems) {  // step f + 2 into the stage step f - 1 used
           issue((f + 2) % kNStage);
           issued++;
@@ -171,16 +183,16 @@ __global__ void __launch_bounds__(512, 1) k_gemm_tp(TpArgs p) {
 #pragma unroll
           for (int j = 0; j < 2; j++) {
             const char* bp = cur + (24 + (2 * wn + j) * 3) * kPiece + lane * 16;
-            bh[j] = *(const bf16x8*)(bp);
-            bm[j] = *(const bf16x8*)(bp + kPiece);
-            bl[j] = *(const bf16x8*)(bp + 2 * kPiece);
+            bh[j] = TP_FRAG(bp);
+            bm[j] = TP_FRAG(bp + kPiece);
+            bl[j] = TP_FRAG(bp + 2 * kPiece);
           }
 #pragma unroll
           for (int i = 0; i < AMW; i++) {
             const char* ap = cur + ((4 * wm + i) * 3) * kPiece + lane * 16;
-            const bf16x8 ah = *(const bf16x8*)(ap);
-            const bf16x8 am = *(const bf16x8*)(ap + kPiece);
-            const bf16x8 al = *(const bf16x8*)(ap + 2 * kPiece);
+            const bf16x8 ah = TP_FRAG(ap);
+            const bf16x8 am = TP_FRAG(ap + kPiece);
+            const bf16x8 al = TP_FRAG(ap + 2 * kPiece);
 #pragma unroll
             for (int j = 0; j < 2; j++) {  // smallest products first (k_gemm_x6's order)
               acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh[j], acc[i][j], 0, 0, 0);
@@ -199,6 +211,9 @@ __global__ void __launch_bounds__(512, 1) k_gemm_tp(TpArgs p) {
     else if (amw == 2) kloop(IC<2>{});
     else if (amw == 1) kloop(IC<1>{});
     else kloop(IC<0>{});
+#ifdef PCNN_TP_NOEPI
+    if (acc[0][0][0] == 1234.5f)  // ablation: stores only on an impossible value
+#endif
     x_epilogue<TT, 4>(g, pl, acc, m0, n0, rl, I.z, wm, wn, r, hsel);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA may outlive the workgroup

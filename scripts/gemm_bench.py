@@ -44,14 +44,24 @@ def cases_for(P):
 
 
 def tp_cases():
-    """The weight gradients on pre-split tiled planes (gemm_tp), the split
+    """The fc6 / fc7 GEMMs on pre-split tiled planes (gemm_tp), the split
     producers timed on their own."""
     K6cap = CAP
     a6, b6 = [torch.empty(ph.tp_bytes(n, K6cap), dtype=torch.uint8, device=D) for n in (K6, U)]
     a7, b7 = [torch.empty(ph.tp_bytes(n, K6cap), dtype=torch.uint8, device=D) for n in (U, U)]
     for src, rows, out in ((x5, K6, a6), (dy6, U, b6), (y6, U, a7), (dy7, U, b7)):
         ph.split_tp(src, rows, CAP, out, 1, rows, K_dev=nr)
+    # forward / dX shapes: op(B)^T of fc6 fwd is W6^T (4096 rows x K6), of fc6 dX W6 itself (K6 rows x 4096)
+    ax, w6f, dyx, w6d = (torch.empty(ph.tp_bytes(n, k), dtype=torch.uint8, device=D)
+                         for n, k in ((CAP, K6), (U, K6), (CAP, U), (K6, U)))
+    ph.split_tp(x5, CAP, K6, ax, K6, 1, rows_dev=nr)
+    ph.split_tp(w6, U, K6, w6f, 1, U)
+    ph.split_tp(dy6, CAP, U, dyx, U, 1, rows_dev=nr)
+    ph.split_tp(w6, K6, U, w6d, U, 1)
     return [
+        ("split_w6", 0, lambda: ph.split_tp(w6, U, K6, w6f, 1, U)),
+        ("fc6_fwd_tp", 2 * R * K6 * U, lambda: ph.gemm_tp(ax, w6f, y6, CAP, U, K6, act=1, M_dev=nr)),
+        ("fc6_dx_tp", 2 * R * K6 * U, lambda: ph.gemm_tp(dyx, w6d, dx, CAP, K6, U, M_dev=nr)),
         ("split_x6T", 0, lambda: ph.split_tp(x5, K6, CAP, a6, 1, K6, K_dev=nr)),
         ("split_dy6T", 0, lambda: ph.split_tp(dy6, U, CAP, b6, 1, U, K_dev=nr)),
         ("fc6_dw_tp", 2 * R * K6 * U, lambda: ph.gemm_tp(a6, b6, gw6, K6, U, CAP, K_dev=nr)),

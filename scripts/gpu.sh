@@ -11,7 +11,7 @@
 #   sq                  SQ instruction / stall counters of the eager step (two passes)
 #   ab V1,V2,...        alternating bench of the tree vs scratch/V.so (scripts/build_variant.sh)
 #   micro NAME          scripts/NAME.py microbench (gemm_bench, roi_bench, hough_bench, label_bench, pcie_rate)
-#   microab NAME V1,... alternating scripts/NAME.py runs of the tree vs scratch/V.so (two rounds)
+#   microab NAME V1,... alternating scripts/NAME.py $MICRO_ARGS runs of the tree vs scratch/V.so (two rounds)
 #   sqmicro NAME ARGS V1,...  the two SQ counter passes over scripts/NAME.py ARGS, tree and each scratch/V.so
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 O=$R/gpurun_out
@@ -74,7 +74,7 @@ while [ $# -gt 0 ]; do
         for v in tree "${vs[@]}"; do
           L=$R/posecnn_amd/libposecnn_hip.so; [ $v = tree ] || L=$R/scratch/$v.so
           echo "== $v" >> $O/${n}_ab.log
-          POSECNN_HIP_LIB=$L timeout -k 10 300 python scripts/$n.py >> $O/${n}_ab.log 2>&1 || exit 1
+          POSECNN_HIP_LIB=$L timeout -k 10 300 python scripts/$n.py $MICRO_ARGS >> $O/${n}_ab.log 2>&1 || exit 1
         done
       done ;;
     sqmicro)
