@@ -59,10 +59,10 @@ __global__ void __launch_bounds__(256) k_dropout_mask(uint8_t* __restrict__ mask
   }
   const uint64_t step = step_dev ? (uint64_t)*step_dev : 0;
   const int q4 = cols >> 2;
-  const long quads = (long)R * q4;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < quads; i += (long)gridDim.x * blockDim.x) {
-    const int r = (int)(i / q4), c = (int)(i - (long)r * q4) * 4;
-    const uint64_t e = (uint64_t)r * (uint64_t)q4 + (uint64_t)(c >> 2);  // element quad of a dense (rows, cols) mask
+  const int quads = R * q4;  // < 2^31 (checked by the host)
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < quads; i += gridDim.x * blockDim.x) {
+    const int r = i / q4, c = (i - r * q4) * 4;
+    const uint64_t e = (uint64_t)i;  // element quad of a dense (rows, cols) mask: r * q4 + c / 4
     const U4 o = philox4x32_10(U4{(uint32_t)e, (uint32_t)(e >> 32), stream_id, (uint32_t)step}, k0, k1);
     const uint32_t b = keep_bit(o.x, keep) | keep_bit(o.y, keep) << 8 | keep_bit(o.z, keep) << 16 |
                        keep_bit(o.w, keep) << 24;
@@ -87,7 +87,7 @@ __global__ void k_philox_check(const uint32_t* __restrict__ ctr, const uint32_t*
 extern "C" int pcnn_dropout_mask(uint8_t* mask, int rows, int cols, int ld, const int32_t* rows_dev, uint64_t seed,
                                  const int64_t* step_dev, int stream_id, float keep_prob, void* stream) {
   PCNN_REQUIRE(mask && rows >= 0 && cols > 0 && cols % 4 == 0 && ld >= cols && ld % 4 == 0 && ((uintptr_t)mask & 3) == 0);
-  PCNN_REQUIRE(keep_prob > 0.f && keep_prob <= 1.f && stream_id >= 0);
+  PCNN_REQUIRE(keep_prob > 0.f && keep_prob <= 1.f && stream_id >= 0 && (long)rows * (cols / 4) < (1l << 31));
   if (rows == 0) return PCNN_OK;
   const long quads = (long)rows * (cols / 4);
   long grid = (quads + 255) / 256;

@@ -134,6 +134,12 @@ __device__ __forceinline__ void x6_store_part(const float (&v)[8], char* pl, int
   }
 }
 
+#ifdef PCNN_X6_NOREAD  // timing ablation (wrong results): fragments from a register, no LDS reads
+#define X6_FRAG(ptr) (fake)
+#else
+#define X6_FRAG(ptr) (*(const bf16x8*)(ptr))
+#endif
+
 template <int T, bool A_T, bool B_T, bool RAGGED, bool A2, bool GEN>
 __global__ void __launch_bounds__(X6Tile<T>::threads, T == 256 ? 1 : 2) k_gemm_x6(GemmArgs g) {
   using X = X6Tile<T>;
@@ -159,6 +165,10 @@ __global__ void __launch_bounds__(X6Tile<T>::threads, T == 256 ? 1 : 2) k_gemm_x
   const int lane = pcnn::lane_id(), wave = threadIdx.x >> 6;
   const int wm = wave / X::wn, wn = wave % X::wn;
   const int r = lane & 31, hsel = lane >> 5;
+#ifdef PCNN_X6_NOREAD
+  bf16x8 fake;
+  for (int e = 0; e < 8; e++) fake[e] = (__bf16)(float)((lane * 7 + e) & 15);
+#endif
   const long a_el = A_T ? (long)(g.K - 1) * g.lda + g.M : (long)(g.M - 1) * g.lda + g.K;
   const long b_el = B_T ? (long)(g.N - 1) * g.ldb + g.K : (long)(g.K - 1) * g.ldb + g.N;
   const XOp oa = x_op(g.A, g.lda, a_el), oa2 = x_op(g.A2, g.lda, a_el), ob = x_op(g.B, g.ldb, b_el),
@@ -246,24 +256,24 @@ __global__ void __launch_bounds__(X6Tile<T>::threads, T == 256 ? 1 : 2) k_gemm_x
             bf16x8 bh[2], bm[2], bl[2];
 #pragma unroll
             for (int j = 0; j < 2; j++) {
-              bh[j] = *(const bf16x8*)(cur + 3 * PART + b_off[j]);
-              bm[j] = *(const bf16x8*)(cur + 4 * PART + b_off[j]);
-              bl[j] = *(const bf16x8*)(cur + 5 * PART + b_off[j]);
+              bh[j] = X6_FRAG(cur + 3 * PART + b_off[j]);
+              bm[j] = X6_FRAG(cur + 4 * PART + b_off[j]);
+              bl[j] = X6_FRAG(cur + 5 * PART + b_off[j]);
             }
             if constexpr (MODE == 2) {
 #pragma unroll
               for (int p = 0; p < 4; p++) stage_part(p, nxt, kn);
             }
             bf16x8 ah[2], am[2], al[2];
-            ah[0] = *(const bf16x8*)(cur + a_off[0]);
-            am[0] = *(const bf16x8*)(cur + PART + a_off[0]);
-            al[0] = *(const bf16x8*)(cur + 2 * PART + a_off[0]);
+            ah[0] = X6_FRAG(cur + a_off[0]);
+            am[0] = X6_FRAG(cur + PART + a_off[0]);
+            al[0] = X6_FRAG(cur + 2 * PART + a_off[0]);
 #pragma unroll
             for (int i = 0; i < AMW; i++) {
               if (i + 1 < AMW) {  // the next row's A fragments in flight under this row's MFMAs
-                ah[(i + 1) & 1] = *(const bf16x8*)(cur + a_off[i + 1]);
-                am[(i + 1) & 1] = *(const bf16x8*)(cur + PART + a_off[i + 1]);
-                al[(i + 1) & 1] = *(const bf16x8*)(cur + 2 * PART + a_off[i + 1]);
+                ah[(i + 1) & 1] = X6_FRAG(cur + a_off[i + 1]);
+                am[(i + 1) & 1] = X6_FRAG(cur + PART + a_off[i + 1]);
+                al[(i + 1) & 1] = X6_FRAG(cur + 2 * PART + a_off[i + 1]);
               }
               const int c = i & 1;
               if constexpr (STAGE_FIRST) {

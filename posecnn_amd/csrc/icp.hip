@@ -729,51 +729,138 @@ __global__ void __launch_bounds__(kBlk) k_score_scatter(const float* __restrict_
   }
 }
 
-constexpr int kScoreTile = 2048;  // depth points per LDS tile
+// Nearest depth point within the radius through a uniform grid (advisor
+// finding: the brute-force M x M scan grows with the square of the object's
+// pixel count).  Cells of edge s = 1.001 r: a point closer than r to q differs
+// from it by < 0.999 cells per axis (cell coordinates from double products,
+// whose rounding is far below the margin for any |coordinate| < 10^7 m), so
+// it lies in one of the 27 cells around q's.  Cells hash into kGridBuckets
+// buckets (counting sort of the depth-point indices); every point of every
+// bucket visited is tested with the brute force's exact arithmetic, so the
+// result -- the smallest squared distance < r^2, ties to the lowest index --
+// is the same (a hash collision only adds candidates; a bucket visited twice
+// changes nothing).
+constexpr int kGridBuckets = 1 << 17;
+
+__device__ __forceinline__ bool grid_cell(float x, float y, float z, double inv_s, int& cx, int& cy, int& cz) {
+  // in double: the product's rounding stays far below the 0.001-cell margin
+  const double fx = floor((double)x * inv_s), fy = floor((double)y * inv_s), fz = floor((double)z * inv_s);
+  if (!(fabs(fx) < 1e9 && fabs(fy) < 1e9 && fabs(fz) < 1e9)) return false;  // NaN / inf (never within r)
+  cx = (int)fx;
+  cy = (int)fy;
+  cz = (int)fz;
+  return true;
+}
+
+__device__ __forceinline__ int grid_bucket(int cx, int cy, int cz) {
+  return (int)(((unsigned)cx * 73856093u ^ (unsigned)cy * 19349663u ^ (unsigned)cz * 83492791u) &
+               (unsigned)(kGridBuckets - 1));
+}
+
+__device__ __forceinline__ int score_m(const int32_t* __restrict__ cnt, int nseg, int* ish) {
+  int c = 0;
+  for (int s = threadIdx.x; s < nseg; s += kBlk) c += cnt[s];
+  return block_sum_int<kBlk>(c, ish);
+}
+
+// depth point -> bucket count (points outside the grid's range go nowhere:
+// no query can be within r of them)
+__global__ void __launch_bounds__(kBlk) k_grid_count(const float4* __restrict__ dpts, const int32_t* __restrict__ cnt,
+                                                     int nseg, double inv_s, int32_t* __restrict__ bcount,
+                                                     int32_t* __restrict__ bucket_of) {
+  __shared__ int ish[kBlk / 64];
+  const int M = score_m(cnt, nseg, ish);
+  const int i = blockIdx.x * kBlk + threadIdx.x;
+  if ((int)blockIdx.x * kBlk >= M || i >= M) return;
+  const float4 d = dpts[i];
+  int cx, cy, cz;
+  int b = -1;
+  if (grid_cell(d.x, d.y, d.z, inv_s, cx, cy, cz)) {
+    b = grid_bucket(cx, cy, cz);
+    atomicAdd(bcount + b, 1);
+  }
+  bucket_of[i] = b;
+}
+
+// exclusive scan of the bucket counts (one workgroup): start[b], start[NB] = total; cursor = start
+__global__ void __launch_bounds__(1024) k_grid_scan(const int32_t* __restrict__ bcount, int32_t* __restrict__ start,
+                                                    int32_t* __restrict__ cursor) {
+  __shared__ int part[1024];
+  constexpr int per = kGridBuckets / 1024;
+  const int t = threadIdx.x;
+  int s = 0;
+  for (int k = 0; k < per; k++) s += bcount[t * per + k];
+  part[t] = s;
+  __syncthreads();
+  for (int off = 1; off < 1024; off <<= 1) {  // Hillis-Steele inclusive scan
+    const int v = t >= off ? part[t - off] : 0;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  int run = part[t] - s;
+  for (int k = 0; k < per; k++) {
+    const int b = t * per + k;
+    start[b] = run;
+    cursor[b] = run;
+    run += bcount[b];
+  }
+  if (t == 1023) start[kGridBuckets] = run;
+}
+
+__global__ void __launch_bounds__(kBlk) k_grid_fill(const int32_t* __restrict__ cnt, int nseg,
+                                                    const int32_t* __restrict__ bucket_of, int32_t* __restrict__ cursor,
+                                                    int32_t* __restrict__ idx) {
+  __shared__ int ish[kBlk / 64];
+  const int M = score_m(cnt, nseg, ish);
+  const int i = blockIdx.x * kBlk + threadIdx.x;
+  if ((int)blockIdx.x * kBlk >= M || i >= M) return;
+  const int b = bucket_of[i];
+  if (b >= 0) idx[atomicAdd(cursor + b, 1)] = i;
+}
 
 // grid (query blocks, hypotheses): nearest depth point of each transformed
 // model point, flagged when within the radius
 __global__ void __launch_bounds__(kBlk) k_score_nn(const float4* __restrict__ model, const float4* __restrict__ dpts,
                                                    const int32_t* __restrict__ cnt, int nseg,
-                                                   const float* __restrict__ hyps, float r2,
+                                                   const float* __restrict__ hyps, float r2, double inv_s,
+                                                   const int32_t* __restrict__ start, const int32_t* __restrict__ idx,
                                                    uint8_t* __restrict__ flags, int cap) {
-  __shared__ float4 tile[kScoreTile];
   __shared__ int ish[kBlk / 64];
-  int c = 0;
-  for (int s = threadIdx.x; s < nseg; s += kBlk) c += cnt[s];
-  const int M = block_sum_int<kBlk>(c, ish);
+  const int M = score_m(cnt, nseg, ish);
   const int h = blockIdx.y;
   const int q = blockIdx.x * kBlk + threadIdx.x;
-  if ((int)blockIdx.x * kBlk >= M) return;  // block-uniform
+  if ((int)blockIdx.x * kBlk >= M || q >= M) return;
   const float* P = hyps + (size_t)h * 7;
   const float qn = sqrtf(P[0] * P[0] + P[1] * P[1] + P[2] * P[2] + P[3] * P[3]);
   const Quat qq = {P[0] / qn, P[1] / qn, P[2] / qn, P[3] / qn};
-  float x = 0.f, y = 0.f, z = 0.f;
-  if (q < M) {
-    const float4 m = model[q];
-    rotate(qq, m.x, m.y, m.z, x, y, z);
-    x = x + P[4];
-    y = y + P[5];
-    z = z + P[6];
-  }
+  float x, y, z;
+  const float4 m = model[q];
+  rotate(qq, m.x, m.y, m.z, x, y, z);
+  x = x + P[4];
+  y = y + P[5];
+  z = z + P[6];
+  int cx, cy, cz;
+  if (!grid_cell(x, y, z, inv_s, cx, cy, cz)) return;
   float best = r2;  // strict: only squared distances < r2 qualify
   int bi = -1;
-  for (int t0 = 0; t0 < M; t0 += kScoreTile) {
-    const int tn = min(kScoreTile, M - t0);
-    __syncthreads();
-    for (int i = threadIdx.x; i < tn; i += kBlk) tile[i] = dpts[t0 + i];
-    __syncthreads();
-    for (int i = 0; i < tn; i++) {
-      const float4 d = tile[i];
-      const float dx = x - d.x, dy = y - d.y, dz = z - d.z;
-      const float d2 = dx * dx + dy * dy + dz * dz;
-      if (d2 < best) {  // ties keep the lower index
-        best = d2;
-        bi = t0 + i;
+  for (int dz = -1; dz <= 1; dz++)
+    for (int dy = -1; dy <= 1; dy++)
+      for (int dx = -1; dx <= 1; dx++) {
+        const int b = grid_bucket(cx + dx, cy + dy, cz + dz);
+        const int e = start[b + 1];
+        for (int k = start[b]; k < e; k++) {
+          const int i = idx[k];
+          const float4 d = dpts[i];
+          const float ex = x - d.x, ey = y - d.y, ez = z - d.z;
+          const float d2 = ex * ex + ey * ey + ez * ez;
+          if (d2 < best || (bi >= 0 && d2 == best && i < bi)) {  // the first minimum in index order
+            best = d2;
+            bi = i;
+          }
+        }
       }
-    }
-  }
-  if (q < M && bi >= 0) flags[(size_t)h * cap + bi] = 1;
+  if (bi >= 0) flags[(size_t)h * cap + bi] = 1;
 }
 
 // score per hypothesis and the first best one (one workgroup)
@@ -968,6 +1055,11 @@ extern "C" size_t pcnn_icp_score_workspace_size(int J, int H, int W) {
   cv.take<float4>((size_t)HW);
   cv.take<float4>((size_t)HW);
   cv.take<uint8_t>((size_t)J * HW);
+  cv.take<int32_t>((size_t)kGridBuckets);      // bucket counts
+  cv.take<int32_t>((size_t)kGridBuckets + 1);  // bucket starts
+  cv.take<int32_t>((size_t)kGridBuckets);      // fill cursors
+  cv.take<int32_t>((size_t)HW);                // bucket of each depth point
+  cv.take<int32_t>((size_t)HW);                // point indices by bucket
   return cv.off + 256;
 }
 
@@ -982,14 +1074,26 @@ extern "C" int pcnn_icp_score(const float* live, const int32_t* label, int obj, 
   float4* model = cv.take<float4>((size_t)HW);
   float4* dpts = cv.take<float4>((size_t)HW);
   uint8_t* flags = cv.take<uint8_t>((size_t)J * HW);
+  int32_t* bcount = cv.take<int32_t>((size_t)kGridBuckets);
+  int32_t* bstart = cv.take<int32_t>((size_t)kGridBuckets + 1);
+  int32_t* cursor = cv.take<int32_t>((size_t)kGridBuckets);
+  int32_t* bucket_of = cv.take<int32_t>((size_t)HW);
+  int32_t* idx = cv.take<int32_t>((size_t)HW);
   if (workspace_bytes < cv.off) return PCNN_ECAPACITY;
+  PCNN_REQUIRE(radius > 0.f && radius < 1e6f);
   hipStream_t st = (hipStream_t)stream;
   if (hipMemsetAsync(flags, 0, (size_t)J * HW, st) != hipSuccess) return PCNN_EHIP;
+  if (hipMemsetAsync(bcount, 0, (size_t)kGridBuckets * sizeof(int32_t), st) != hipSuccess) return PCNN_EHIP;
+  const double inv_s = 1.0 / ((double)radius * 1.001);
+  const unsigned qblocks = (unsigned)((HW + kBlk - 1) / kBlk);
   hipLaunchKernelGGL(k_score_count, dim3(nseg), dim3(kBlk), 0, st, live, label, obj, vertmap, HW, nseg, cnt);
   hipLaunchKernelGGL(k_score_scatter, dim3(nseg), dim3(kBlk), 0, st, live, label, obj, vertmap, HW, nseg, cnt, model,
                      dpts);
-  hipLaunchKernelGGL(k_score_nn, dim3((HW + kBlk - 1) / kBlk, J), dim3(kBlk), 0, st, model, dpts, cnt, nseg, hyps,
-                     radius * radius, flags, HW);
+  hipLaunchKernelGGL(k_grid_count, dim3(qblocks), dim3(kBlk), 0, st, dpts, cnt, nseg, inv_s, bcount, bucket_of);
+  hipLaunchKernelGGL(k_grid_scan, dim3(1), dim3(1024), 0, st, bcount, bstart, cursor);
+  hipLaunchKernelGGL(k_grid_fill, dim3(qblocks), dim3(kBlk), 0, st, cnt, nseg, bucket_of, cursor, idx);
+  hipLaunchKernelGGL(k_score_nn, dim3(qblocks, J), dim3(kBlk), 0, st, model, dpts, cnt, nseg, hyps, radius * radius,
+                     inv_s, bstart, idx, flags, HW);
   hipLaunchKernelGGL(k_score_select, dim3(1), dim3(kBlk), 0, st, flags, cnt, nseg, J, HW, score, choose);
   PCNN_CHECK_LAUNCH();
   return PCNN_OK;

@@ -40,7 +40,7 @@ class PoseStep:
     def __init__(self, B, H, W, num_classes, device, conv4_hw=None, conv5_hw=None, channels=512, units=4096,
                  is_train=1, skip_pixels=10, vote_threshold=-1.0, vote_percentage=0.02, margin=0.01,
                  global_batch=None, batch_base=0, weights=None, dist=None, backward=True, precision=2,
-                 overlap_weight_grads=True, pixel_argmax=True, keep_prob=None, drop_seed=0x5EED):
+                 overlap_weight_grads=True, pixel_argmax=True, keep_prob=None, drop_seed=0x5EED, side_prep=True):
         self.B, self.H, self.W, self.C = B, H, W, num_classes
         self.dev = device
         self.is_train, self.skip, self.vthr, self.vper, self.margin = is_train, skip_pixels, vote_threshold, \
@@ -126,6 +126,11 @@ class PoseStep:
         self._in_step = False  # forward() inside step(): the loss all-reduce is joined at the step's end
         # weight-gradient branch of the backward (None: everything on the caller's stream)
         self.side_stream = torch.cuda.Stream(device=device) if overlap_weight_grads else None
+        # the post-vote side work (dropout keep masks, the ADD loss's row
+        # classification): on the side stream beside the RoI pool (True), or
+        # on the step's stream with no fork / join (False: masks right after
+        # the vote, the row classification right before the loss)
+        self.side_prep = side_prep and self.side_stream is not None
 
     # ------------------------------------------------------------------
     def _t(self, name):
@@ -158,7 +163,7 @@ class PoseStep:
             self.add_ws = torch.empty(adl.workspace_bytes(CAP, self.C, points.shape[1]), dtype=torch.uint8,
                                       device=self.dev)
         h = self.hough
-        side = self.side_stream if self.timer is None else None
+        side = self.side_stream if self.timer is None and self.side_prep else None
         if side is not None:
             side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side or torch.cuda.current_stream()):
@@ -178,12 +183,12 @@ class PoseStep:
 
     def draw_drop_masks(self):
         """This step's drop6 / drop7 keep masks (Philox, keyed on the device
-        step counter so graph replays draw new ones), on the side stream; the
-        fc6 forward waits for them."""
+        step counter so graph replays draw new ones), on the side stream (the
+        fc6 forward waits for them) or, without side_prep, on the step's stream."""
         if self.keep >= 1.0 or self._drop_external:
             return
         nr = self.hough["num_rois"][1:2]
-        side = self.side_stream if self.timer is None else None
+        side = self.side_stream if self.timer is None and self.side_prep else None
         if side is not None:
             side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side or torch.cuda.current_stream()):
@@ -257,7 +262,7 @@ class PoseStep:
             ph.head_fwd(self.y8, h["weight"], self.t8, self.pred, num_rois=nr)
             if not getattr(self, "_prepped", False):  # forward() called without step()
                 self.add_prep(points, symmetry)
-            if self.timer is None and self.side_stream is not None:
+            if self.timer is None and self.side_prep:
                 torch.cuda.current_stream().wait_stream(self.side_stream)  # the row classes (add_prep)
             self._prepped = False
             # the previous step's in-place loss all-reduce must be done before
@@ -349,7 +354,8 @@ class PoseStep:
     def step(self, inputs):
         self.vote(inputs["label"], inputs["vertex"], inputs["extents"], inputs["meta"], inputs["gt"])
         self.draw_drop_masks()
-        self.add_prep(inputs["points"], inputs["symmetry"])
+        if self.side_prep:  # else forward() classifies the rows right before the loss
+            self.add_prep(inputs["points"], inputs["symmetry"])
         self.exchange()
         if self.dist is not None:  # the RoI / pose all-gather: started here, joined at the end of the step
             with self._t("allgather_rois"):

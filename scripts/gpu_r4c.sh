@@ -15,6 +15,14 @@ for i in 1 2; do
       >> $O/dwblk_ab.log || exit 1
   done
 done
+: > $O/x6noread_ab.log
+for i in 1 2; do
+  for v in tree x6noread; do
+    L=$PWD/posecnn_amd/libposecnn_hip.so; [ $v = tree ] || L=$PWD/scratch/$v.so
+    echo "== $v" >> $O/x6noread_ab.log
+    POSECNN_HIP_LIB=$L timeout -k 10 120 python scripts/gemm_bench.py --only fc6_fwd,fc6_dx,fc6_dw,fc7_fwd,fc7_dx >> $O/x6noread_ab.log 2>&1 || exit 1
+  done
+done
 timeout -k 10 300 python scripts/pose2d_bench.py > $O/pose2d_bench.json 2> $O/pose2d_bench.err || exit 1
 timeout -k 10 600 python bench.py > $O/bench_full2.json 2> $O/bench_full2.err || exit 1
 echo "exit=0"

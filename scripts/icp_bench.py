@@ -68,6 +68,25 @@ res = {"metric": "refined hypotheses/s (8-iteration df::icp on 640x480 maps)",
                     "bytes_per_iteration": iter_bytes,
                     "note": "step + solve launches per iteration; latency-bound at this size"},
        "data": "synthetic (ray-cast box, tests/refine_scene.py)"}
+# SegICP score of 8 hypotheses (grid-bucketed nearest-point search) on the
+# scene's object and on a dense 640x480 cloud (every pixel one object point)
+hyps8 = t(np.repeat(sc["init"].astype(np.float32)[None], 8, 0))
+vm_obj = t(sc["pred"]["vertmap"])
+score_scene_us = timed(lambda: R.icp_score(lv[0], lab, sc["cls"], vm_obj, hyps8))
+rng = np.random.default_rng(0)
+dense_live = (rng.uniform(-0.15, 0.15, (H, W, 3)) + np.array([0, 0, 1.0])).astype(np.float32)
+dense_vm = rng.uniform(-0.15, 0.15, (H, W, 3)).astype(np.float32)
+dense_vm[..., 0] += 1.0
+dense_lab = t(np.ones((H, W), np.int32))
+dh = np.zeros((8, 7), np.float32)
+dh[:, 0] = 1.0
+dh[:, 6] = 1.0 + 0.002 * np.arange(8)
+dl, dv, dhy = t(dense_live), t(dense_vm), t(dh)
+score_dense_us = timed(lambda: R.icp_score(dl, dense_lab, 1, dv, dhy))
+res["icp_score_us"] = {"scene_object": round(score_scene_us, 1), "dense_640x480": round(score_dense_us, 1),
+                       "scene_object_points": int(((sc["live"]["label"] == sc["cls"])).sum()),
+                       "dense_points": H * W, "hypotheses": 8,
+                       "note": "pcnn_icp_score: compaction, 1 cm grid buckets, nearest depth point per model point"}
 # solve_icp end to end (live vertices, re-centring, Nelder-Mead on optEnergy,
 # 8 hypotheses x ICP, SegICP score) for a RoIs of one frame, the renderer a
 # GPU ray-caster standing in for the reference's OpenGL pass

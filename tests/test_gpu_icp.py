@@ -117,6 +117,38 @@ def test_icp_score_matches_oracle(hip, orc):
     assert int(ch[0]) == cho
 
 
+def test_icp_score_grid_ties_and_far_points(hip, orc):
+    """The grid-bucketed nearest-point search against the oracle's brute force
+    on a dense lattice cloud: depth and model points on a 4 mm lattice (many
+    candidates per 1 cm radius, exact distance ties -> the lowest index wins),
+    duplicated depth points, points far from the camera (60 m) and a
+    hypothesis that moves the model onto them, and one that misses all."""
+    from posecnn_amd.synthesize import icp as R
+    H, W, obj = 48, 64, 3
+    rng = np.random.default_rng(7)
+    lat = rng.integers(-6, 7, size=(H * W, 3)).astype(np.float32) * 0.004
+    live = (lat + np.array([0.0, 0.0, 0.8], np.float32)).astype(np.float32)
+    live[100:140] = live[60:100]                          # exact duplicates: ties by index
+    live[-50:] += np.array([0.0, 0.0, 60.0], np.float32)  # far points
+    model = rng.integers(-6, 7, size=(H * W, 3)).astype(np.float32) * 0.004
+    vm = model.copy()
+    vm[:, 0] += obj                                        # the class offset in x's integer part
+    label = np.full((H, W), obj, np.int32)
+    label[0, :5] = 0                                       # not the object
+    hyps = np.zeros((4, 7), np.float32)
+    hyps[:, 0] = 1.0
+    hyps[0, 6] = 0.8                                       # onto the lattice: exact ties
+    hyps[1, 4:] = (0.001, -0.002, 0.803)
+    hyps[2, 6] = 60.8                                      # onto the far points
+    hyps[3, 6] = 5.0                                       # misses everything
+    hyps[1, :4] = (0.9995, 0.02, -0.01, 0.0)
+    s, ch = R.icp_score(t(live.reshape(H, W, 3)), t(label), obj, t(vm.reshape(H, W, 3)), t(hyps))
+    so, cho = orc.icp_score(live.reshape(H, W, 3), label, obj, vm.reshape(H, W, 3), hyps)
+    np.testing.assert_array_equal(s.cpu().numpy(), so)
+    assert int(ch[0]) == cho
+    assert so[0] > 0 and so[2] > 0 and so[3] == 0
+
+
 def test_solve_icp_end_to_end(hip, orc):
     """The solveICP flow (synthesize.cpp:2052-2395) with the box ray-caster as
     the renderer: poses_new is the re-centred pose (no Nelder-Mead stage here),

@@ -109,3 +109,35 @@ def test_pose_step_vs_fp64_autograd(hip, orc, drop):
             a = np.where(a == 0xFFFF, -1, a * CH + np.arange(CH))
         od = orc.roi_pool_bwd(dx.reshape(n, 7, 7, CH), a.astype(np.int32), tuple(data.shape), box, 7, 7, s, 0)
         np.testing.assert_array_equal(dconv.cpu().numpy(), od)
+
+
+def test_step_side_prep_placement_is_bitwise_neutral(hip):
+    """PoseStep(side_prep=False) runs the dropout masks and the ADD row
+    classification on the step's own stream (no fork / join) instead of the
+    side stream: the same kernels on the same data, so every output of two
+    steps (masks drawn from the device step counter each step) is bit-identical."""
+    fr = synth.make_frames(B, H=H, W=W, num_classes=C, objects_per_image=4, seed=92)
+    g = torch.Generator().manual_seed(5)
+    conv4 = torch.randn((B, H // 8, W // 8, CH), generator=g)
+    conv5 = torch.randn((B, H // 16, W // 16, CH), generator=g)
+    pts, sym = synth.rescaled_points(C)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(D)
+    inputs = dict(label=t(fr["label"]), vertex=t(fr["vertex"]), extents=t(fr["extents"]), meta=t(fr["meta"]),
+                  gt=t(fr["gt"]), conv4=conv4.to(D), conv5=conv5.to(D), points=t(pts), symmetry=t(sym))
+    outs = []
+    weights = None
+    for side_prep in (True, False):
+        step = PoseStep(B, H, W, C, D, channels=CH, units=UNITS, is_train=1, skip_pixels=3, weights=weights,
+                        side_prep=side_prep)
+        weights = step.weights
+        res = []
+        for _ in range(2):
+            loss = step.step(inputs)
+            torch.cuda.synchronize()
+            res.append([loss.clone(), step.drop6.clone(), step.drop7.clone(), step.y7.clone(), step.dx.clone(),
+                        step.dconv4.clone(), step.grads["w6"].clone(), step.grads["b7"].clone()])
+        outs.append(res)
+    for a_step, b_step in zip(*outs):
+        for a, b in zip(a_step, b_step):
+            assert torch.equal(a, b)
+    assert not torch.equal(outs[0][0][1], outs[0][1][1])  # the second step drew new masks
