@@ -267,6 +267,19 @@ int pcnn_gemm_drop(int M, int N, int K, const float* A, const float* A2, int lda
                    const uint8_t* drop, int ldd, float keep_prob, const int32_t* M_dev, const int32_t* K_dev,
                    int precision, void* workspace, size_t workspace_bytes, void* stream);
 
+/* The forward of pcnn_gemm_drop with the keep mask drawn in the epilogue: the
+ * reduce pass draws, for every live element (m < effective M, n < N), the bit
+ * pcnn_dropout_mask would write for a dense (M, N) mask with the same seed,
+ * *step_dev and stream_id, applies C = (v / keep_prob) * bit, and stores the
+ * bits into drop_out (uint8 (M, ldd)) for the backward (pcnn_gemm_drop with
+ * mask).  Bit-identical to pcnn_dropout_mask (rows_dev = M_dev) followed by
+ * pcnn_gemm_drop, without the mask launch.  N % 4 == 0, ldd % 4 == 0. */
+int pcnn_gemm_drop_gen(int M, int N, int K, const float* A, const float* A2, int lda, int a_trans, const float* B,
+                       int ldb, int b_trans, float* Cm, int ldc, const float* bias, int act, uint8_t* drop_out,
+                       int ldd, float keep_prob, uint64_t seed, const int64_t* step_dev, int stream_id,
+                       const int32_t* M_dev, const int32_t* K_dev, int precision, void* workspace,
+                       size_t workspace_bytes, void* stream);
+
 /* The x6 GEMM on pre-split operands (gemm_tp.hip), bit-identical to pcnn_gemm
  * precision 2 on the same fp32 values, with no split work in its K loop.
  * Tiled planes ("TP") of a rows x K operand: block (rb, ks) of 32 rows x 16 k

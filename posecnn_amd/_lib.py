@@ -75,6 +75,9 @@ _SIGS = {
     "pcnn_gemm_drop": (c_int, [c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_int,
                                c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_float, c_void_p,
                                c_void_p, c_int, c_void_p, c_size_t, c_void_p]),
+    "pcnn_gemm_drop_gen": (c_int, [c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_int,
+                                   c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_float, ctypes.c_uint64,
+                                   c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_size_t, c_void_p]),
     "pcnn_dropout_mask": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, ctypes.c_uint64, c_void_p, c_int, c_float,
                                   c_void_p]),
     "pcnn_philox_check": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p]),

@@ -13,40 +13,11 @@
 // in device memory so that a captured HIP graph draws fresh masks on every
 // replay (the caller bumps it once per step).
 #include "pcnn_common.h"
+#include "pcnn_philox.h"
 
 namespace {
 
-struct U4 {
-  uint32_t x, y, z, w;
-};
-
-__host__ __device__ __forceinline__ void mulhilo(uint32_t a, uint32_t b, uint32_t& hi, uint32_t& lo) {
-  const uint64_t p = (uint64_t)a * b;
-  hi = (uint32_t)(p >> 32);
-  lo = (uint32_t)p;
-}
-
-// Philox4x32 with 10 rounds (Random123 constants)
-__host__ __device__ __forceinline__ U4 philox4x32_10(U4 c, uint32_t k0, uint32_t k1) {
-  constexpr uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u, W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
-#pragma unroll
-  for (int r = 0; r < 10; r++) {
-    uint32_t h0, l0, h1, l1;
-    mulhilo(M0, c.x, h0, l0);
-    mulhilo(M1, c.z, h1, l1);
-    c = U4{h1 ^ c.y ^ k0, l1, h0 ^ c.w ^ k1, l0};
-    k0 += W0;
-    k1 += W1;
-  }
-  return c;
-}
-
-// TF's Uint32ToFloat (random_distributions.h): 23 random mantissa bits -> [1, 2) - 1
-__device__ __forceinline__ float u01(uint32_t x) { return __uint_as_float((x & 0x7fffffu) | 0x3f800000u) - 1.0f; }
-
-__device__ __forceinline__ uint32_t keep_bit(uint32_t x, float keep) {
-  return floorf(keep + u01(x)) >= 1.0f ? 1u : 0u;
-}
+using namespace pcnn_philox;
 
 __global__ void __launch_bounds__(256) k_dropout_mask(uint8_t* __restrict__ mask, int rows, int cols, int ld,
                                                       const int32_t* __restrict__ rows_dev, uint32_t k0, uint32_t k1,
@@ -63,10 +34,7 @@ __global__ void __launch_bounds__(256) k_dropout_mask(uint8_t* __restrict__ mask
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < quads; i += gridDim.x * blockDim.x) {
     const int r = i / q4, c = (i - r * q4) * 4;
     const uint64_t e = (uint64_t)i;  // element quad of a dense (rows, cols) mask: r * q4 + c / 4
-    const U4 o = philox4x32_10(U4{(uint32_t)e, (uint32_t)(e >> 32), stream_id, (uint32_t)step}, k0, k1);
-    const uint32_t b = keep_bit(o.x, keep) | keep_bit(o.y, keep) << 8 | keep_bit(o.z, keep) << 16 |
-                       keep_bit(o.w, keep) << 24;
-    *(uint32_t*)(mask + (size_t)r * ld + c) = b;
+    *(uint32_t*)(mask + (size_t)r * ld + c) = keep_quad(e, k0, k1, stream_id, (uint32_t)step, keep);
   }
 }
 

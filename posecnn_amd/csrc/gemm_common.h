@@ -42,6 +42,12 @@ struct GemmArgs {
   const uint8_t* drop;
   int ldd;
   float keep;  // keep_prob; 1 = no dropout
+  // drop_gen: the reduce draws the keep bits itself (Philox, pcnn_philox.h;
+  // the same bits pcnn_dropout_mask writes for a dense (M, N) mask) and
+  // stores them into drop for the backward
+  int drop_gen;
+  uint32_t drop_k0, drop_k1, drop_sid;
+  const int64_t* drop_step;
 };
 
 // The dropout part of the epilogue, after bias / act / mask: tf.nn.dropout's

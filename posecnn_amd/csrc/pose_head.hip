@@ -16,6 +16,7 @@
 // fixed order by a second kernel that also applies the epilogue (bit-stable
 // across runs).  The pool5 + pool4 addition is fused into the A-tile load.
 #include "gemm_common.h"
+#include "pcnn_philox.h"
 #include <math.h>
 #include <stdlib.h>
 
@@ -564,11 +565,23 @@ __global__ void __launch_bounds__(XTile<T>::threads, T == 256 ? 1 : 2) k_gemm_x3
   }
 }
 
+// drop_gen: keep byte of element (m, n), drawn (element quad m N/4 + n/4) and
+// stored for the backward; the lane whose n is the quad's first stores all four
+__device__ __forceinline__ float drop_gen_epi(float v, const GemmArgs& g, uint32_t step, int m, int n) {
+  const uint32_t q = pcnn_philox::keep_quad((uint64_t)m * (uint64_t)(g.N >> 2) + (uint64_t)(n >> 2), g.drop_k0,
+                                            g.drop_k1, g.drop_sid, step, g.keep);
+  if ((n & 3) == 0) *(uint32_t*)((uint8_t*)g.drop + (size_t)m * g.ldd + n) = q;
+  if (g.keep != 1.f) v = v / g.keep;
+  return v * (float)((q >> (8 * (n & 3))) & 1u);
+}
+
 __global__ void __launch_bounds__(256) k_gemm_reduce(GemmArgs g) {
   const int Meff = eff_dim(g.M, g.M_dev);
   const int Keff = eff_dim(g.K, g.K_dev);
   const int S = g.prec ? x_plan(Meff, g.N, Keff, g.tile, g.xgrid, split_bk(g.prec)).S : split_for(Meff, g.N, Keff);
   const bool dr = g.drop || g.keep != 1.f;
+  const uint32_t step = g.drop_gen && g.drop_step ? (uint32_t)*g.drop_step : 0u;
+  auto dropv = [&](float v, int m, int n) { return g.drop_gen ? drop_gen_epi(v, g, step, m, n) : drop_epi(v, g, m, n); };
   if (S == 1) {
     // whole tiles: the GEMM's own epilogue wrote bias / act / mask; dropout
     // (or the backward's 1 / keep) is applied here, in place
@@ -577,7 +590,7 @@ __global__ void __launch_bounds__(256) k_gemm_reduce(GemmArgs g) {
     for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
       const int m = (int)(i / g.N), n = (int)(i % g.N);
       float* c = g.C + (size_t)m * g.ldc + n;
-      *c = drop_epi(*c, g, m, n);
+      *c = dropv(*c, m, n);
     }
     return;
   }
@@ -600,8 +613,17 @@ __global__ void __launch_bounds__(256) k_gemm_reduce(GemmArgs g) {
       }
       float4 o = make_float4(epilogue(v.x, g, m, n), epilogue(v.y, g, m, n + 1), epilogue(v.z, g, m, n + 2),
                              epilogue(v.w, g, m, n + 3));
-      if (dr) o = make_float4(drop_epi(o.x, g, m, n), drop_epi(o.y, g, m, n + 1), drop_epi(o.z, g, m, n + 2),
-                              drop_epi(o.w, g, m, n + 3));
+      if (g.drop_gen) {  // one Philox block per float4: the element quad
+        const uint32_t q = pcnn_philox::keep_quad((uint64_t)i, g.drop_k0, g.drop_k1, g.drop_sid, step, g.keep);
+        *(uint32_t*)((uint8_t*)g.drop + (size_t)m * g.ldd + n) = q;
+        o = make_float4((g.keep != 1.f ? o.x / g.keep : o.x) * (float)(q & 1u),
+                        (g.keep != 1.f ? o.y / g.keep : o.y) * (float)((q >> 8) & 1u),
+                        (g.keep != 1.f ? o.z / g.keep : o.z) * (float)((q >> 16) & 1u),
+                        (g.keep != 1.f ? o.w / g.keep : o.w) * (float)((q >> 24) & 1u));
+      } else if (dr) {
+        o = make_float4(drop_epi(o.x, g, m, n), drop_epi(o.y, g, m, n + 1), drop_epi(o.z, g, m, n + 2),
+                        drop_epi(o.w, g, m, n + 3));
+      }
       *(float4*)(g.C + (size_t)m * g.ldc + n) = o;
     }
     return;
@@ -612,7 +634,7 @@ __global__ void __launch_bounds__(256) k_gemm_reduce(GemmArgs g) {
     float v = 0.f;
     for (int z = 0; z < S; z++) v += g.slab[((size_t)z * g.M + m) * g.N + n];
     v = epilogue(v, g, m, n);
-    g.C[(size_t)m * g.ldc + n] = dr ? drop_epi(v, g, m, n) : v;
+    g.C[(size_t)m * g.ldc + n] = dr ? dropv(v, m, n) : v;
   }
 }
 
@@ -738,12 +760,14 @@ extern "C" int pcnn_gemm(int M, int N, int K, const float* A, const float* A2, i
                         M_dev, K_dev, precision, workspace, workspace_bytes, stream);
 }
 
-extern "C" int pcnn_gemm_drop(int M, int N, int K, const float* A, const float* A2, int lda, int a_trans,
-                              const float* B, int ldb, int b_trans, float* Cm, int ldc, const float* bias, int act,
-                              const float* mask, int ldm, const uint8_t* drop, int ldd, float keep_prob,
-                              const int32_t* M_dev, const int32_t* K_dev, int precision, void* workspace,
-                              size_t workspace_bytes, void* stream) {
+static int gemm_impl(int M, int N, int K, const float* A, const float* A2, int lda, int a_trans, const float* B,
+                     int ldb, int b_trans, float* Cm, int ldc, const float* bias, int act, const float* mask, int ldm,
+                     const uint8_t* drop, int ldd, float keep_prob, const int32_t* M_dev, const int32_t* K_dev,
+                     int precision, void* workspace, size_t workspace_bytes, void* stream, int drop_gen,
+                     uint64_t seed, const int64_t* step_dev, int stream_id) {
   PCNN_REQUIRE(M >= 0 && N > 0 && K >= 0 && A && B && Cm);
+  PCNN_REQUIRE(!drop_gen || (drop && N % 4 == 0 && ldd % 4 == 0 && ((uintptr_t)drop & 3) == 0 && stream_id >= 0 &&
+                             (long)M * (N / 4) < (1l << 31)));
   PCNN_REQUIRE(keep_prob > 0.f && keep_prob <= 1.f);
   PCNN_REQUIRE(!drop || (ldd >= N && (long)M * ldd < (1l << 31)));
   PCNN_REQUIRE(precision >= 0 && precision <= 2);
@@ -760,6 +784,13 @@ extern "C" int pcnn_gemm_drop(int M, int N, int K, const float* A, const float* 
     return PCNN_ECAPACITY;
   GemmArgs g{M, N, K, A, A2, lda, B, ldb, Cm, ldc, bias, act, mask, ldm, M_dev, K_dev, (float*)workspace, precision,
              tile_x3(M, N, K), 0, 0, drop, ldd, keep_prob};
+  if (drop_gen) {
+    g.drop_gen = 1;
+    g.drop_k0 = (uint32_t)seed;
+    g.drop_k1 = (uint32_t)(seed >> 32);
+    g.drop_sid = (uint32_t)stream_id;
+    g.drop_step = step_dev;
+  }
   hipStream_t st = (hipStream_t)stream;
   if (precision == 1 || precision == 2) {
     // ragged edges: a KC operand whose K (or device-side K) is not a multiple of
@@ -850,6 +881,25 @@ extern "C" int pcnn_gemm_drop(int M, int N, int K, const float* A, const float* 
   if (may_split) hipLaunchKernelGGL(k_gemm_reduce, dim3(1024), dim3(256), 0, st, g);
   PCNN_CHECK_LAUNCH();
   return PCNN_OK;
+}
+
+extern "C" int pcnn_gemm_drop(int M, int N, int K, const float* A, const float* A2, int lda, int a_trans,
+                              const float* B, int ldb, int b_trans, float* Cm, int ldc, const float* bias, int act,
+                              const float* mask, int ldm, const uint8_t* drop, int ldd, float keep_prob,
+                              const int32_t* M_dev, const int32_t* K_dev, int precision, void* workspace,
+                              size_t workspace_bytes, void* stream) {
+  return gemm_impl(M, N, K, A, A2, lda, a_trans, B, ldb, b_trans, Cm, ldc, bias, act, mask, ldm, drop, ldd, keep_prob,
+                   M_dev, K_dev, precision, workspace, workspace_bytes, stream, 0, 0, nullptr, 0);
+}
+
+extern "C" int pcnn_gemm_drop_gen(int M, int N, int K, const float* A, const float* A2, int lda, int a_trans,
+                                  const float* B, int ldb, int b_trans, float* Cm, int ldc, const float* bias, int act,
+                                  uint8_t* drop_out, int ldd, float keep_prob, uint64_t seed,
+                                  const int64_t* step_dev, int stream_id, const int32_t* M_dev, const int32_t* K_dev,
+                                  int precision, void* workspace, size_t workspace_bytes, void* stream) {
+  return gemm_impl(M, N, K, A, A2, lda, a_trans, B, ldb, b_trans, Cm, ldc, bias, act, nullptr, 0, drop_out, ldd,
+                   keep_prob, M_dev, K_dev, precision, workspace, workspace_bytes, stream, 1, seed, step_dev,
+                   stream_id);
 }
 
 extern "C" int pcnn_colsum(const float* X, int M, int N, int ldx, const int32_t* M_dev, float* out, void* stream) {

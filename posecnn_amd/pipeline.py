@@ -40,7 +40,8 @@ class PoseStep:
     def __init__(self, B, H, W, num_classes, device, conv4_hw=None, conv5_hw=None, channels=512, units=4096,
                  is_train=1, skip_pixels=10, vote_threshold=-1.0, vote_percentage=0.02, margin=0.01,
                  global_batch=None, batch_base=0, weights=None, dist=None, backward=True, precision=2,
-                 overlap_weight_grads=True, pixel_argmax=True, keep_prob=None, drop_seed=0x5EED, side_prep=True):
+                 overlap_weight_grads=True, pixel_argmax=True, keep_prob=None, drop_seed=0x5EED, side_prep=True,
+                 drop_in_reduce=True):
         self.B, self.H, self.W, self.C = B, H, W, num_classes
         self.dev = device
         self.is_train, self.skip, self.vthr, self.vper, self.margin = is_train, skip_pixels, vote_threshold, \
@@ -104,6 +105,8 @@ class PoseStep:
             raise ValueError("keep_prob must be in (0, 1]")
         self.drop6 = self.drop7 = None
         self._drop_external = False
+        self.drop_in_reduce = drop_in_reduce  # keep bits drawn in the fc6 / fc7 reduce epilogues
+        self._bump_drop_step = False
         if self.keep < 1.0:
             u8 = dict(dtype=torch.uint8, device=device)
             self.drop6 = torch.zeros((CAP, units), **u8)
@@ -183,9 +186,12 @@ class PoseStep:
 
     def draw_drop_masks(self):
         """This step's drop6 / drop7 keep masks (Philox, keyed on the device
-        step counter so graph replays draw new ones), on the side stream (the
-        fc6 forward waits for them) or, without side_prep, on the step's stream."""
-        if self.keep >= 1.0 or self._drop_external:
+        step counter so graph replays draw new ones) as separate launches, on
+        the side stream (the fc6 forward waits for them) or, without side_prep,
+        on the step's stream.  Only with drop_in_reduce=False: by default the
+        fc6 / fc7 forward reduces draw the same bits in their epilogue
+        (pcnn_gemm_drop_gen) and store them for the backward."""
+        if self.keep >= 1.0 or self._drop_external or self.drop_in_reduce:
             return
         nr = self.hough["num_rois"][1:2]
         side = self.side_stream if self.timer is None and self.side_prep else None
@@ -246,12 +252,20 @@ class PoseStep:
         if self.keep < 1.0 and getattr(self, "_drop_ready", None) is not None:
             torch.cuda.current_stream().wait_event(self._drop_ready)  # this step's keep masks (side stream)
             self._drop_ready = None
+        gen = self.keep < 1.0 and self.drop_in_reduce and not self._drop_external
+        g6 = dict(drop_gen=(self.drop_seed, self.drop_step, 6)) if gen else {}
+        g7 = dict(drop_gen=(self.drop_seed, self.drop_step, 7)) if gen else {}
         with self._t("gemm_fc6_fwd"):
-            self._g("fc6_fwd", x, w.w6, self.y6, bias=w.b6, act=1, M_dev=nr, drop=self.drop6, **dk)
+            self._g("fc6_fwd", x, w.w6, self.y6, bias=w.b6, act=1, M_dev=nr, drop=self.drop6, **dk, **g6)
         if gs is not None:
             gs.send_input("w7", self.y6)
         with self._t("gemm_fc7_fc8_fwd"):
-            self._g("fc7_fwd", self.y6, w.w7, self.y7, bias=w.b7, act=1, M_dev=nr, drop=self.drop7, **dk)
+            self._g("fc7_fwd", self.y6, w.w7, self.y7, bias=w.b7, act=1, M_dev=nr, drop=self.drop7, **dk, **g7)
+        if gen:  # the step counter moves on once both masks are drawn
+            if self._in_step and self.backward:
+                self._bump_drop_step = True  # at the end of the data-gradient chain, beside the dW tail
+            else:
+                self.drop_step.add_(1)
             if gs is not None:
                 gs.send_input("w8", self.y7)
             self._g("fc8_fwd", self.y7, w.w8, self.y8, bias=w.b8, act=0, M_dev=nr)
@@ -333,6 +347,9 @@ class PoseStep:
                              batch_base=self.batch_base)
             rp.roi_pool_grad(conv4, h["box"], self.arg4, dxp, 7, 7, 1.0 / 8.0, 0, num_rois=nr, out=self.dconv4,
                              batch_base=self.batch_base)
+        if self._bump_drop_step:  # next step's dropout draws (off the critical path: the side stream's tail runs)
+            self.drop_step.add_(1)
+            self._bump_drop_step = False
         if side is not None:
             main.wait_stream(side)
 

@@ -16,11 +16,13 @@ from . import _lib
 
 
 def gemm(A, B, C, a_trans=0, b_trans=0, A2=None, bias=None, act=0, mask=None, M_dev=None, K_dev=None, M=None,
-         N=None, K=None, precision=2, drop=None, keep_prob=1.0, stream=None):
+         N=None, K=None, precision=2, drop=None, keep_prob=1.0, drop_gen=None, stream=None):
     """C[M,N] = epilogue(op(A) (+ op(A2)) @ op(B)); see pcnn_gemm / pcnn_gemm_drop in
     include/posecnn_hip.h.  drop (uint8 (M, >=N) 0/1) applies tf.nn.dropout after
     the activation, (v / keep_prob) * drop; with mask, keep_prob scales the kept
-    gradient (v / keep_prob: the backward of relu + dropout)."""
+    gradient (v / keep_prob: the backward of relu + dropout).  drop_gen =
+    (seed, step_dev, stream_id): the reduce draws the keep bits itself (as
+    dropout_mask would) and writes them into drop (pcnn_gemm_drop_gen)."""
     _lib.require_gpu(A, B, C)
     for t in (A, B, C, A2, bias, mask):
         if t is not None and (t.dtype != torch.float32 or t.stride(-1) != 1):
@@ -36,7 +38,18 @@ def gemm(A, B, C, a_trans=0, b_trans=0, A2=None, bias=None, act=0, mask=None, M_
     lib = _lib.load()
     ws = _lib.workspace(lib.pcnn_gemm_workspace_size(M, N, K, int(M_dev is not None), precision), C.device, "gemm",
                         stream)
-    if drop is None and keep_prob == 1.0:
+    if drop_gen is not None:
+        if drop is None or mask is not None:
+            raise ValueError("gemm: drop_gen needs the drop output buffer and no mask (forward only)")
+        seed, step_dev, sid = drop_gen
+        if step_dev is not None and (step_dev.dtype != torch.int64 or not step_dev.is_cuda):
+            raise ValueError("gemm: drop_gen's step counter must be an int64 device tensor")
+        rc = lib.pcnn_gemm_drop_gen(M, N, K, _lib.ptr(A), _lib.ptr(A2), A.stride(0), int(a_trans), _lib.ptr(B),
+                                    B.stride(0), int(b_trans), _lib.ptr(C), C.stride(0), _lib.ptr(bias), int(act),
+                                    _lib.ptr(drop), drop.stride(0), float(keep_prob), int(seed) & ((1 << 64) - 1),
+                                    _lib.ptr(step_dev), int(sid), _lib.ptr(M_dev), _lib.ptr(K_dev), int(precision),
+                                    _lib.ptr(ws), ws.numel(), _lib.stream_ptr(stream))
+    elif drop is None and keep_prob == 1.0:
         rc = lib.pcnn_gemm(M, N, K, _lib.ptr(A), _lib.ptr(A2), A.stride(0), int(a_trans), _lib.ptr(B), B.stride(0),
                            int(b_trans), _lib.ptr(C), C.stride(0), _lib.ptr(bias), int(act), _lib.ptr(mask),
                            mask.stride(0) if mask is not None else 0, _lib.ptr(M_dev), _lib.ptr(K_dev),

@@ -5,7 +5,7 @@
 # refinement timings.  Stops at the first failure.
 cd ${GRAFT_REPO_ROOT:-$(dirname "$0")/..}
 O=gpurun_out; mkdir -p $O
-timeout -k 10 600 python -u -m pytest tests/test_gpu_icp.py tests/test_gpu_step.py -m gpu -x -v --timeout 300 \
+timeout -k 10 600 python -u -m pytest tests/test_gpu_icp.py tests/test_gpu_step.py tests/test_gpu_dropout.py tests/test_gpu_step_full.py -m gpu -x -v --timeout 300 \
   --timeout-method thread -p no:cacheprovider > $O/t_d.log 2>&1 || { echo "tests failed"; exit 1; }
 : > $O/prep_ab.log
 for i in 1 2 3; do

@@ -114,3 +114,38 @@ def test_gemm_drop_rejects_bad_keep(hip):
         ph.gemm(A, A, A.clone(), keep_prob=1.5)
     with pytest.raises(ValueError):
         ph.gemm(A, A, A.clone(), drop=torch.ones((4, 4), device=D), keep_prob=0.5)  # not uint8
+
+
+@pytest.mark.parametrize("precision", [2, 0])
+@pytest.mark.parametrize("shape", [(405, 4096, 4096, True), (1152, 512, 96, False), (77, 300, 1000, True)])
+def test_gemm_drop_gen_matches_mask_kernel(hip, precision, shape):
+    """pcnn_gemm_drop_gen (keep bits drawn in the reduce epilogue) against the
+    mask kernel + pcnn_gemm_drop: the same output bit for bit and the same
+    bits stored (oracle/philox.py), rows past the device-side M untouched --
+    on the split-K float4 reduce (fc7's forward), the in-place whole-tile pass
+    and the element-wise reduce (an output pitch that is not a multiple of 4)."""
+    M, N, K, mdev = shape
+    g = torch.Generator(device=D)
+    g.manual_seed(M * 7 + N + K)
+    A = torch.randn((M, K), generator=g, device=D)
+    Bm = torch.randn((K, N), generator=g, device=D) * 0.05
+    bias = torch.randn((N,), generator=g, device=D) * 0.1
+    keep, seed, sid = 0.5, 0x5EED + (1 << 40), 6
+    step = torch.tensor([9], dtype=torch.int64, device=D)
+    m_eff = M - 3 if mdev else M
+    Md = torch.tensor([m_eff], dtype=torch.int32, device=D) if mdev else None
+    mask = torch.full((M, N), 7, dtype=torch.uint8, device=D)
+    ph.dropout_mask(mask, keep, seed, step, sid, rows_dev=Md)
+    pad = 1 if M == 77 else 0  # an output pitch that is not a multiple of 4: the element-wise reduce
+    C_ref = torch.zeros((M, N + pad), device=D)[:, :N]
+    ph.gemm(A, Bm, C_ref, bias=bias, act=1, M_dev=Md, precision=precision, drop=mask, keep_prob=keep)
+    drop = torch.full((M, N), 7, dtype=torch.uint8, device=D)
+    C = torch.zeros((M, N + pad), device=D)[:, :N]
+    ph.gemm(A, Bm, C, bias=bias, act=1, M_dev=Md, precision=precision, drop=drop, keep_prob=keep,
+            drop_gen=(seed, step, sid))
+    torch.cuda.synchronize()
+    assert torch.equal(C, C_ref)
+    np.testing.assert_array_equal(drop[:m_eff].cpu().numpy(), philox.dropout_mask(m_eff, N, seed, 9, sid, keep))
+    assert bool((drop[m_eff:] == 7).all())
+    with pytest.raises(ValueError):
+        ph.gemm(A, Bm, C, drop=drop, mask=C_ref, keep_prob=keep, drop_gen=(seed, step, sid))
