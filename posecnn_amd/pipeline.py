@@ -129,10 +129,10 @@ class PoseStep:
         self._in_step = False  # forward() inside step(): the loss all-reduce is joined at the step's end
         # weight-gradient branch of the backward (None: everything on the caller's stream)
         self.side_stream = torch.cuda.Stream(device=device) if overlap_weight_grads else None
-        # the post-vote side work (dropout keep masks, the ADD loss's row
-        # classification): on the side stream beside the RoI pool (True), or
-        # on the step's stream with no fork / join (False: masks right after
-        # the vote, the row classification right before the loss)
+        # the post-vote side work (the ADD loss's row classification, and the
+        # dropout keep masks when drop_in_reduce is off): on the side stream
+        # beside the RoI pool (True), or on the step's stream with no fork /
+        # join (False: the row classification right before the loss)
         self.side_prep = side_prep and self.side_stream is not None
 
     # ------------------------------------------------------------------
@@ -261,14 +261,14 @@ class PoseStep:
             gs.send_input("w7", self.y6)
         with self._t("gemm_fc7_fc8_fwd"):
             self._g("fc7_fwd", self.y6, w.w7, self.y7, bias=w.b7, act=1, M_dev=nr, drop=self.drop7, **dk, **g7)
+            if gs is not None:
+                gs.send_input("w8", self.y7)
+            self._g("fc8_fwd", self.y7, w.w8, self.y8, bias=w.b8, act=0, M_dev=nr)
         if gen:  # the step counter moves on once both masks are drawn
             if self._in_step and self.backward:
                 self._bump_drop_step = True  # at the end of the data-gradient chain, beside the dW tail
             else:
                 self.drop_step.add_(1)
-            if gs is not None:
-                gs.send_input("w8", self.y7)
-            self._g("fc8_fwd", self.y7, w.w8, self.y8, bias=w.b8, act=0, M_dev=nr)
         if self.dist is not None:
             self._wait("rows")
             self.norm_rows.clamp_(min=1)
