@@ -49,6 +49,8 @@ def parse():
     p.add_argument("--precision", type=int, choices=[0, 1, 2], default=2,
                    help="FC GEMMs: 2 = exact 3-way split-bf16 x6 MFMA (fp32-faithful, default), "
                         "1 = split-bf16 x3 MFMA (~2^-16 per product), 0 = fp32 MFMA")
+    p.add_argument("--mask-kernel", action="store_true",
+                   help="draw the dropout masks with their own kernel (PoseStep drop_in_reduce=False), for A/Bs")
     p.add_argument("--prep-on-main", action="store_true",
                    help="dropout masks and ADD row classification on the step's stream (PoseStep side_prep=False)")
     p.add_argument("--no-fp32-leg", "--no-precision-legs", dest="no_legs", action="store_true",
@@ -112,7 +114,7 @@ def main():
     if full:
         step = PoseStep(B, H, W, C, dev, is_train=1, skip_pixels=10, global_batch=gB, batch_base=rank * B,
                         dist=dist, precision=args.precision, pixel_argmax=not args.flat_argmax,
-                        side_prep=not args.prep_on_main)
+                        side_prep=not args.prep_on_main, drop_in_reduce=not args.mask_kernel)
         run = lambda: step.step(inputs)
     if linemod:  # + the depth back-projection op, forward and backward (no reference caller)
         from posecnn_amd.backprojecting_layer import backprojecting_op as bpo

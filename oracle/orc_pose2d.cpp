@@ -151,14 +151,22 @@ int quartic_roots(const double* c, double* out) {
   cd w(1, 0);
   for (int k = 0; k < 4; k++) { z[k] = w * bound; w *= seed; }
   auto pe = [&](cd x) { return (((x + a[3]) * x + a[2]) * x + a[1]) * x + a[0]; };
-  for (int it = 0; it < 200; it++)
+  // up to 200 sweeps, stopping at the first whose steps are all below 1e-13
+  // of their root (pose2d.hip stops at the same sweep)
+  for (int it = 0; it < 200; it++) {
+    double mstep = 0;
     for (int k = 0; k < 4; k++) {
       cd den(1, 0);
       for (int j = 0; j < 4; j++)
         if (j != k) den *= (z[k] - z[j]);
       if (den == cd(0, 0)) continue;
-      z[k] -= pe(z[k]) / den;
+      const cd st = pe(z[k]) / den;
+      z[k] -= st;
+      mstep = std::max(mstep, (std::fabs(st.real()) + std::fabs(st.imag())) /
+                                  (1 + std::fabs(z[k].real()) + std::fabs(z[k].imag())));
     }
+    if (mstep < 1e-13) break;
+  }
   int n = 0;
   for (int k = 0; k < 4; k++) {
     if (!(std::fabs(z[k].imag()) <= 1e-6 * (1 + std::abs(z[k])))) continue;

@@ -334,23 +334,8 @@ __global__ void __launch_bounds__(X6Tile<T>::threads, T == 256 ? 1 : 2) k_gemm_x
   };
 
   const int kstep = (pl.ns + pl.S - 1) / pl.S;  // split-K: K steps per slice
-#ifdef PCNN_DW_BLOCK2D
-  // 2-D blocked order for whole-tile plans: XCD x owns an (mt / 2) x (nt / 4)
-  // block of tiles, so per round it keeps nt / 4 B panels (not all nt) in L2
-  const bool blk2d = !GEN && !pl.m_fast && active % 8 == 0 && pl.mt % 2 == 0 && pl.nt % 4 == 0 &&
-                     pl.tiles % active == 0;
-#endif
   for (int item = wg; item < pl.tiles * pl.S; item += active) {
-    int z = item / pl.tiles, t = item % pl.tiles;
-#ifdef PCNN_DW_BLOCK2D
-    if (blk2d) {
-      const int q = active / 8, w = item % active;
-      const int x = w / q, l = (item / active) * q + w % q;
-      const int bm = pl.mt / 2, bn = pl.nt / 4;
-      t = ((x / 4) * bm + l / bn) * pl.nt + (x % 4) * bn + l % bn;
-      z = 0;
-    }
-#endif
+    const int z = item / pl.tiles, t = item % pl.tiles;
     const int kl = z * kstep;
     segment(t, kl, min(pl.ns, kl + kstep), z);
   }

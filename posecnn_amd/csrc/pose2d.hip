@@ -154,7 +154,11 @@ __device__ int quartic_roots(const double* c, double* out) {
     z[k] = {w.re * bound, w.im * bound};
     w = cmul(w, sd);
   }
-  for (int it = 0; it < 200; it++)
+  // up to 200 sweeps, stopping at the first sweep whose steps are all below
+  // 1e-13 of their root (the oracle stops at the same sweep: identical IEEE
+  // double operations on both sides)
+  for (int it = 0; it < 200; it++) {
+    double mstep = 0;
     for (int k = 0; k < 4; k++) {
       Cx den{1, 0};
       for (int j = 0; j < 4; j++)
@@ -164,8 +168,12 @@ __device__ int quartic_roots(const double* c, double* out) {
       p = cadd(cmul(p, z[k]), Cx{a[2], 0});
       p = cadd(cmul(p, z[k]), Cx{a[1], 0});
       p = cadd(cmul(p, z[k]), Cx{a[0], 0});
-      z[k] = csub(z[k], cdiv(p, den));
+      const Cx st = cdiv(p, den);
+      z[k] = csub(z[k], st);
+      mstep = fmax(mstep, (fabs(st.re) + fabs(st.im)) / (1 + fabs(z[k].re) + fabs(z[k].im)));
     }
+    if (mstep < 1e-13) break;
+  }
   int n = 0;
   for (int k = 0; k < 4; k++) {
     const double az = sqrt(z[k].re * z[k].re + z[k].im * z[k].im);
@@ -307,13 +315,19 @@ struct P2dWs {
   double* hyp;       // (n_hyp, 16): obj, R (9), t (3)
 };
 
-__global__ void k_p2d_colcount(const int32_t* __restrict__ label, int H, int W, int C, int32_t* colcnt) {
-  const int x = blockIdx.x * blockDim.x + threadIdx.x;
+// one thread per column, its class counts in LDS (a global read-modify-write
+// per pixel would put a memory latency on every step of the column walk)
+__global__ void __launch_bounds__(64) k_p2d_colcount(const int32_t* __restrict__ label, int H, int W, int C,
+                                                     int32_t* colcnt) {
+  extern __shared__ int cc[];  // [C][64]
+  const int x = blockIdx.x * 64 + threadIdx.x;
+  for (int c = 0; c < C; c++) cc[c * 64 + threadIdx.x] = 0;
   if (x >= W) return;
   for (int y = 0; y < H; y++) {
     const int c = label[y * W + x];
-    if (c >= 0 && c < C) colcnt[c * W + x]++;  // one thread per column: no contention
+    if (c >= 0 && c < C) cc[c * 64 + threadIdx.x]++;
   }
+  for (int c = 0; c < C; c++) colcnt[c * W + x] = cc[c * 64 + threadIdx.x];
 }
 
 __global__ void __launch_bounds__(1024) k_p2d_scan(const int32_t* __restrict__ colcnt, int W, int32_t* coloff,
@@ -563,11 +577,11 @@ extern "C" int pcnn_pose2d(const int32_t* label, const float* vertmap, const flo
   ws.hyp = (double*)(base + l.hyp);
   ws.sub = (int32_t*)(base + l.sub);
   hipStream_t st = (hipStream_t)stream;
-  if (hipMemsetAsync(ws.colcnt, 0, (size_t)C * W * sizeof(int32_t), st) != hipSuccess) return PCNN_EHIP;
   if (hipMemsetAsync(poses_out, 0, (size_t)12 * C * sizeof(float), st) != hipSuccess) return PCNN_EHIP;
   if (hipMemsetAsync(inl_out, 0xFF, (size_t)n_hyp * kRounds * sizeof(int32_t), st) != hipSuccess) return PCNN_EHIP;
   if (hipMemsetAsync(final_out, 0xFF, (size_t)C * 3 * sizeof(int32_t), st) != hipSuccess) return PCNN_EHIP;
-  hipLaunchKernelGGL(k_p2d_colcount, dim3((W + 255) / 256), dim3(256), 0, st, label, H, W, C, ws.colcnt);
+  hipLaunchKernelGGL(k_p2d_colcount, dim3((W + 63) / 64), dim3(64), C * 64 * sizeof(int), st, label, H, W, C,
+                     ws.colcnt);
   hipLaunchKernelGGL(k_p2d_scan, dim3(C), dim3(1024), 0, st, ws.colcnt, W, ws.coloff, ws.count);
   PCNN_CHECK_LAUNCH();
   // the class sizes decide object_ids (> minArea = 400, :1027) and the
