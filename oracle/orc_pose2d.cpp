@@ -15,8 +15,10 @@
 //   std::negative_binomial_distribution<int>(1, maxPixels / N) pixel skips),
 //   getWorkingQueue (:1150-1160), and the output layout (:1729-1764).
 // Deliberate, documented choices (parity unpinned: OpenCV, NLopt absent):
-//   * RNG: hypothesis h draws from its own Philox4x32-10 stream (key = seed,
-//     counter = (draw, h, 'P2D', 0)), uniform ints by rejection; the
+//   * RNG: attempt a of hypothesis h draws from its own Philox4x32-10 stream
+//     (key = seed, counter = (draw, h, 'P2D', a)), uniform ints by rejection;
+//     h keeps its first accepted attempt (independent attempts: the GPU
+//     evaluates a batch of them at once); the
 //     reference's per-thread mt19937 streams (thread_rand.cpp) are assigned
 //     to hypotheses by the OpenMP schedule, i.e. nondeterministically.
 //   * Hypotheses are stored in ascending h (the reference appends in
@@ -24,7 +26,8 @@
 //     (inliers descending, then h): one legal order of std::sort's ties.
 //   * cv::solvePnP(CV_P3P) is restated as Grunert's P3P (distance ratios
 //     u = s2/s1, v = s3/s1; the quartic in v from eliminating u, its roots by
-//     Durand-Kerner iteration polished by Newton steps), the camera-frame
+//     Durand-Kerner sweeps until the steps fall below 1e-13, polished by
+//     Newton steps), the camera-frame
 //     triangle aligned to the model triangle by orthonormal triads, and the
 //     solution whose reprojection of the 4th point is closest kept -- as
 //     OpenCV's p3p.cpp selects it.
@@ -62,13 +65,14 @@ U4 philox(U4 c, uint32_t k0, uint32_t k1) {
 }
 
 struct Stream {
-  uint32_t k0, k1, h, ctr = 0;
+  uint32_t k0, k1, h, a, ctr = 0;
   int word = 4;
   U4 buf;
-  Stream(uint64_t seed, uint32_t hyp) : k0((uint32_t)seed), k1((uint32_t)(seed >> 32)), h(hyp) {}
+  Stream(uint64_t seed, uint32_t hyp, uint32_t attempt)
+      : k0((uint32_t)seed), k1((uint32_t)(seed >> 32)), h(hyp), a(attempt) {}
   uint32_t next() {
     if (word == 4) {
-      buf = philox(U4{{ctr++, h, 0x50324400u, 0u}}, k0, k1);
+      buf = philox(U4{{ctr++, h, 0x50324400u, a}}, k0, k1);
       word = 0;
     }
     return buf.v[word++];
@@ -305,8 +309,8 @@ ORC_API int orc_pose2d(const int* label, const float* vertmap, const float* exte
   if (objs.empty()) return 0;
   std::vector<std::vector<Hyp>> hypmap(C);
   for (int h = 0; h < n_hyp; h++) {
-    Stream rs(seed, (uint32_t)h);
     for (int it = 0; it < max_iter; it++) {
+      Stream rs(seed, (uint32_t)h, (uint32_t)it);  // attempt it of hypothesis h draws from its own stream
       const int obj = objs[rs.uniform((int)objs.size())];
       const auto& L = labels[obj];
       float m[4][2];

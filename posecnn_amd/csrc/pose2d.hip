@@ -17,9 +17,12 @@
 //       std::negative_binomial_distribution<int>(1, maxPixels / N) per round,
 //       :1183-1213 -- identical for every hypothesis of the round) and copied
 //       up once;
-//   k_p2d_hyps: one lane per hypothesis runs the rejection-sampling loop
-//       (samplePoint2D x 4, degeneracy tests, Grunert P3P in double, the
-//       reprojection and getBB2D area checks) on its own Philox stream;
+//   k_p2d_attempts / k_p2d_pick: the rejection-sampling loop (samplePoint2D
+//       x 4, degeneracy tests, Grunert P3P in double, the reprojection and
+//       getBB2D area checks) as independent attempts, each on its own Philox
+//       stream: the first 32 attempts of every hypothesis run at once (one
+//       lane each), then one lane per hypothesis keeps its first accepted
+//       attempt (further attempts one by one if none of the 32 was);
 //   k_p2d_ransac: one workgroup per object runs the 8 rounds: its waves count
 //       inliers of the surviving hypotheses over the round's subset (double
 //       projections, one hypothesis per wave at a time), a stable rank sort
@@ -40,6 +43,8 @@ namespace {
 constexpr int kRounds = 8;       // <= 256 hypotheses halve to one in <= 8 rounds; refIt = 8 (:1601)
 constexpr int kRansacThreads = 256;
 constexpr int kMaxHypBlock = 1024;
+constexpr int kAttempts = 32;  // sampling attempts per hypothesis evaluated in one launch
+constexpr int kAttRec = 17;    // attempt record: obj (-1 rejected), R (9), t (3), pixels (4)
 
 struct U4 { uint32_t x, y, z, w; };
 
@@ -54,16 +59,16 @@ __device__ __forceinline__ U4 philox(U4 c, uint32_t k0, uint32_t k1) {
   return c;
 }
 
-// hypothesis h's draws: Philox4x32-10 block (draw / 4, h, 'P2D', 0), words in order
+// attempt a of hypothesis h draws Philox4x32-10 blocks (draw / 4, h, 'P2D', a), words in order
 struct Stream {
-  uint32_t k0, k1, h, ctr;
+  uint32_t k0, k1, h, a, ctr;
   int word;
   U4 buf;
-  __device__ Stream(uint64_t seed, uint32_t hyp) : k0((uint32_t)seed), k1((uint32_t)(seed >> 32)), h(hyp), ctr(0),
-                                                   word(4), buf{0, 0, 0, 0} {}
+  __device__ Stream(uint64_t seed, uint32_t hyp, uint32_t attempt)
+      : k0((uint32_t)seed), k1((uint32_t)(seed >> 32)), h(hyp), a(attempt), ctr(0), word(4), buf{0, 0, 0, 0} {}
   __device__ uint32_t next() {
     if (word == 4) {
-      buf = philox(U4{ctr++, h, 0x50324400u, 0u}, k0, k1);
+      buf = philox(U4{ctr++, h, 0x50324400u, a}, k0, k1);
       word = 0;
     }
     const uint32_t v = word == 0 ? buf.x : word == 1 ? buf.y : word == 2 ? buf.z : buf.w;
@@ -313,6 +318,7 @@ struct P2dWs {
   int32_t* sub;      // subsets: indices into the class list, rounds concatenated per object
   int32_t* suboff;   // (n_obj, kRounds + 1)
   double* hyp;       // (n_hyp, 16): obj, R (9), t (3)
+  double* att;       // (n_hyp, kAttempts, kAttRec) attempt records
 };
 
 // one thread per column, its class counts in LDS (a global read-modify-write
@@ -366,10 +372,86 @@ __global__ void __launch_bounds__(64) k_p2d_scatter(const int32_t* __restrict__ 
   }
 }
 
-// One lane per hypothesis: the sampling loop of :1616-1688
-__global__ void __launch_bounds__(64) k_p2d_hyps(const float* __restrict__ vm, const float* __restrict__ ext, int H,
+// One sampling attempt of :1616-1688 (samplePoint2D x 4, the degeneracy
+// tests, P3P, the 10 px reprojection and getBB2D area checks) on attempt a's
+// own stream; true with the hypothesis when it is accepted.
+__device__ bool p2d_attempt(const float* __restrict__ vm, const float* __restrict__ ext, int H, int W, int C,
+                            const Cam& k, uint64_t seed, int h, int a, int n_obj, const P2dWs& ws, int& obj_out,
+                            int* px_out, Pose& P) {
+  Stream rs(seed, (uint32_t)h, (uint32_t)a);
+  const int obj = ws.objs[rs.uniform(n_obj)];
+  const int* L = ws.lists + ws.listoff[obj];
+  const int N = ws.count[obj];
+  float m[4][2];
+  F3 X[4];
+  int px4[4], n = 0;
+  for (int s = 0; s < 4; s++) {  // samplePoint2D (:1084-1104)
+    const int idx = L[rs.uniform(N)];
+    const float u = (float)(idx % W), v = (float)(idx / W);
+    double md = -1;
+    for (int q = 0; q < n; q++) {
+      const float dx = m[q][0] - u, dy = m[q][1] - v;
+      const double d = sqrt((double)dx * dx + (double)dy * dy);
+      md = md < 0 ? d : fmin(md, d);
+    }
+    if (md > 0 && md < 10) return false;
+    const F3 o = mode3d(vm, ext, C, obj, idx);
+    if (o.x == 0 && o.y == 0 && o.z == 0) return false;
+    md = -1;
+    for (int q = 0; q < n; q++) {
+      const double d = norm3f(X[q], o);
+      md = md < 0 ? d : fmin(md, d);
+    }
+    if (md > 0 && md < 0.01) return false;
+    m[n][0] = u;
+    m[n][1] = v;
+    X[n] = o;
+    px4[n] = idx;
+    n++;
+  }
+  if (point_line(X[0], X[1], X[2]) < 0.01 || point_line(X[0], X[1], X[3]) < 0.01 ||
+      point_line(X[0], X[2], X[3]) < 0.01 || point_line(X[1], X[2], X[3]) < 0.01)
+    return false;
+  if (!p3p(X, m, k, P)) return false;
+  for (int q = 0; q < 4; q++) {  // the 4 samples must reproject within 10 px (:1664-1672)
+    double u, v;
+    project(P, D3{X[q].x, X[q].y, X[q].z}, k, u, v);
+    const float du = m[q][0] - (float)u, dv = m[q][1] - (float)v;
+    if (!(sqrt((double)du * du + (double)dv * dv) < 10)) return false;
+  }
+  if ((float)bb_area(P, ext, obj, k, W, H) < 400.0f) return false;  // :1678-1680
+  obj_out = obj;
+  for (int i = 0; i < 4; i++) px_out[i] = px4[i];
+  return true;
+}
+
+// The first kAttempts attempts of every hypothesis at once, one lane each:
+// the reference's loop runs attempts until one is accepted, and attempts are
+// independent (each its own stream), so they need not wait for each other.
+__global__ void __launch_bounds__(64) k_p2d_attempts(const float* __restrict__ vm, const float* __restrict__ ext,
+                                                     int H, int W, int C, Cam k, uint64_t seed, int n_hyp,
+                                                     int n_obj, int T, P2dWs ws) {
+  const int id = blockIdx.x * blockDim.x + threadIdx.x;
+  if (id >= n_hyp * T) return;
+  const int h = id % n_hyp, a = id / n_hyp;
+  double* rec = ws.att + (size_t)(h * T + a) * kAttRec;
+  int obj, px4[4];
+  Pose P;
+  if (!p2d_attempt(vm, ext, H, W, C, k, seed, h, a, n_obj, ws, obj, px4, P)) {
+    rec[0] = -1;
+    return;
+  }
+  rec[0] = obj;
+  for (int i = 0; i < 9; i++) rec[1 + i] = P.R[i];
+  for (int i = 0; i < 3; i++) rec[10 + i] = P.t[i];
+  for (int i = 0; i < 4; i++) rec[13 + i] = px4[i];
+}
+
+// One lane per hypothesis: its first accepted attempt (the batch above, then
+// -- rarely -- further attempts one by one), written out as :1682-1686 stores it.
+__global__ void __launch_bounds__(64) k_p2d_pick(const float* __restrict__ vm, const float* __restrict__ ext, int H,
                                                  int W, int C, Cam k, uint64_t seed, int n_hyp, int n_obj,
-                                                 int max_iter, P2dWs ws, float* __restrict__ hyps_out,
+                                                 int max_iter, int T, P2dWs ws, float* __restrict__ hyps_out,
                                                  int32_t* __restrict__ hyp_px) {
   const int h = blockIdx.x * blockDim.x + threadIdx.x;
   if (h >= n_hyp) return;
@@ -378,63 +460,27 @@ __global__ void __launch_bounds__(64) k_p2d_hyps(const float* __restrict__ vm, c
   hyps_out[(size_t)h * 13] = -1.f;
   for (int i = 1; i < 13; i++) hyps_out[(size_t)h * 13 + i] = 0.f;
   for (int i = 0; i < 4; i++) hyp_px[h * 4 + i] = -1;
-  Stream rs(seed, (uint32_t)h);
-  for (int it = 0; it < max_iter; it++) {
-    const int obj = ws.objs[rs.uniform(n_obj)];
-    const int* L = ws.lists + ws.listoff[obj];
-    const int N = ws.count[obj];
-    float m[4][2];
-    F3 X[4];
-    int px4[4], n = 0;
-    bool ok = true;
-    for (int s = 0; s < 4 && ok; s++) {  // samplePoint2D (:1084-1104)
-      const int idx = L[rs.uniform(N)];
-      const float u = (float)(idx % W), v = (float)(idx / W);
-      double md = -1;
-      for (int q = 0; q < n; q++) {
-        const float dx = m[q][0] - u, dy = m[q][1] - v;
-        const double d = sqrt((double)dx * dx + (double)dy * dy);
-        md = md < 0 ? d : fmin(md, d);
-      }
-      if (md > 0 && md < 10) { ok = false; break; }
-      const F3 o = mode3d(vm, ext, C, obj, idx);
-      if (o.x == 0 && o.y == 0 && o.z == 0) { ok = false; break; }
-      md = -1;
-      for (int q = 0; q < n; q++) {
-        const double d = norm3f(X[q], o);
-        md = md < 0 ? d : fmin(md, d);
-      }
-      if (md > 0 && md < 0.01) { ok = false; break; }
-      m[n][0] = u;
-      m[n][1] = v;
-      X[n] = o;
-      px4[n] = idx;
-      n++;
-    }
-    if (!ok) continue;
-    if (point_line(X[0], X[1], X[2]) < 0.01 || point_line(X[0], X[1], X[3]) < 0.01 ||
-        point_line(X[0], X[2], X[3]) < 0.01 || point_line(X[1], X[2], X[3]) < 0.01)
-      continue;
-    Pose P;
-    if (!p3p(X, m, k, P)) continue;
-    bool out = false;
-    for (int q = 0; q < 4 && !out; q++) {  // the 4 samples must reproject within 10 px (:1664-1672)
-      double u, v;
-      project(P, D3{X[q].x, X[q].y, X[q].z}, k, u, v);
-      const float du = m[q][0] - (float)u, dv = m[q][1] - (float)v;
-      if (!(sqrt((double)du * du + (double)dv * dv) < 10)) out = true;
-    }
-    if (out) continue;
-    if ((float)bb_area(P, ext, obj, k, W, H) < 400.0f) continue;  // :1678-1680
-    hr[0] = obj;
-    for (int i = 0; i < 9; i++) hr[1 + i] = P.R[i];
-    for (int i = 0; i < 3; i++) hr[10 + i] = P.t[i];
-    hyps_out[(size_t)h * 13] = (float)obj;
-    for (int i = 0; i < 9; i++) hyps_out[(size_t)h * 13 + 1 + i] = (float)P.R[i];
-    for (int i = 0; i < 3; i++) hyps_out[(size_t)h * 13 + 10 + i] = (float)P.t[i];
-    for (int i = 0; i < 4; i++) hyp_px[h * 4 + i] = px4[i];
-    return;
+  if (n_obj == 0) return;
+  int obj = -1, px4[4];
+  Pose P;
+  for (int a = 0; a < T && obj < 0; a++) {
+    const double* rec = ws.att + (size_t)(h * T + a) * kAttRec;
+    if (rec[0] < 0) continue;
+    obj = (int)rec[0];
+    for (int i = 0; i < 9; i++) P.R[i] = rec[1 + i];
+    for (int i = 0; i < 3; i++) P.t[i] = rec[10 + i];
+    for (int i = 0; i < 4; i++) px4[i] = (int)rec[13 + i];
   }
+  for (int a = T; a < max_iter && obj < 0; a++)
+    if (!p2d_attempt(vm, ext, H, W, C, k, seed, h, a, n_obj, ws, obj, px4, P)) obj = -1;
+  if (obj < 0) return;
+  hr[0] = obj;
+  for (int i = 0; i < 9; i++) hr[1 + i] = P.R[i];
+  for (int i = 0; i < 3; i++) hr[10 + i] = P.t[i];
+  hyps_out[(size_t)h * 13] = (float)obj;
+  for (int i = 0; i < 9; i++) hyps_out[(size_t)h * 13 + 1 + i] = (float)P.R[i];
+  for (int i = 0; i < 3; i++) hyps_out[(size_t)h * 13 + 10 + i] = (float)P.t[i];
+  for (int i = 0; i < 4; i++) hyp_px[h * 4 + i] = px4[i];
 }
 
 // One workgroup per object: the preemptive rounds of :1693-1727 and the output of :1729-1764
@@ -522,7 +568,7 @@ __global__ void __launch_bounds__(kRansacThreads) k_p2d_ransac(const float* __re
 }
 
 struct Layout {
-  size_t colcnt, coloff, count, lists, listoff, objs, suboff, hyp, sub, total;
+  size_t colcnt, coloff, count, lists, listoff, objs, suboff, hyp, att, sub, total;
 };
 
 Layout layout(int H, int W, int C, int n_hyp) {
@@ -543,6 +589,7 @@ Layout layout(int H, int W, int C, int n_hyp) {
   l.objs = take((size_t)C * sizeof(int32_t));
   l.suboff = take((size_t)C * (kRounds + 1) * sizeof(int32_t));
   l.hyp = take((size_t)n_hyp * 16 * sizeof(double));
+  l.att = take((size_t)n_hyp * kAttempts * kAttRec * sizeof(double));
   // subsets: a round visits at most every pixel of the class once
   l.sub = take((size_t)kRounds * H * W * sizeof(int32_t));
   l.total = off + 256;
@@ -575,6 +622,7 @@ extern "C" int pcnn_pose2d(const int32_t* label, const float* vertmap, const flo
   ws.objs = (int32_t*)(base + l.objs);
   ws.suboff = (int32_t*)(base + l.suboff);
   ws.hyp = (double*)(base + l.hyp);
+  ws.att = (double*)(base + l.att);
   ws.sub = (int32_t*)(base + l.sub);
   hipStream_t st = (hipStream_t)stream;
   if (hipMemsetAsync(poses_out, 0, (size_t)12 * C * sizeof(float), st) != hipSuccess) return PCNN_EHIP;
@@ -599,8 +647,8 @@ extern "C" int pcnn_pose2d(const int32_t* label, const float* vertmap, const flo
   }
   const int n_obj = (int)objs.size();
   if (n_obj == 0) {  // no object: hypotheses stay empty (:1586-1587)
-    hipLaunchKernelGGL(k_p2d_hyps, dim3((n_hyp + 63) / 64), dim3(64), 0, st, vertmap, extents, H, W, C,
-                       Cam{fx, fy, px, py}, seed, n_hyp, 0, 0, ws, hyps_out, hyp_px);
+    hipLaunchKernelGGL(k_p2d_pick, dim3((n_hyp + 63) / 64), dim3(64), 0, st, vertmap, extents, H, W, C,
+                       Cam{fx, fy, px, py}, seed, n_hyp, 0, 0, 0, ws, hyps_out, hyp_px);
     PCNN_CHECK_LAUNCH();
     return PCNN_OK;
   }
@@ -632,8 +680,11 @@ extern "C" int pcnn_pose2d(const int32_t* label, const float* vertmap, const flo
     return PCNN_EHIP;
   const Cam k{fx, fy, px, py};
   hipLaunchKernelGGL(k_p2d_scatter, dim3((W + 63) / 64), dim3(64), C * 64 * sizeof(int), st, label, H, W, C, ws);
-  hipLaunchKernelGGL(k_p2d_hyps, dim3((n_hyp + 63) / 64), dim3(64), 0, st, vertmap, extents, H, W, C, k, seed, n_hyp,
-                     n_obj, max_iter, ws, hyps_out, hyp_px);
+  const int T = max_iter < kAttempts ? max_iter : kAttempts;
+  hipLaunchKernelGGL(k_p2d_attempts, dim3((n_hyp * T + 63) / 64), dim3(64), 0, st, vertmap, extents, H, W, C, k, seed,
+                     n_hyp, n_obj, T, ws);
+  hipLaunchKernelGGL(k_p2d_pick, dim3((n_hyp + 63) / 64), dim3(64), 0, st, vertmap, extents, H, W, C, k, seed, n_hyp,
+                     n_obj, max_iter, T, ws, hyps_out, hyp_px);
   hipLaunchKernelGGL(k_p2d_ransac, dim3(n_obj), dim3(kRansacThreads), 0, st, vertmap, extents, W, C, k, n_hyp, ws,
                      inl_out, final_out, poses_out);
   PCNN_CHECK_LAUNCH();
