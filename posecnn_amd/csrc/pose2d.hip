@@ -36,6 +36,7 @@
 #include <climits>
 #include <algorithm>
 #include <random>
+#include <thread>
 #include <vector>
 
 namespace {
@@ -652,39 +653,65 @@ extern "C" int pcnn_pose2d(const int32_t* label, const float* vertmap, const flo
     PCNN_CHECK_LAUNCH();
     return PCNN_OK;
   }
-  // countInliers2D's pixel subsets of the 8 rounds (the same for every
-  // hypothesis of a round: a fresh default-seeded std::mt19937 per call)
-  std::vector<int32_t> sub, suboff;
-  for (int oi = 0; oi < n_obj; oi++) {
-    const int N = cnt[objs[oi]];
-    for (int r = 1; r <= kRounds; r++) {
-      suboff.push_back((int32_t)sub.size());
-      const int maxPixels = 1000 * r;
-      const float rate = maxPixels / (float)N;
-      std::mt19937 gen;
-      std::negative_binomial_distribution<int> nb(1, rate < 1 ? rate : 0.5f);
-      for (int i = 0; i < N;) {
-        sub.push_back(i);
-        if (rate < 1) i += std::max(1, nb(gen));
-        else i++;
-      }
-    }
-    suboff.push_back((int32_t)sub.size());
-  }
-  if (sub.size() > (size_t)kRounds * H * W) return PCNN_ECAPACITY;
   if (hipMemcpyAsync(ws.listoff, listoff.data(), C * sizeof(int32_t), hipMemcpyHostToDevice, st) != hipSuccess ||
-      hipMemcpyAsync(ws.objs, objs.data(), n_obj * sizeof(int32_t), hipMemcpyHostToDevice, st) != hipSuccess ||
-      hipMemcpyAsync(ws.suboff, suboff.data(), suboff.size() * sizeof(int32_t), hipMemcpyHostToDevice, st) !=
-          hipSuccess ||
-      hipMemcpyAsync(ws.sub, sub.data(), sub.size() * sizeof(int32_t), hipMemcpyHostToDevice, st) != hipSuccess)
+      hipMemcpyAsync(ws.objs, objs.data(), n_obj * sizeof(int32_t), hipMemcpyHostToDevice, st) != hipSuccess)
     return PCNN_EHIP;
   const Cam k{fx, fy, px, py};
+  // the class lists and the hypotheses run on the GPU while the host draws
+  // the rounds' pixel subsets below
   hipLaunchKernelGGL(k_p2d_scatter, dim3((W + 63) / 64), dim3(64), C * 64 * sizeof(int), st, label, H, W, C, ws);
   const int T = max_iter < kAttempts ? max_iter : kAttempts;
   hipLaunchKernelGGL(k_p2d_attempts, dim3((n_hyp * T + 63) / 64), dim3(64), 0, st, vertmap, extents, H, W, C, k, seed,
                      n_hyp, n_obj, T, ws);
   hipLaunchKernelGGL(k_p2d_pick, dim3((n_hyp + 63) / 64), dim3(64), 0, st, vertmap, extents, H, W, C, k, seed, n_hyp,
                      n_obj, max_iter, T, ws, hyps_out, hyp_px);
+  PCNN_CHECK_LAUNCH();
+  // countInliers2D's pixel subsets of the 8 rounds (the same for every
+  // hypothesis of a round: a fresh default-seeded std::mt19937 per call,
+  // :1183-1213), one (object, round) per task: std::negative_binomial_
+  // distribution draws (a gamma and a Poisson variate each) are the costly
+  // part, so the 8 n_obj independent streams run on host threads
+  const int n_task = n_obj * kRounds;
+  std::vector<std::vector<int32_t>> part(n_task);
+  auto draw = [&](int t) {
+    const int N = cnt[objs[t / kRounds]];
+    const int r = t % kRounds + 1;
+    const int maxPixels = 1000 * r;
+    const float rate = maxPixels / (float)N;
+    std::mt19937 gen;
+    std::negative_binomial_distribution<int> nb(1, rate < 1 ? rate : 0.5f);
+    std::vector<int32_t>& out = part[t];
+    for (int i = 0; i < N;) {
+      out.push_back(i);
+      if (rate < 1) i += std::max(1, nb(gen));
+      else i++;
+    }
+  };
+  {
+    const unsigned hw = std::thread::hardware_concurrency();
+    const int nthr = std::max(1, std::min(n_task, (int)std::min(hw ? hw : 1u, 16u)));
+    std::vector<std::thread> pool;
+    for (int w = 1; w < nthr; w++)
+      pool.emplace_back([&, w] {
+        for (int t = w; t < n_task; t += nthr) draw(t);
+      });
+    for (int t = 0; t < n_task; t += nthr) draw(t);
+    for (auto& th : pool) th.join();
+  }
+  std::vector<int32_t> sub, suboff;
+  for (int oi = 0; oi < n_obj; oi++) {
+    for (int r = 0; r < kRounds; r++) {
+      suboff.push_back((int32_t)sub.size());
+      const auto& v = part[oi * kRounds + r];
+      sub.insert(sub.end(), v.begin(), v.end());
+    }
+    suboff.push_back((int32_t)sub.size());
+  }
+  if (sub.size() > (size_t)kRounds * H * W) return PCNN_ECAPACITY;
+  if (hipMemcpyAsync(ws.suboff, suboff.data(), suboff.size() * sizeof(int32_t), hipMemcpyHostToDevice, st) !=
+          hipSuccess ||
+      hipMemcpyAsync(ws.sub, sub.data(), sub.size() * sizeof(int32_t), hipMemcpyHostToDevice, st) != hipSuccess)
+    return PCNN_EHIP;
   hipLaunchKernelGGL(k_p2d_ransac, dim3(n_obj), dim3(kRansacThreads), 0, st, vertmap, extents, W, C, k, n_hyp, ws,
                      inl_out, final_out, poses_out);
   PCNN_CHECK_LAUNCH();
