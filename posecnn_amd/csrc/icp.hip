@@ -731,15 +731,16 @@ __global__ void __launch_bounds__(kBlk) k_score_scatter(const float* __restrict_
 
 // Nearest depth point within the radius through a uniform grid (advisor
 // finding: the brute-force M x M scan grows with the square of the object's
-// pixel count).  Cells of edge s = 1.001 r: a point closer than r to q differs
-// from it by < 0.999 cells per axis (cell coordinates from double products,
-// whose rounding is far below the margin for any |coordinate| < 10^7 m), so
-// it lies in one of the 27 cells around q's.  Cells hash into kGridBuckets
-// buckets (counting sort of the depth-point indices); every point of every
-// bucket visited is tested with the brute force's exact arithmetic, so the
-// result -- the smallest squared distance < r^2, ties to the lowest index --
-// is the same (a hash collision only adds candidates; a bucket visited twice
-// changes nothing).
+// pixel count).  Cells of edge s = 0.5005 r: a point closer than r to q
+// differs from it by < 1.998 cells per axis (cell coordinates from double
+// products, whose rounding is far below the margin for any |coordinate| <
+// 10^7 m), so it lies within 2 cells of q's.  Cells hash into kGridBuckets
+// buckets (counting sort of the depth-point indices); the query visits rings
+// of cells outward and stops when the next ring cannot hold a point as close
+// as its best.  Every point of every bucket visited is tested with the brute
+// force's exact arithmetic, so the result -- the smallest squared distance
+// < r^2, ties to the lowest index -- is the same (a hash collision only adds
+// candidates; a bucket visited twice changes nothing).
 constexpr int kGridBuckets = 1 << 17;
 
 __device__ __forceinline__ bool grid_cell(float x, float y, float z, double inv_s, int& cx, int& cy, int& cz) {
@@ -844,55 +845,65 @@ __global__ void __launch_bounds__(kBlk) k_score_nn(const float4* __restrict__ mo
   if (!grid_cell(x, y, z, inv_s, cx, cy, cz)) return;
   float best = r2;  // strict: only squared distances < r2 qualify
   int bi = -1;
-  for (int dz = -1; dz <= 1; dz++)
-    for (int dy = -1; dy <= 1; dy++)
-      for (int dx = -1; dx <= 1; dx++) {
-        const int b = grid_bucket(cx + dx, cy + dy, cz + dz);
-        const int e = start[b + 1];
-        for (int k = start[b]; k < e; k++) {
-          const int i = idx[k];
-          const float4 d = dpts[i];
-          const float ex = x - d.x, ey = y - d.y, ez = z - d.z;
-          const float d2 = ex * ex + ey * ey + ez * ez;
-          if (d2 < best || (bi >= 0 && d2 == best && i < bi)) {  // the first minimum in index order
-            best = d2;
-            bi = i;
+  // rings of cells by Chebyshev distance d = 0, 1, 2 around q's cell (cells
+  // of edge s = 0.5005 r: every point within r is at most 2 cells away).  A
+  // point in ring d >= 1 is farther than (d - 1) s from q, so ring d is
+  // skipped once that bound (with a 1e-6 margin for the fp32 distances)
+  // exceeds the best squared distance so far: no point there can equal or
+  // beat it.
+  const double s_cell = 1.0 / inv_s;
+  for (int d = 0; d <= 2; d++) {
+    if (d >= 2 && (double)(d - 1) * s_cell * (d - 1) * s_cell * (1.0 - 1e-6) > (double)best) break;
+    for (int dz = -d; dz <= d; dz++)
+      for (int dy = -d; dy <= d; dy++)
+        for (int dx = -d; dx <= d; dx++) {
+          if (max(abs(dx), max(abs(dy), abs(dz))) != d) continue;
+          const int b = grid_bucket(cx + dx, cy + dy, cz + dz);
+          const int e = start[b + 1];
+          for (int k = start[b]; k < e; k++) {
+            const int i = idx[k];
+            const float4 p = dpts[i];
+            const float ex = x - p.x, ey = y - p.y, ez = z - p.z;
+            const float d2 = ex * ex + ey * ey + ez * ez;
+            if (d2 < best || (bi >= 0 && d2 == best && i < bi)) {  // the first minimum in index order
+              best = d2;
+              bi = i;
+            }
           }
         }
-      }
+  }
   if (bi >= 0) flags[(size_t)h * cap + bi] = 1;
 }
 
-// score per hypothesis and the first best one (one workgroup)
-__global__ void __launch_bounds__(kBlk) k_score_select(const uint8_t* __restrict__ flags, const int32_t* __restrict__ cnt,
-                                                       int nseg, int J, int cap, float* __restrict__ score,
-                                                       int32_t* __restrict__ choose) {
-  __shared__ int ish[kBlk / 64];
-  __shared__ float sc[64];
+// score per hypothesis: one workgroup per hypothesis counts its flags
+__global__ void __launch_bounds__(1024) k_score_count_flags(const uint8_t* __restrict__ flags,
+                                                            const int32_t* __restrict__ cnt, int nseg, int cap,
+                                                            float* __restrict__ score) {
+  __shared__ int ish[1024 / 64];
   int c = 0;
-  for (int s = threadIdx.x; s < nseg; s += kBlk) c += cnt[s];
-  const int M = block_sum_int<kBlk>(c, ish);
-  for (int h = 0; h < J; h++) {
-    int f = 0;
-    for (int i = threadIdx.x; i < M; i += kBlk) f += flags[(size_t)h * cap + i];
-    f = block_sum_int<kBlk>(f, ish);
-    if (threadIdx.x == 0) {
-      const float v = M > 0 ? (float)f / (float)M : 0.f;
-      score[h] = v;
-      if (h < 64) sc[h] = v;
+  for (int s = threadIdx.x; s < nseg; s += 1024) c += cnt[s];
+  const int M = block_sum_int<1024>(c, ish);
+  const int h = blockIdx.x;
+  int f = 0;
+  for (int i = threadIdx.x; i < M; i += 1024) f += flags[(size_t)h * cap + i];
+  f = block_sum_int<1024>(f, ish);
+  if (threadIdx.x == 0) score[h] = M > 0 ? (float)f / (float)M : 0.f;
+}
+
+// the first best hypothesis (one lane)
+__global__ void k_score_choose(const float* __restrict__ score, const int32_t* __restrict__ cnt, int nseg, int J,
+                               int32_t* __restrict__ choose) {
+  if (threadIdx.x != 0) return;
+  int M = 0;
+  for (int s = 0; s < nseg; s++) M += cnt[s];
+  float mx = -3.402823466e38f;
+  int ch = -1;
+  for (int h = 0; h < J; h++)
+    if (score[h] > mx) {
+      mx = score[h];
+      ch = h;
     }
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    float mx = -3.402823466e38f;
-    int ch = -1;
-    for (int h = 0; h < J && h < 64; h++)
-      if (sc[h] > mx) {
-        mx = sc[h];
-        ch = h;
-      }
-    *choose = M > 0 ? ch : 0;  // no depth point: hyps[0] (synthesize.cpp:2333-2334)
-  }
+  *choose = M > 0 ? ch : 0;  // no depth point: hyps[0] (synthesize.cpp:2333-2334)
 }
 
 struct IcpWs {
@@ -1084,7 +1095,7 @@ extern "C" int pcnn_icp_score(const float* live, const int32_t* label, int obj, 
   hipStream_t st = (hipStream_t)stream;
   if (hipMemsetAsync(flags, 0, (size_t)J * HW, st) != hipSuccess) return PCNN_EHIP;
   if (hipMemsetAsync(bcount, 0, (size_t)kGridBuckets * sizeof(int32_t), st) != hipSuccess) return PCNN_EHIP;
-  const double inv_s = 1.0 / ((double)radius * 1.001);
+  const double inv_s = 1.0 / ((double)radius * 0.5005);
   const unsigned qblocks = (unsigned)((HW + kBlk - 1) / kBlk);
   hipLaunchKernelGGL(k_score_count, dim3(nseg), dim3(kBlk), 0, st, live, label, obj, vertmap, HW, nseg, cnt);
   hipLaunchKernelGGL(k_score_scatter, dim3(nseg), dim3(kBlk), 0, st, live, label, obj, vertmap, HW, nseg, cnt, model,
@@ -1094,7 +1105,8 @@ extern "C" int pcnn_icp_score(const float* live, const int32_t* label, int obj, 
   hipLaunchKernelGGL(k_grid_fill, dim3(qblocks), dim3(kBlk), 0, st, cnt, nseg, bucket_of, cursor, idx);
   hipLaunchKernelGGL(k_score_nn, dim3(qblocks, J), dim3(kBlk), 0, st, model, dpts, cnt, nseg, hyps, radius * radius,
                      inv_s, bstart, idx, flags, HW);
-  hipLaunchKernelGGL(k_score_select, dim3(1), dim3(kBlk), 0, st, flags, cnt, nseg, J, HW, score, choose);
+  hipLaunchKernelGGL(k_score_count_flags, dim3(J), dim3(1024), 0, st, flags, cnt, nseg, HW, score);
+  hipLaunchKernelGGL(k_score_choose, dim3(1), dim3(64), 0, st, score, cnt, nseg, J, choose);
   PCNN_CHECK_LAUNCH();
   return PCNN_OK;
 }
