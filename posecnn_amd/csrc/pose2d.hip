@@ -23,11 +23,12 @@
 //       stream: the first 32 attempts of every hypothesis run at once (one
 //       lane each), then one lane per hypothesis keeps its first accepted
 //       attempt (further attempts one by one if none of the 32 was);
-//   k_p2d_ransac: one workgroup per object runs the 8 rounds: its waves count
-//       inliers of the surviving hypotheses over the round's subset (double
-//       projections, one hypothesis per wave at a time), a stable rank sort
-//       keeps the better half, and the survivor's pose is written in the
-//       reference's (3, 4, C) layout.
+//   k_p2d_collect / k_p2d_count / k_p2d_select / k_p2d_finish: the 8 rounds
+//       as launches: per round one workgroup per (surviving hypothesis,
+//       object) counts inliers over the round's subset (double projections),
+//       then one workgroup per object keeps the better half by a stable rank
+//       sort; the survivor's pose is written in the reference's (3, 4, C)
+//       layout.
 // The reference's refinement steps are inert in this path (updateHyp3D on an
 // empty 3-D inlier list, optEnergy2D divided by that list's size: NLopt keeps
 // the start point) and are not run; the oracle (oracle/orc_pose2d.cpp)
@@ -35,6 +36,7 @@
 #include "pcnn_common.h"
 #include <climits>
 #include <algorithm>
+#include <atomic>
 #include <random>
 #include <thread>
 #include <vector>
@@ -42,7 +44,6 @@
 namespace {
 
 constexpr int kRounds = 8;       // <= 256 hypotheses halve to one in <= 8 rounds; refIt = 8 (:1601)
-constexpr int kRansacThreads = 256;
 constexpr int kMaxHypBlock = 1024;
 constexpr int kAttempts = 32;  // sampling attempts per hypothesis evaluated in one launch
 constexpr int kAttRec = 17;    // attempt record: obj (-1 rejected), R (9), t (3), pixels (4)
@@ -320,6 +321,9 @@ struct P2dWs {
   int32_t* suboff;   // (n_obj, kRounds + 1)
   double* hyp;       // (n_hyp, 16): obj, R (9), t (3)
   double* att;       // (n_hyp, kAttempts, kAttRec) attempt records
+  int32_t* rl;       // (C, kMaxHypBlock) surviving hypotheses per object, in rank order
+  int32_t* rc;       // (C, kMaxHypBlock) their inlier counts of the last round
+  int32_t* rm;       // (C) survivors per object
 };
 
 // one thread per column, its class counts in LDS (a global read-modify-write
@@ -484,92 +488,99 @@ __global__ void __launch_bounds__(64) k_p2d_pick(const float* __restrict__ vm, c
   for (int i = 0; i < 4; i++) hyp_px[h * 4 + i] = px4[i];
 }
 
-// One workgroup per object: the preemptive rounds of :1693-1727 and the output of :1729-1764
-__global__ void __launch_bounds__(kRansacThreads) k_p2d_ransac(const float* __restrict__ vm, const float* __restrict__ ext,
-                                                               int W, int C, Cam k, int n_hyp, P2dWs ws,
-                                                               int32_t* __restrict__ inl_out,
-                                                               int32_t* __restrict__ final_out,
-                                                               float* __restrict__ poses_out) {
-  __shared__ int hl[kMaxHypBlock], hcnt[kMaxHypBlock], tmp[kMaxHypBlock];
-  __shared__ int s_m;
+// The preemptive rounds of :1693-1727 as launches over (surviving
+// hypothesis, object): per round one workgroup counts one hypothesis's
+// inliers over the round's subset (k_p2d_count), then one workgroup per
+// object keeps the better half (k_p2d_select); survivor lists live in the
+// workspace.  k_p2d_collect seeds them (each object's hypotheses in
+// ascending h, the stored order -- see the oracle), k_p2d_finish writes the
+// output of :1729-1764.
+__global__ void __launch_bounds__(64) k_p2d_collect(int n_hyp, P2dWs ws) {
   const int oi = blockIdx.x;
+  if (threadIdx.x != 0) return;
+  const double obj = ws.objs[oi];
+  int m = 0;
+  for (int h = 0; h < n_hyp; h++)
+    if (ws.hyp[(size_t)h * 16] == obj && m < kMaxHypBlock) ws.rl[oi * kMaxHypBlock + m++] = h;
+  ws.rm[oi] = m;
+}
+
+__global__ void __launch_bounds__(256) k_p2d_count(const float* __restrict__ vm, const float* __restrict__ ext, int W,
+                                                   int C, Cam k, P2dWs ws, int r, int32_t* __restrict__ inl_out) {
+  __shared__ int part[4];
+  const int j = blockIdx.x, oi = blockIdx.y;
+  if (j >= ws.rm[oi]) return;  // block-uniform
   const int obj = ws.objs[oi];
   const int* L = ws.lists + ws.listoff[obj];
-  const int lane = pcnn::lane_id(), wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  // this object's hypotheses in ascending h (stored order, see the oracle)
-  if (threadIdx.x == 0) {
-    int m = 0;
-    for (int h = 0; h < n_hyp; h++)
-      if (ws.hyp[(size_t)h * 16] == (double)obj && m < kMaxHypBlock) hl[m++] = h;
-    s_m = m;
+  const int h = ws.rl[oi * kMaxHypBlock + j];
+  const int* S = ws.sub + ws.suboff[oi * (kRounds + 1) + r];
+  const int ns = ws.suboff[oi * (kRounds + 1) + r + 1] - ws.suboff[oi * (kRounds + 1) + r];
+  const double* hr = ws.hyp + (size_t)h * 16;
+  Pose P;
+  for (int i = 0; i < 9; i++) P.R[i] = hr[1 + i];
+  for (int i = 0; i < 3; i++) P.t[i] = hr[10 + i];
+  int cnt = 0;
+  for (int i = threadIdx.x; i < ns; i += 256) {  // countInliers2D (:1171-1214)
+    const int idx = L[S[i]];
+    const double u0 = idx % W, v0 = idx / W;
+    const F3 o = mode3d(vm, ext, C, obj, idx);
+    double u, v;
+    project(P, D3{o.x, o.y, o.z}, k, u, v);
+    if (sqrt((u0 - u) * (u0 - u) + (v0 - v) * (v0 - v)) < 10.0f) cnt++;
   }
+  cnt = pcnn::wave_sum(cnt);
+  if (pcnn::lane_id() == 0) part[threadIdx.x >> 6] = cnt;
   __syncthreads();
-  int m = s_m;
-  if (m == 0) return;
-  for (int r = 0; r < kRounds; r++) {
-    const int* S = ws.sub + ws.suboff[oi * (kRounds + 1) + r];
-    const int ns = ws.suboff[oi * (kRounds + 1) + r + 1] - ws.suboff[oi * (kRounds + 1) + r];
-    for (int j = wave; j < m; j += nw) {  // countInliers2D (:1171-1214) of hypothesis hl[j]
-      const double* hr = ws.hyp + (size_t)hl[j] * 16;
-      Pose P;
-      for (int i = 0; i < 9; i++) P.R[i] = hr[1 + i];
-      for (int i = 0; i < 3; i++) P.t[i] = hr[10 + i];
-      int cnt = 0;
-      for (int i = lane; i < ns; i += 64) {
-        const int idx = L[S[i]];
-        const double u0 = idx % W, v0 = idx / W;
-        const F3 o = mode3d(vm, ext, C, obj, idx);
-        double u, v;
-        project(P, D3{o.x, o.y, o.z}, k, u, v);
-        if (sqrt((u0 - u) * (u0 - u) + (v0 - v) * (v0 - v)) < 10.0f) cnt++;
-      }
-      cnt = pcnn::wave_sum(cnt);
-      if (lane == 0) {
-        hcnt[j] = cnt;
-        inl_out[hl[j] * kRounds + r] = cnt;
-      }
-    }
-    __syncthreads();
-    if (m > 1) {  // stable sort by inliers (descending), keep the better half
-      for (int j = threadIdx.x; j < m; j += blockDim.x) {
-        int rank = 0;
-        for (int q = 0; q < m; q++) rank += hcnt[q] > hcnt[j] || (hcnt[q] == hcnt[j] && q < j);
-        tmp[rank] = j;
-      }
-      __syncthreads();
-      const int keep = m / 2;
-      int nh = 0, nc = 0;
-      if (threadIdx.x < keep) {
-        nh = hl[tmp[threadIdx.x]];
-        nc = hcnt[tmp[threadIdx.x]];
-      }
-      int nh2 = 0, nc2 = 0;  // keep <= 512: a second element per thread
-      if (threadIdx.x + blockDim.x < keep) {
-        nh2 = hl[tmp[threadIdx.x + blockDim.x]];
-        nc2 = hcnt[tmp[threadIdx.x + blockDim.x]];
-      }
-      __syncthreads();
-      if (threadIdx.x < keep) { hl[threadIdx.x] = nh; hcnt[threadIdx.x] = nc; }
-      if (threadIdx.x + blockDim.x < keep) { hl[threadIdx.x + blockDim.x] = nh2; hcnt[threadIdx.x + blockDim.x] = nc2; }
-      m = keep;
-      __syncthreads();
-    }
-  }
   if (threadIdx.x == 0) {
-    const int h = hl[0];
-    int nh = 0;
-    for (int q = 0; q < n_hyp; q++) nh += ws.hyp[(size_t)q * 16] == (double)obj;
-    final_out[obj * 3] = h;
-    final_out[obj * 3 + 1] = hcnt[0];
-    final_out[obj * 3 + 2] = nh;
-    const double* hr = ws.hyp + (size_t)h * 16;
-    for (int y = 0; y < 3; y++)
-      for (int x = 0; x < 4; x++) poses_out[obj + C * (y * 4 + x)] = x < 3 ? (float)hr[1 + y * 3 + x] : (float)hr[10 + y];
+    const int c = part[0] + part[1] + part[2] + part[3];
+    ws.rc[oi * kMaxHypBlock + j] = c;
+    inl_out[h * kRounds + r] = c;
   }
 }
 
+// stable sort by inliers (descending, then list position), keep the better half
+__global__ void __launch_bounds__(1024) k_p2d_select(P2dWs ws) {
+  __shared__ int hl[kMaxHypBlock], hc[kMaxHypBlock], tmp[kMaxHypBlock];
+  const int oi = blockIdx.x;
+  const int m = ws.rm[oi];
+  if (m <= 1) return;
+  for (int j = threadIdx.x; j < m; j += blockDim.x) {
+    hl[j] = ws.rl[oi * kMaxHypBlock + j];
+    hc[j] = ws.rc[oi * kMaxHypBlock + j];
+  }
+  __syncthreads();
+  for (int j = threadIdx.x; j < m; j += blockDim.x) {
+    int rank = 0;
+    for (int q = 0; q < m; q++) rank += hc[q] > hc[j] || (hc[q] == hc[j] && q < j);
+    tmp[rank] = j;
+  }
+  __syncthreads();
+  const int keep = m / 2;
+  for (int j = threadIdx.x; j < keep; j += blockDim.x) {
+    ws.rl[oi * kMaxHypBlock + j] = hl[tmp[j]];
+    ws.rc[oi * kMaxHypBlock + j] = hc[tmp[j]];
+  }
+  if (threadIdx.x == 0) ws.rm[oi] = keep;
+}
+
+__global__ void __launch_bounds__(64) k_p2d_finish(int C, int n_hyp, P2dWs ws, int32_t* __restrict__ final_out,
+                                                   float* __restrict__ poses_out) {
+  const int oi = blockIdx.x;
+  if (threadIdx.x != 0 || ws.rm[oi] == 0) return;
+  const int obj = ws.objs[oi];
+  const int h = ws.rl[oi * kMaxHypBlock];
+  int nh = 0;
+  for (int q = 0; q < n_hyp; q++) nh += ws.hyp[(size_t)q * 16] == (double)obj;
+  final_out[obj * 3] = h;
+  final_out[obj * 3 + 1] = ws.rc[oi * kMaxHypBlock];
+  final_out[obj * 3 + 2] = nh;
+  const double* hr = ws.hyp + (size_t)h * 16;
+  for (int y = 0; y < 3; y++)
+    for (int x = 0; x < 4; x++) poses_out[obj + C * (y * 4 + x)] = x < 3 ? (float)hr[1 + y * 3 + x] : (float)hr[10 + y];
+}
+
 struct Layout {
-  size_t colcnt, coloff, count, lists, listoff, objs, suboff, hyp, att, sub, total;
+  size_t colcnt, coloff, count, lists, listoff, objs, suboff, hyp, att, rl, rc, rm, sub, total;
 };
 
 Layout layout(int H, int W, int C, int n_hyp) {
@@ -591,6 +602,9 @@ Layout layout(int H, int W, int C, int n_hyp) {
   l.suboff = take((size_t)C * (kRounds + 1) * sizeof(int32_t));
   l.hyp = take((size_t)n_hyp * 16 * sizeof(double));
   l.att = take((size_t)n_hyp * kAttempts * kAttRec * sizeof(double));
+  l.rl = take((size_t)C * kMaxHypBlock * sizeof(int32_t));
+  l.rc = take((size_t)C * kMaxHypBlock * sizeof(int32_t));
+  l.rm = take((size_t)C * sizeof(int32_t));
   // subsets: a round visits at most every pixel of the class once
   l.sub = take((size_t)kRounds * H * W * sizeof(int32_t));
   l.total = off + 256;
@@ -624,6 +638,9 @@ extern "C" int pcnn_pose2d(const int32_t* label, const float* vertmap, const flo
   ws.suboff = (int32_t*)(base + l.suboff);
   ws.hyp = (double*)(base + l.hyp);
   ws.att = (double*)(base + l.att);
+  ws.rl = (int32_t*)(base + l.rl);
+  ws.rc = (int32_t*)(base + l.rc);
+  ws.rm = (int32_t*)(base + l.rm);
   ws.sub = (int32_t*)(base + l.sub);
   hipStream_t st = (hipStream_t)stream;
   if (hipMemsetAsync(poses_out, 0, (size_t)12 * C * sizeof(float), st) != hipSuccess) return PCNN_EHIP;
@@ -688,14 +705,25 @@ extern "C" int pcnn_pose2d(const int32_t* label, const float* vertmap, const flo
     }
   };
   {
+    // largest first (a task draws about min(N, 1000 r) variates) from a
+    // shared counter: the makespan is close to the total over the threads,
+    // not three round-8 tasks on one thread
+    std::vector<int> order(n_task);
+    for (int t = 0; t < n_task; t++) order[t] = t;
+    auto cost = [&](int t) {
+      const int N = cnt[objs[t / kRounds]], r = t % kRounds + 1;
+      return 1000 * r < N ? 1000 * r : 0;
+    };
+    std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return cost(a) > cost(b); });
+    std::atomic<int> next{0};
+    auto work = [&] {
+      for (int i; (i = next.fetch_add(1)) < n_task;) draw(order[i]);
+    };
     const unsigned hw = std::thread::hardware_concurrency();
     const int nthr = std::max(1, std::min(n_task, (int)std::min(hw ? hw : 1u, 16u)));
     std::vector<std::thread> pool;
-    for (int w = 1; w < nthr; w++)
-      pool.emplace_back([&, w] {
-        for (int t = w; t < n_task; t += nthr) draw(t);
-      });
-    for (int t = 0; t < n_task; t += nthr) draw(t);
+    for (int w = 1; w < nthr; w++) pool.emplace_back(work);
+    work();
     for (auto& th : pool) th.join();
   }
   std::vector<int32_t> sub, suboff;
@@ -712,8 +740,13 @@ extern "C" int pcnn_pose2d(const int32_t* label, const float* vertmap, const flo
           hipSuccess ||
       hipMemcpyAsync(ws.sub, sub.data(), sub.size() * sizeof(int32_t), hipMemcpyHostToDevice, st) != hipSuccess)
     return PCNN_EHIP;
-  hipLaunchKernelGGL(k_p2d_ransac, dim3(n_obj), dim3(kRansacThreads), 0, st, vertmap, extents, W, C, k, n_hyp, ws,
-                     inl_out, final_out, poses_out);
+  hipLaunchKernelGGL(k_p2d_collect, dim3(n_obj), dim3(64), 0, st, n_hyp, ws);
+  for (int r = 0; r < kRounds; r++) {
+    const int gx = std::max(1, n_hyp >> r);  // survivors halve each round (one stays one)
+    hipLaunchKernelGGL(k_p2d_count, dim3(gx, n_obj), dim3(256), 0, st, vertmap, extents, W, C, k, ws, r, inl_out);
+    hipLaunchKernelGGL(k_p2d_select, dim3(n_obj), dim3(1024), 0, st, ws);
+  }
+  hipLaunchKernelGGL(k_p2d_finish, dim3(n_obj), dim3(64), 0, st, C, n_hyp, ws, final_out, poses_out);
   PCNN_CHECK_LAUNCH();
   // the host vectors above are the sources of the async copies
   if (hipStreamSynchronize(st) != hipSuccess) return PCNN_EHIP;
