@@ -787,10 +787,14 @@ __global__ void __launch_bounds__(kBlk) k_grid_count(const float4* __restrict__ 
 __global__ void __launch_bounds__(1024) k_grid_scan(const int32_t* __restrict__ bcount, int32_t* __restrict__ start,
                                                     int32_t* __restrict__ cursor) {
   __shared__ int part[1024];
-  constexpr int per = kGridBuckets / 1024;
+  constexpr int per = kGridBuckets / 1024;  // 128 consecutive buckets per thread, as 32 int4 loads in flight
   const int t = threadIdx.x;
+  int4 v[per / 4];
+#pragma unroll
+  for (int k = 0; k < per / 4; k++) v[k] = ((const int4*)(bcount + t * per))[k];
   int s = 0;
-  for (int k = 0; k < per; k++) s += bcount[t * per + k];
+#pragma unroll
+  for (int k = 0; k < per / 4; k++) s += v[k].x + v[k].y + v[k].z + v[k].w;
   part[t] = s;
   __syncthreads();
   for (int off = 1; off < 1024; off <<= 1) {  // Hillis-Steele inclusive scan
@@ -800,11 +804,16 @@ __global__ void __launch_bounds__(1024) k_grid_scan(const int32_t* __restrict__ 
     __syncthreads();
   }
   int run = part[t] - s;
-  for (int k = 0; k < per; k++) {
-    const int b = t * per + k;
-    start[b] = run;
-    cursor[b] = run;
-    run += bcount[b];
+#pragma unroll
+  for (int k = 0; k < per / 4; k++) {
+    int4 o;
+    o.x = run;
+    o.y = o.x + v[k].x;
+    o.z = o.y + v[k].y;
+    o.w = o.z + v[k].z;
+    run = o.w + v[k].w;
+    ((int4*)(start + t * per))[k] = o;
+    ((int4*)(cursor + t * per))[k] = o;
   }
   if (t == 1023) start[kGridBuckets] = run;
 }

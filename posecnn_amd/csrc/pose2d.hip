@@ -495,14 +495,18 @@ __global__ void __launch_bounds__(64) k_p2d_pick(const float* __restrict__ vm, c
 // workspace.  k_p2d_collect seeds them (each object's hypotheses in
 // ascending h, the stored order -- see the oracle), k_p2d_finish writes the
 // output of :1729-1764.
-__global__ void __launch_bounds__(64) k_p2d_collect(int n_hyp, P2dWs ws) {
-  const int oi = blockIdx.x;
-  if (threadIdx.x != 0) return;
+__global__ void __launch_bounds__(64) k_p2d_collect(int n_hyp, P2dWs ws) {  // one wave per object
+  const int oi = blockIdx.x, lane = pcnn::lane_id();
   const double obj = ws.objs[oi];
   int m = 0;
-  for (int h = 0; h < n_hyp; h++)
-    if (ws.hyp[(size_t)h * 16] == obj && m < kMaxHypBlock) ws.rl[oi * kMaxHypBlock + m++] = h;
-  ws.rm[oi] = m;
+  for (int h0 = 0; h0 < n_hyp; h0 += 64) {  // ballot compaction keeps ascending h
+    const int h = h0 + lane;
+    const bool mine = h < n_hyp && ws.hyp[(size_t)h * 16] == obj;
+    const uint64_t b = __ballot(mine);
+    if (mine) ws.rl[oi * kMaxHypBlock + m + __popcll(b & pcnn::lanemask_lt())] = h;
+    m += __popcll(b);
+  }
+  if (lane == 0) ws.rm[oi] = m;
 }
 
 __global__ void __launch_bounds__(256) k_p2d_count(const float* __restrict__ vm, const float* __restrict__ ext, int W,
@@ -565,12 +569,14 @@ __global__ void __launch_bounds__(1024) k_p2d_select(P2dWs ws) {
 
 __global__ void __launch_bounds__(64) k_p2d_finish(int C, int n_hyp, P2dWs ws, int32_t* __restrict__ final_out,
                                                    float* __restrict__ poses_out) {
-  const int oi = blockIdx.x;
-  if (threadIdx.x != 0 || ws.rm[oi] == 0) return;
+  const int oi = blockIdx.x, lane = pcnn::lane_id();  // one wave per object
+  if (ws.rm[oi] == 0) return;
   const int obj = ws.objs[oi];
   const int h = ws.rl[oi * kMaxHypBlock];
   int nh = 0;
-  for (int q = 0; q < n_hyp; q++) nh += ws.hyp[(size_t)q * 16] == (double)obj;
+  for (int q = lane; q < n_hyp; q += 64) nh += ws.hyp[(size_t)q * 16] == (double)obj;
+  nh = pcnn::wave_sum(nh);
+  if (lane != 0) return;
   final_out[obj * 3] = h;
   final_out[obj * 3 + 1] = ws.rc[oi * kMaxHypBlock];
   final_out[obj * 3 + 2] = nh;

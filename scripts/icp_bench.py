@@ -86,7 +86,8 @@ score_dense_us = timed(lambda: R.icp_score(dl, dense_lab, 1, dv, dhy))
 res["icp_score_us"] = {"scene_object": round(score_scene_us, 1), "dense_640x480": round(score_dense_us, 1),
                        "scene_object_points": int(((sc["live"]["label"] == sc["cls"])).sum()),
                        "dense_points": H * W, "hypotheses": 8,
-                       "note": "pcnn_icp_score: compaction, 1 cm grid buckets, nearest depth point per model point"}
+                       "note": "pcnn_icp_score: compaction, hashed half-radius cells searched ring by ring, nearest depth point "
+                               "per model point, per-hypothesis flag counts"}
 # solve_icp end to end (live vertices, re-centring, Nelder-Mead on optEnergy,
 # 8 hypotheses x ICP, SegICP score) for a RoIs of one frame, the renderer a
 # GPU ray-caster standing in for the reference's OpenGL pass
