@@ -254,6 +254,7 @@ __global__ void __launch_bounds__(X6Tile<T>::threads, T == 256 ? 1 : 2) k_gemm_x
             for (int c = 0; c < 4; c++) stage_part(c, nxt, kn);
           } else {
             bf16x8 bh[2], bm[2], bl[2];
+            bf16x8 ah[2], am[2], al[2];
 #pragma unroll
             for (int j = 0; j < 2; j++) {
               bh[j] = X6_FRAG(cur + 3 * PART + b_off[j]);
@@ -264,7 +265,6 @@ __global__ void __launch_bounds__(X6Tile<T>::threads, T == 256 ? 1 : 2) k_gemm_x
 #pragma unroll
               for (int p = 0; p < 4; p++) stage_part(p, nxt, kn);
             }
-            bf16x8 ah[2], am[2], al[2];
             ah[0] = X6_FRAG(cur + a_off[0]);
             am[0] = X6_FRAG(cur + PART + a_off[0]);
             al[0] = X6_FRAG(cur + 2 * PART + a_off[0]);
