@@ -261,68 +261,6 @@ __device__ __forceinline__ void x_epilogue(const GemmArgs& g, const XPlan& pl, c
   }
 }
 
-// x_epilogue for the v_mfma_f32_16x16x32 accumulator layout: block (i, j)
-// of 16 x 16, lane l holds rows 4 (l >> 4) + q (q < 4) of column l & 15.
-template <int T, int EI, int EJ>
-__device__ __forceinline__ void x_epilogue16(const GemmArgs& g, const XPlan& pl, const f32x4 (&acc)[EI][EJ], int m0,
-                                             int n0, int rl, int z, int wm, int wn, int lane) {
-  constexpr int EQ = 4, EB = 16;
-  const int rlane = wm * (T / 2) + 4 * (lane >> 4), clane = wn * (EB * EJ) + (lane & 15);
-  auto qrow = [](int i, int q) { return i * EB + q; };
-  const int rlim = rl - m0, clim = g.N - n0;
-  if (pl.mode == 1) {  // split-K slice: raw partial sums to slab z
-    const XOp oslab = x_op(g.slab, g.N, (long)pl.S * g.M * g.N);
-    const unsigned sb = (unsigned)(((z * g.M + m0 + rlane) * g.N + n0 + clane) * 4);
-#pragma unroll
-    for (int j = 0; j < EJ; j++)
-#pragma unroll
-      for (int i = 0; i < EI; i++)
-#pragma unroll
-        for (int q = 0; q < EQ; q++) {
-          const bool ok = clane < clim - j * EB && rlane < rlim - qrow(i, q);
-          const float v = acc[i][j][q];
-          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), oslab.rs,
-                                                ok ? sb + (unsigned)((qrow(i, q) * g.N + j * EB) * 4) : kXOob,
-                                                0, 0);
-        }
-    return;
-  }
-  const bool msk = g.mask != nullptr;
-  const XOp oc = x_op(g.C, g.ldc, (long)(g.M - 1) * g.ldc + g.N);
-  const XOp obias = x_op(g.bias, 0, g.N);
-  const XOp omask = x_op(g.mask, g.ldm, g.mask ? (long)(g.M - 1) * g.ldm + g.N : 0);
-  const unsigned cbase = (unsigned)(((m0 + rlane) * g.ldc + n0 + clane) * 4);
-  const unsigned mbase = (unsigned)(((m0 + rlane) * g.ldm + n0 + clane) * 4);
-#pragma unroll
-  for (int j = 0; j < EJ; j++) {
-    const bool nok = clane < clim - j * EB;
-    const float bv = g.bias ? x_ld1(obias, nok ? (unsigned)((n0 + clane + j * EB) * 4) : kXOob, 0) : 0.f;
-#pragma unroll
-    for (int i = 0; i < EI; i++) {
-      float mv[EQ];
-      if (msk) {
-#pragma unroll
-        for (int q = 0; q < EQ; q++) {
-          const bool ok = nok && rlane < rlim - qrow(i, q);
-          mv[q] = x_ld1(omask, ok ? mbase + (unsigned)((qrow(i, q) * g.ldm + j * EB) * 4) : kXOob, 0);
-        }
-      }
-#pragma unroll
-      for (int q = 0; q < EQ; q++) {
-        const bool ok = nok && rlane < rlim - qrow(i, q);
-        float v = acc[i][j][q] + bv;
-        if (g.act == 1) v = v > 0.f ? v : 0.f;
-        if (msk && !(mv[q] > 0.f)) v = 0.f;
-        const unsigned co = ok ? cbase + (unsigned)((qrow(i, q) * g.ldc + j * EB) * 4) : kXOob;
-        if (g.c_stream)
-          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), oc.rs, co, 0, kXNonTemporal);
-        else
-          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), oc.rs, co, 0, 0);
-      }
-    }
-  }
-}
-
 // Launch of the x6 kernel (gemm_x6.hip) for a prepared argument block.
 void launch_gemm_x6(const GemmArgs& g, int grid, bool a_trans, bool b_trans, bool ragged, bool a2, bool gen,
                     hipStream_t st);

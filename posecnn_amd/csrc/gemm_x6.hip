@@ -179,14 +179,6 @@ __global__ void __launch_bounds__(X6Tile<T>::threads, T == 256 ? 1 : 2) k_gemm_x
   for (int i = 0; i < AM; i++) a_off[i] = x6_off(wm * (T / 2) + i * 32 + r, hsel);
 #pragma unroll
   for (int j = 0; j < 2; j++) b_off[j] = x6_off(wn * 64 + j * 32 + r, hsel);
-#ifdef PCNN_X6_MFMA16
-  // 16 x 16 x 32 fragments: lane -> row (or column) l & 15, k half (l >> 4) & 1
-  int a16_off[2 * AM], b16_off[4];
-#pragma unroll
-  for (int i = 0; i < 2 * AM; i++) a16_off[i] = x6_off(wm * (T / 2) + i * 16 + (lane & 15), (lane >> 4) & 1);
-#pragma unroll
-  for (int j = 0; j < 4; j++) b16_off[j] = x6_off(wn * 64 + j * 16 + (lane & 15), (lane >> 4) & 1);
-#endif
 
   auto segment = [&](int t, int kl, int kh, int z) {
     const int m0 = pl.mi_of(t) * pl.Tm, n0 = pl.ni_of(t) * T;
@@ -196,19 +188,11 @@ __global__ void __launch_bounds__(X6Tile<T>::threads, T == 256 ? 1 : 2) k_gemm_x
     const int live = rl - (m0 + wm * (T / 2));
     int amw = live <= 0 ? 0 : (live + 31) / 32;
     amw = __builtin_amdgcn_readfirstlane(amw < AM ? amw : AM);
-#ifdef PCNN_X6_MFMA16
-    f32x4 acc[2 * AM][4];  // 16 x 16 blocks (v_mfma_f32_16x16x32_bf16)
-#pragma unroll
-    for (int i = 0; i < 2 * AM; i++)
-#pragma unroll
-      for (int j = 0; j < 4; j++) acc[i][j] = (f32x4){};
-#else
     f32x16 acc[AM][2];
 #pragma unroll
     for (int i = 0; i < AM; i++)
 #pragma unroll
       for (int j = 0; j < 2; j++) acc[i][j] = (f32x16){};
-#endif
     if (nsteps > 0) {
       float va[8], vb[8];
       // prologue: stage 0 -> LDS buffer 0, stage 1 -> registers
@@ -269,53 +253,6 @@ __global__ void __launch_bounds__(X6Tile<T>::threads, T == 256 ? 1 : 2) k_gemm_x
 #pragma unroll
             for (int c = 0; c < 4; c++) stage_part(c, nxt, kn);
           } else {
-#ifdef PCNN_X6_MFMA16
-            // 16 x 16 x 32 MFMAs on plane pairs concatenated along K: lanes
-            // 0-31 carry k 0-15 of one plane, lanes 32-63 of another, so one
-            // MFMA adds two of the six products: [lo | hi] . [hi ; lo],
-            // [mid | mid] . [mid ; hi], [hi | hi] . [mid ; hi]
-            const int up = lane >> 5;
-            bf16x8 bp1[4], bp2[4];
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-              bp1[j] = X6_FRAG(cur + (up ? 5 : 3) * PART + b16_off[j]);
-              bp2[j] = X6_FRAG(cur + (up ? 3 : 4) * PART + b16_off[j]);
-            }
-            if constexpr (MODE == 2) {
-#pragma unroll
-              for (int p = 0; p < 4; p++) stage_part(p, nxt, kn);
-            }
-            bf16x8 a1[2], a2[2], a3[2];
-            a1[0] = X6_FRAG(cur + (up ? 0 : 2) * PART + a16_off[0]);
-            a2[0] = X6_FRAG(cur + PART + a16_off[0]);
-            a3[0] = X6_FRAG(cur + a16_off[0]);
-#pragma unroll
-            for (int i = 0; i < AMW; i++) {
-              if constexpr (STAGE_FIRST) {
-#pragma unroll
-                for (int p = i * 4 / AMW; p < (i + 1) * 4 / AMW; p++) stage_part(p, nxt, kn);
-              }
-#pragma unroll
-              for (int sb = 0; sb < 2; sb++) {
-                const int ii = 2 * i + sb, c = ii & 1;
-                if (ii + 1 < 2 * AMW) {  // the next 16-row block's fragments in flight
-                  a1[c ^ 1] = X6_FRAG(cur + (up ? 0 : 2) * PART + a16_off[ii + 1]);
-                  a2[c ^ 1] = X6_FRAG(cur + PART + a16_off[ii + 1]);
-                  a3[c ^ 1] = X6_FRAG(cur + a16_off[ii + 1]);
-                }
-#pragma unroll
-                for (int j = 0; j < 4; j++) {
-                  acc[ii][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[c], bp1[j], acc[ii][j], 0, 0, 0);
-                  acc[ii][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a2[c], bp2[j], acc[ii][j], 0, 0, 0);
-                  acc[ii][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a3[c], bp2[j], acc[ii][j], 0, 0, 0);
-                }
-              }
-              if constexpr (MODE == 0) {
-#pragma unroll
-                for (int p = i * 4 / AMW; p < (i + 1) * 4 / AMW; p++) stage_part(p, nxt, kn);
-              }
-            }
-#else
             bf16x8 bh[2], bm[2], bl[2];
             bf16x8 ah[2], am[2], al[2];
 #pragma unroll
@@ -357,7 +294,6 @@ __global__ void __launch_bounds__(X6Tile<T>::threads, T == 256 ? 1 : 2) k_gemm_x
                 for (int p = i * 4 / AMW; p < (i + 1) * 4 / AMW; p++) stage_part(p, nxt, kn);
               }
             }
-#endif
             if constexpr (MODE == 3) {
 #pragma unroll
               for (int p = 0; p < 4; p++) stage_part(p, nxt, kn);
@@ -394,11 +330,7 @@ __global__ void __launch_bounds__(X6Tile<T>::threads, T == 256 ? 1 : 2) k_gemm_x
         else kloop_w(IC<3>{});
       }
     }
-#ifdef PCNN_X6_MFMA16
-    x_epilogue16<T, 2 * AM, 4>(g, pl, acc, m0, n0, rl, z, wm, wn, lane);
-#else
     x_epilogue<T, AM>(g, pl, acc, m0, n0, rl, z, wm, wn, r, hsel);
-#endif
   };
 
   const int kstep = (pl.ns + pl.S - 1) / pl.S;  // split-K: K steps per slice
