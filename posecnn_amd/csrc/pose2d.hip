@@ -326,19 +326,24 @@ struct P2dWs {
   int32_t* rm;       // (C) survivors per object
 };
 
-// one thread per column, its class counts in LDS (a global read-modify-write
-// per pixel would put a memory latency on every step of the column walk)
-__global__ void __launch_bounds__(64) k_p2d_colcount(const int32_t* __restrict__ label, int H, int W, int C,
-                                                     int32_t* colcnt) {
-  extern __shared__ int cc[];  // [C][64]
-  const int x = blockIdx.x * 64 + threadIdx.x;
-  for (int c = 0; c < C; c++) cc[c * 64 + threadIdx.x] = 0;
-  if (x >= W) return;
-  for (int y = 0; y < H; y++) {
-    const int c = label[y * W + x];
-    if (c >= 0 && c < C) cc[c * 64 + threadIdx.x]++;
+// one wave per column (4 per workgroup): 64 rows at a time, class counts by
+// LDS atomics (integer adds: order-free, exact), C <= 64 counters per wave
+__global__ void __launch_bounds__(256) k_p2d_colcount(const int32_t* __restrict__ label, int H, int W, int C,
+                                                      int32_t* colcnt) {
+  __shared__ int cc[4][64];
+  const int lane = pcnn::lane_id(), wv = threadIdx.x >> 6;
+  const int x = blockIdx.x * 4 + wv;
+  cc[wv][lane] = 0;
+  __syncthreads();
+  if (x < W) {
+    for (int y0 = 0; y0 < H; y0 += 64) {
+      const int y = y0 + lane;
+      const int c = y < H ? label[y * W + x] : -1;
+      if (c >= 0 && c < C) atomicAdd(&cc[wv][c], 1);
+    }
   }
-  for (int c = 0; c < C; c++) colcnt[c * W + x] = cc[c * 64 + threadIdx.x];
+  __syncthreads();
+  if (x < W && lane < C) colcnt[lane * W + x] = cc[wv][lane];
 }
 
 __global__ void __launch_bounds__(1024) k_p2d_scan(const int32_t* __restrict__ colcnt, int W, int32_t* coloff,
@@ -364,16 +369,30 @@ __global__ void __launch_bounds__(1024) k_p2d_scan(const int32_t* __restrict__ c
   if (threadIdx.x == 0) count[c] = carry;
 }
 
-__global__ void __launch_bounds__(64) k_p2d_scatter(const int32_t* __restrict__ label, int H, int W, int C, P2dWs ws) {
-  extern __shared__ int run[];  // [C][64] running counts of this block's columns
-  const int x = blockIdx.x * 64 + threadIdx.x;
-  for (int c = 0; c < C; c++) run[c * 64 + threadIdx.x] = 0;
+// one wave per column: 64 rows at a time; the lanes of one class take their
+// ranks by ballot (classes peeled one at a time, usually 1-3 per chunk), so
+// each class list keeps the column's ascending row order
+__global__ void __launch_bounds__(256) k_p2d_scatter(const int32_t* __restrict__ label, int H, int W, int C, P2dWs ws) {
+  __shared__ int run[4][64];  // per wave: class -> pixels placed so far in this column
+  const int lane = pcnn::lane_id(), wv = threadIdx.x >> 6;
+  const int x = blockIdx.x * 4 + wv;
+  run[wv][lane] = 0;
+  __syncthreads();
   if (x >= W) return;
-  for (int y = 0; y < H; y++) {
-    const int c = label[y * W + x];
-    if (c < 0 || c >= C) continue;
-    const int r = run[c * 64 + threadIdx.x]++;
-    ws.lists[ws.listoff[c] + ws.coloff[c * W + x] + r] = y * W + x;
+  for (int y0 = 0; y0 < H; y0 += 64) {
+    const int y = y0 + lane;
+    const int c = y < H ? label[y * W + x] : -1;
+    bool pending = c >= 0 && c < C;
+    for (uint64_t left = __ballot(pending); left; left = __ballot(pending)) {
+      const int cl = __shfl(c, __ffsll((unsigned long long)left) - 1);
+      const uint64_t m = __ballot(pending && c == cl);
+      const int base = run[wv][cl];
+      if (pending && c == cl) {
+        ws.lists[ws.listoff[cl] + ws.coloff[cl * W + x] + base + __popcll(m & pcnn::lanemask_lt())] = y * W + x;
+        pending = false;
+      }
+      if (lane == 0) run[wv][cl] = base + __popcll(m);
+    }
   }
 }
 
@@ -652,8 +671,7 @@ extern "C" int pcnn_pose2d(const int32_t* label, const float* vertmap, const flo
   if (hipMemsetAsync(poses_out, 0, (size_t)12 * C * sizeof(float), st) != hipSuccess) return PCNN_EHIP;
   if (hipMemsetAsync(inl_out, 0xFF, (size_t)n_hyp * kRounds * sizeof(int32_t), st) != hipSuccess) return PCNN_EHIP;
   if (hipMemsetAsync(final_out, 0xFF, (size_t)C * 3 * sizeof(int32_t), st) != hipSuccess) return PCNN_EHIP;
-  hipLaunchKernelGGL(k_p2d_colcount, dim3((W + 63) / 64), dim3(64), C * 64 * sizeof(int), st, label, H, W, C,
-                     ws.colcnt);
+  hipLaunchKernelGGL(k_p2d_colcount, dim3((W + 3) / 4), dim3(256), 0, st, label, H, W, C, ws.colcnt);
   hipLaunchKernelGGL(k_p2d_scan, dim3(C), dim3(1024), 0, st, ws.colcnt, W, ws.coloff, ws.count);
   PCNN_CHECK_LAUNCH();
   // the class sizes decide object_ids (> minArea = 400, :1027) and the
@@ -682,7 +700,7 @@ extern "C" int pcnn_pose2d(const int32_t* label, const float* vertmap, const flo
   const Cam k{fx, fy, px, py};
   // the class lists and the hypotheses run on the GPU while the host draws
   // the rounds' pixel subsets below
-  hipLaunchKernelGGL(k_p2d_scatter, dim3((W + 63) / 64), dim3(64), C * 64 * sizeof(int), st, label, H, W, C, ws);
+  hipLaunchKernelGGL(k_p2d_scatter, dim3((W + 3) / 4), dim3(256), 0, st, label, H, W, C, ws);
   const int T = max_iter < kAttempts ? max_iter : kAttempts;
   hipLaunchKernelGGL(k_p2d_attempts, dim3((n_hyp * T + 63) / 64), dim3(64), 0, st, vertmap, extents, H, W, C, k, seed,
                      n_hyp, n_obj, T, ws);
