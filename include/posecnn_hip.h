@@ -317,21 +317,23 @@ int pcnn_dropout_mask(uint8_t* mask, int rows, int cols, int ld, const int32_t* 
 int pcnn_philox_check(const uint32_t* ctr, const uint32_t* key, int n, uint32_t* out, void* stream);
 
 /* ---------------------------------------------------------------------------
- * RGB-only pose estimation (SURVEY §8(f) rank 4, the RANSAC half).
+ * RGB-only pose estimation (SURVEY §8(f) row 4, the RANSAC half).
  * Replaces Synthesizer::estimatePose2D (lib/synthesize/synthesize.cpp:1571-1766;
  * synthesizer.pyx:74-82 estimate_poses_2d, called from lib/fcn/test.py:1364).
  *  label (H,W) int32, vertmap (H,W,3C) object coordinates scaled to [0,1] by the
  *  class extents (getMode3D, :1052-1071), extents (C,3), pinhole fx fy px py.
  *  Preemptive RANSAC: n_hyp (256 in the reference) hypotheses, each from 4
- *  pixels of one object (> 400 pixels) through P3P, sampled on Philox stream h
- *  of `seed` (at most max_iter draws each); 8 rounds of inlier counting (< 10 px)
+ *  pixels of one object (> 400 pixels) through P3P; attempt a of hypothesis h
+ *  draws on its own Philox stream (h, a) of `seed`, h keeps its first accepted
+ *  attempt (at most max_iter attempts); 8 rounds of inlier counting (< 10 px)
  *  over the reference's negative-binomial pixel subsets, keeping the better
  *  half.  Outputs (device): poses_out (3,4,C) [R | t] per class (the reference's
  *  layout; classes without a hypothesis 0); hyps_out (n_hyp,13) [objID or -1 |
  *  R | t]; hyp_px (n_hyp,4) sampled pixel indices; inl_out (n_hyp,8) inliers per
  *  round (-1: not queued); final_out (C,3) [h, inliers, hypotheses] (-1: none).
  *  Synchronises `stream` (the class sizes decide the objects and the subsets,
- *  drawn on the host with the reference's std::mt19937 / negative_binomial). */
+ *  drawn on up to 16 host threads with the reference's std::mt19937 /
+ *  negative_binomial while the sampling kernels run). */
 size_t pcnn_pose2d_workspace_size(int H, int W, int C, int n_hyp);
 int pcnn_pose2d(const int32_t* label, const float* vertmap, const float* extents, int H, int W, int C, float fx,
                 float fy, float px, float py, uint64_t seed, int n_hyp, int max_iter, float* poses_out,
