@@ -117,7 +117,8 @@ def test_icp_score_matches_oracle(hip, orc):
     assert int(ch[0]) == cho
 
 
-def test_icp_score_grid_ties_and_far_points(hip, orc):
+@pytest.mark.parametrize("radius", [0.005, 0.01, 0.03])
+def test_icp_score_grid_ties_and_far_points(hip, orc, radius):
     """The grid-bucketed nearest-point search against the oracle's brute force
     on a dense lattice cloud: depth and model points on a 4 mm lattice (many
     candidates per 1 cm radius, exact distance ties -> the lowest index wins),
@@ -142,8 +143,8 @@ def test_icp_score_grid_ties_and_far_points(hip, orc):
     hyps[2, 6] = 60.8                                      # onto the far points
     hyps[3, 6] = 5.0                                       # misses everything
     hyps[1, :4] = (0.9995, 0.02, -0.01, 0.0)
-    s, ch = R.icp_score(t(live.reshape(H, W, 3)), t(label), obj, t(vm.reshape(H, W, 3)), t(hyps))
-    so, cho = orc.icp_score(live.reshape(H, W, 3), label, obj, vm.reshape(H, W, 3), hyps)
+    s, ch = R.icp_score(t(live.reshape(H, W, 3)), t(label), obj, t(vm.reshape(H, W, 3)), t(hyps), radius=radius)
+    so, cho = orc.icp_score(live.reshape(H, W, 3), label, obj, vm.reshape(H, W, 3), hyps, radius=radius)
     np.testing.assert_array_equal(s.cpu().numpy(), so)
     assert int(ch[0]) == cho
     assert so[0] > 0 and so[2] > 0 and so[3] == 0

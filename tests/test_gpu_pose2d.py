@@ -48,6 +48,23 @@ def test_pose2d_matches_oracle(hip, noise, seed):
         assert np.abs(got - want).max() < (0.1 if noise == 0.0 else 5.0)
 
 
+@pytest.mark.parametrize("max_iter", [3, 40])
+def test_pose2d_attempt_limit_matches_oracle(hip, max_iter):
+    """max_iter bounds each hypothesis's attempts: 3 (< the 32 evaluated at
+    once: some hypotheses stay empty) and 40 (attempts past the batch run one
+    by one); hypotheses, survivors and poses against the oracle."""
+    sc = make_scene(seed=6, coord_noise=0.01)
+    poses, d = _run(sc, max_iter=max_iter)
+    r = oracle.pose2d(sc["label"], sc["vertmap"], sc["extents"], *sc["camera"], max_iter=max_iter)
+    np.testing.assert_array_equal(d["hyps"][:, 0], r["hyps"][:, 0])
+    np.testing.assert_array_equal(d["hyp_px"], r["hyp_px"])
+    np.testing.assert_array_equal(d["inliers"], r["inliers"])
+    np.testing.assert_array_equal(d["final"], r["final"])
+    np.testing.assert_allclose(poses, r["poses"], atol=1e-5)
+    if max_iter == 3:
+        assert (d["hyps"][:, 0] < 0).any()  # the limit bites
+
+
 def test_pose2d_device_inputs_and_no_object(hip):
     sc = make_scene(seed=4, n_obj=2)
     dev = torch.device("cuda")
