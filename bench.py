@@ -290,7 +290,7 @@ def main():
     # it does not touch): one HIP event pair per step (median and
     # p10 / p90), and the practical HBM peak (device-to-device copy) beside the
     # spec peak of the roofline
-    dist_steps = distribution(graph_replay if mode == "hipgraph" else run, min(max(args.steps, 20), 200))
+    dist_steps = distribution(graph_replay if mode == "hipgraph" else run, min(max(args.steps, 100), 200))
     dist_steps["mode"] = mode
     practical = d2d_gbs(dev)
     value = frames / elapsed
