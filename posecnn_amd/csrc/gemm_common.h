@@ -58,6 +58,13 @@ __device__ __forceinline__ float drop_epi(float v, const GemmArgs& g, int m, int
   return v;
 }
 
+// Whether the GEMM epilogue of a whole-tile plan already applied 1 / keep
+// (x_epilogue, 128-row tiles, no forward drop mask): then k_gemm_reduce has
+// nothing left to do for S == 1.
+__host__ __device__ __forceinline__ bool keep_in_epilogue(const GemmArgs& g) {
+  return g.prec != 0 && g.tile == 128 && g.drop == nullptr;
+}
+
 __device__ __forceinline__ int eff_dim(int full, const int32_t* dev) {
   if (!dev) return full;
   int v = *dev;
@@ -97,7 +104,7 @@ __host__ __device__ __forceinline__ int tile_x3(int M, int N, int K) {
 //  evenly over workgroup pairs, partial tiles fixed up in fixed order by the
 //  last segment to finish): fc6 dX 295 -> 343 us — the slab round trip and
 //  the per-segment fix-up cost more than the balance gains.
-constexpr int kMaxSplitX = 16;   // split-K slices
+constexpr int kMaxSplitX = 32;   // split-K slices
 struct XPlan {
   int mt, nt, ns, Tm, tiles, mode, S;
   bool m_fast;  // tile order: the dimension with fewer tiles runs fastest (its
@@ -248,6 +255,10 @@ __device__ __forceinline__ void x_epilogue(const GemmArgs& g, const XPlan& pl, c
         float v = acc[i][j][q] + bv;
         if (g.act == 1) v = v > 0.f ? v : 0.f;
         if (msk && !(mv[gi & 1][q] > 0.f)) v = 0.f;
+        // 128-row tiles: the backward's 1 / keep_prob (no drop mask) applied
+        // here rather than by an in-place reduce pass (keep_in_epilogue)
+        if constexpr (T == 128)
+          if (!g.drop && g.keep != 1.f) v = v / g.keep;
 #ifdef PCNN_ABL_NOEPI
         if (v != 1.2345e-30f) continue;
 #endif

@@ -584,8 +584,9 @@ __global__ void __launch_bounds__(256) k_gemm_reduce(GemmArgs g) {
   auto dropv = [&](float v, int m, int n) { return g.drop_gen ? drop_gen_epi(v, g, step, m, n) : drop_epi(v, g, m, n); };
   if (S == 1) {
     // whole tiles: the GEMM's own epilogue wrote bias / act / mask; dropout
-    // (or the backward's 1 / keep) is applied here, in place
-    if (!dr) return;
+    // (or the backward's 1 / keep) is applied here, in place -- unless the
+    // 128-tile epilogue already scaled by 1 / keep
+    if (!dr || keep_in_epilogue(g)) return;
     const long total = (long)Meff * g.N;
     for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
       const int m = (int)(i / g.N), n = (int)(i % g.N);
@@ -860,7 +861,8 @@ static int gemm_impl(int M, int N, int K, const float* A, const float* A2, int l
     // split-K slab reduction when the plan can split (a no-op launch is not
     // free: queued behind a persistent GEMM on another stream it holds back
     // everything after it on its own stream)
-    if (may_split || drop || keep_prob != 1.f) hipLaunchKernelGGL(k_gemm_reduce, dim3(1024), dim3(256), 0, st, g);
+    if (may_split || drop || (keep_prob != 1.f && !keep_in_epilogue(g)))
+      hipLaunchKernelGGL(k_gemm_reduce, dim3(1024), dim3(256), 0, st, g);
     PCNN_CHECK_LAUNCH();
     return PCNN_OK;
   }
