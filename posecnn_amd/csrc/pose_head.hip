@@ -803,7 +803,11 @@ static int gemm_impl(int M, int N, int K, const float* A, const float* A2, int l
     const int max_grid = x3_max_grid(T);
     long grid = max_grid;
     bool may_split = true, gen = true;
-    if (!M_dev) {
+    if (M_dev) {
+      // device-side M: the fewest tiles (M = 1) give the largest split; if even
+      // that plan runs whole tiles, no effective M splits (fc8 dX, K = 88)
+      may_split = x_plan(1, N, K, T, max_grid, split_bk(precision)).mode == 1;
+    } else {
       // static M: if the plan runs whole tiles (a device-side K can only lower
       // the split), use the fewest workgroups that keep the same number of
       // rounds (fc6 dW: 1568 tiles -> 224 workgroups x 7): the makespan is
