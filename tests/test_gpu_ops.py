@@ -278,6 +278,79 @@ def test_add_loss_symmetric_large(hip, orc, P, near):
     np.testing.assert_allclose(diff.cpu().numpy(), od, rtol=1e-4, atol=1e-6 * np.abs(od).max())
 
 
+def _add_s_f64(pred, target, weight, pts, margin):
+    """ADD-S loss and bottom_diff in float64 from fp32 first-minimum picks: the
+    nearest GT-rotated point by the reference's fp32 expression (numpy does not
+    contract, so these are the oracle's picks), then the per-point terms of
+    cu.cc:174-203 summed in float64 -- a reference free of the fp32 sums'
+    order, so a single different pick shows up far above its tolerance."""
+    R, PC = pred.shape
+    P = pts.shape[1]
+    loss = 0.0
+    diff = np.zeros((R, PC))
+
+    def rot(q):
+        s, u, v, w = q
+        return np.array([[s * s + u * u - v * v - w * w, 2 * (u * v - s * w), 2 * (u * w + s * v)],
+                         [2 * (u * v + s * w), s * s - u * u + v * v - w * w, 2 * (v * w - s * u)],
+                         [2 * (u * w - s * v), 2 * (v * w + s * u), s * s - u * u - v * v + w * w]], np.float32)
+    for r in range(R):
+        cls = np.flatnonzero(weight[r, 0::4] > 0)
+        if len(cls) == 0:
+            continue
+        c = cls[0]
+        s, u, v, w = (float(x) for x in pred[r, 4 * c:4 * c + 4])
+        X = pts[c]
+        Rp, Rg = rot(pred[r, 4 * c:4 * c + 4]), rot(target[r, 4 * c:4 * c + 4])
+        q = np.stack([Rp[i, 0] * X[:, 0] + Rp[i, 1] * X[:, 1] + Rp[i, 2] * X[:, 2] for i in range(3)], 1)
+        g = np.stack([Rg[i, 0] * X[:, 0] + Rg[i, 1] * X[:, 1] + Rg[i, 2] * X[:, 2] for i in range(3)], 1)
+        e = [q[:, None, i] - g[None, :, i] for i in range(3)]
+        d = e[0] * e[0] + e[1] * e[1] + e[2] * e[2]
+        j = np.argmin(d, 1)
+        dist = d[np.arange(P), j]
+        on = ~(dist < margin)
+        loss += np.sum((dist[on].astype(np.float64) - margin) / (2.0 * R * P))
+        df = (q - g[j]).astype(np.float64)[on]
+        Xo = X.astype(np.float64)[on]
+        D = [np.array(m, np.float64).reshape(3, 3) for m in (
+            [2 * s, -2 * w, 2 * v, 2 * w, 2 * s, -2 * u, -2 * v, 2 * u, 2 * s],
+            [2 * u, 2 * v, 2 * w, 2 * v, -2 * u, -2 * s, 2 * w, 2 * s, -2 * u],
+            [-2 * v, 2 * u, 2 * s, 2 * u, 2 * v, 2 * w, -2 * s, 2 * w, -2 * v],
+            [-2 * w, -2 * s, 2 * u, 2 * s, -2 * w, 2 * v, 2 * u, 2 * v, 2 * w])]
+        for i in range(4):
+            diff[r, 4 * c + i] = np.einsum("na,ab,nb->", df, D[i], Xo) / (R * P)
+    return loss, diff
+
+
+@pytest.mark.parametrize("scale", [1e-3, 0.05, 3.0])
+def test_add_loss_symmetric_unnormalised(hip, orc, scale):
+    """ADD-S on unnormalised predicted quaternions -- the random-init head's outputs: query
+    points shrunk towards the origin (|q|^2 = 1e-6 .. 2.5e-3) or spread past
+    the candidates (|q|^2 ~ 9) -- and on the LOV models of the two symmetric
+    classes.  Against the oracle (whose sequential fp32 sums of R P nearly
+    equal terms drift by ~1e-5 when the queries collapse: rtol 1e-4) and
+    against a float64 evaluation of the oracle's picks (rtol 2e-6)."""
+    rng = np.random.default_rng(int(scale * 1000) + 5)
+    pts, sym = synth.rescaled_points(22)
+    R, C = 24, 22
+    pred = (rng.normal(size=(R, 4 * C)) * scale).astype(np.float32)
+    target = np.zeros((R, 4 * C), np.float32)
+    weight = np.zeros((R, 4 * C), np.float32)
+    for r in range(R):
+        c = (16, 21)[r % 2]
+        q = rng.normal(size=4)
+        target[r, 4 * c:4 * c + 4] = q / np.linalg.norm(q)
+        weight[r, 4 * c:4 * c + 4] = 1
+    loss, diff = adl.average_distance_loss(T(pred), T(target), T(weight), T(pts), T(sym), 0.01)
+    loss, diff = loss.cpu().numpy(), diff.cpu().numpy()
+    ol, od, _ = orc.average_distance_loss(pred, target, weight, pts, sym, 0.01)
+    np.testing.assert_allclose(loss, ol, rtol=1e-4)
+    np.testing.assert_allclose(diff, od, rtol=1e-4, atol=1e-6 * np.abs(od).max())
+    l64, d64 = _add_s_f64(pred, target, weight, pts, 0.01)
+    np.testing.assert_allclose(loss[0], l64, rtol=2e-6)
+    np.testing.assert_allclose(diff, d64, rtol=2e-5, atol=1e-6 * np.abs(d64).max())
+
+
 @pytest.mark.parametrize("Ch,NC,ks", [(16, 5, 1), (12, 8, 1), (64, 16, 2), (20, 4, 0), (8, 8, 3)])
 def test_backproject(hip, orc, Ch, NC, ks):
     """Scalar kernels (NC = 5) and the float4 vector forms (lanes per row 4 /
