@@ -346,10 +346,18 @@ def main():
             if roof_vote is not None and "hough_voting_gpu op" in wl:
                 hop = wl["hough_voting_gpu op"]
                 roof_vote["traffic"] = round(hop["traffic_bytes"])
-                roof_vote["traffic_unit"] = "bytes/launch (rocprofv3 2*FETCH_SIZE + WRITE_SIZE)"
+                roof_vote["traffic_unit"] = "bytes/launch (rocprofv3 2*FETCH_SIZE + WRITE_SIZE, every op kernel)"
+                roof_vote["traffic_kernels"] = hop.get("kernels")
+                # the op's real HBM rate: counter bytes over the op's measured time, against the
+                # spec peak (`frac` above is SURVEY 8(d)'s contract-byte metric)
+                cnt_gbs = hop["traffic_bytes"] / t_vote / 1e9
+                roof_vote["achieved_counters"] = round(cnt_gbs, 1)
+                roof_vote["hbm_frac_counters"] = round(cnt_gbs / HBM_PEAK_GBS, 4)
                 if "valu_busy_pct" in hop:  # the voting limiter is VALU / LDS, not HBM
                     roof_vote["valu_busy_pct"] = hop["valu_busy_pct"]
-                    roof_vote["valu_busy_vote_kernel_pct"] = wl.get("k_hough_vote", {}).get("valu_busy_pct")
+                    # the trace key carries the template arguments (k_hough_vote<4, 512>)
+                    vk = [v for k, v in wl.items() if k.split("<", 1)[0] == "k_hough_vote"]
+                    roof_vote["valu_busy_vote_kernel_pct"] = vk[0].get("valu_busy_pct") if vk else None
         except Exception as e:  # pragma: no cover - a stale file must not break the bench
             log(f"pmc traffic unavailable: {e}")
 
@@ -534,21 +542,30 @@ def cpu_baseline(fr, train, budget_s):
         oracle.ransac_hough(fr["label"][:1], vert[:1], fr["extents"], fr["meta"][:1], int(train), nt)  # warm-up
         n, t0 = 0, time.perf_counter()
         while True:
-            for i in range(B):
-                oracle.ransac_hough(fr["label"][i:i + 1], vert[i:i + 1], fr["extents"], fr["meta"][i:i + 1],
-                                    int(train), nt)
-                n += 1
-            if time.perf_counter() - t0 > budget or n >= 400:
+            i = n % B
+            oracle.ransac_hough(fr["label"][i:i + 1], vert[i:i + 1], fr["extents"], fr["meta"][i:i + 1],
+                                int(train), nt)
+            n += 1
+            if (time.perf_counter() - t0 > budget and n >= B) or n >= 400:
                 break
         return n, n / (time.perf_counter() - t0)
 
     allow = cpu["allowance_threads"]
     counts = sorted({c for c in (1, 2, 4, 8, 16, 32, 64, 128, 256) if c <= allow} | {min(threads, allow), allow})
-    per = max(1.0, budget_s / len(counts))
+    # three interleaved sweeps (1, 2, 4, ..., then again): each thread count's
+    # rate is the median of its three samples, so one busy moment of the host's
+    # other tenants moves one sample, not the value
+    n_sweeps = 3
+    per = max(0.7, budget_s / (len(counts) * n_sweeps))
+    samples = {c: [] for c in counts}
+    for _ in range(n_sweeps):
+        for c in counts:
+            samples[c].append(rate(c, per))
     sweep = {}
     for c in counts:
-        nc, f = rate(c, per)
-        sweep[c] = {"frames_per_s": round(f, 2), "frames": nc}
+        fs = sorted(f for _, f in samples[c])
+        sweep[c] = {"frames_per_s": round(fs[len(fs) // 2], 2), "samples_frames_per_s": [round(f, 2) for f in fs],
+                    "frames": sum(n for n, _ in samples[c])}
     best = max(sweep, key=lambda c: sweep[c]["frames_per_s"])
     fps, n = sweep[best]["frames_per_s"], sweep[best]["frames"]
     return {"value": round(fps, 2), "unit": "frames/s", "cores": best, "kind": "port",
@@ -556,10 +573,11 @@ def cpu_baseline(fr, train, budget_s):
                               "frames": sweep[1]["frames"]},
             "thread_sweep": {str(c): v for c, v in sweep.items()},
             "host": cpu,
-            "sample": f"{n} frames ({B} distinct synthetic 640x480 frames cycled) at the best of a thread sweep "
-                      f"{counts} within the process's allowance of {allow} threads, reference Houghvoting op "
+            "sample": f"{n} frames ({B} distinct synthetic 640x480 frames cycled) at the best thread count of "
+                      f"{counts} within the process's allowance of {allow} threads, each count's rate the median "
+                      f"of {n_sweeps} interleaved sweeps of about {per:.1f} s per point; reference Houghvoting op "
                       f"(preemptive RANSAC, {'train' if train else 'test'} mode) restated in oracle/orc_ransac.cpp "
-                      f"(OpenMP), about {per:.0f} s per point"}
+                      f"(OpenMP)"}
 
 
 if __name__ == "__main__":

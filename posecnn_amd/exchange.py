@@ -51,7 +51,11 @@ class RoiExchange:
                          d.all_gather_into_tensor(self.g_rows, self.l_rows, async_op=True)]
 
     def finish(self):
-        """Join the all-gathers and compact the live rows rank-major on the device."""
+        """Join the all-gathers and compact the live rows rank-major on the device.
+
+        The returned tensors are views of this exchange's own buffers, valid
+        until its next start() / gather(): a caller that keeps a step's rows
+        clones them (PoseStep.step stores clones in `detections`)."""
         for w in self._pending:
             if w is not None:
                 w.wait()

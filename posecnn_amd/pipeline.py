@@ -107,6 +107,7 @@ class PoseStep:
         self._drop_external = False
         self.drop_in_reduce = drop_in_reduce  # keep bits drawn in the fc6 / fc7 reduce epilogues
         self._bump_drop_step = False
+        self._drawn = False  # this step's keep masks drawn by draw_drop_masks() (mask-kernel mode)
         if self.keep < 1.0:
             u8 = dict(dtype=torch.uint8, device=device)
             self.drop6 = torch.zeros((CAP, units), **u8)
@@ -193,6 +194,7 @@ class PoseStep:
         (pcnn_gemm_drop_gen) and store them for the backward."""
         if self.keep >= 1.0 or self._drop_external or self.drop_in_reduce:
             return
+        self._drawn = True
         nr = self.hough["num_rois"][1:2]
         side = self.side_stream if self.timer is None and self.side_prep else None
         if side is not None:
@@ -249,6 +251,9 @@ class PoseStep:
         if gs is not None:  # fc6 input column blocks to their owners (overlaps the forward)
             gs.send_input("w6", x)
         dk = dict(keep_prob=self.keep) if self.keep < 1.0 else {}
+        if not self._drawn:  # forward() on its own in mask-kernel mode: this pass's masks (a no-op otherwise)
+            self.draw_drop_masks()
+        self._drawn = False
         if self.keep < 1.0 and getattr(self, "_drop_ready", None) is not None:
             torch.cuda.current_stream().wait_event(self._drop_ready)  # this step's keep masks (side stream)
             self._drop_ready = None
@@ -387,5 +392,8 @@ class PoseStep:
             self._in_step = False
         self._wait("loss")
         if self.dist is not None:
-            self.detections = self.xchg.finish()
+            # clones: the exchange reuses its buffers on the next step and on
+            # gather_detections(), so a kept step's rows must not alias them
+            rows, total = self.xchg.finish()
+            self.detections = (rows.clone(), total.clone())
         return loss

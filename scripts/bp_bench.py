@@ -23,6 +23,8 @@ from posecnn_amd.backprojecting_layer import backprojecting_op as bpo
 ap = argparse.ArgumentParser()
 ap.add_argument("--iters", type=int, default=50)
 ap.add_argument("--batch", type=int, default=8)
+ap.add_argument("--scene", choices=["scene", "objects", "both"], default="both",
+                help="one scene only (the rocprofv3 --pmc passes of scripts/bp_pmc.py take one scene per run)")
 a = ap.parse_args()
 B, H, W, C, G, CH = a.batch, 480, 640, 16, 64, 64
 dev = torch.device("cuda")
@@ -32,6 +34,8 @@ voxel = ([1.2 / G, 0.9 / G, 1.2 / G], [-0.6, -0.45, 0.9])  # as bench.py --workl
 # feature-averaging gather runs; "objects": depth only on the objects (holes
 # elsewhere) -- nearly every voxel misses, the forward is a store stream
 SCENES = {"scene": (1.0, 2.0), "objects": None}
+if a.scene != "both":
+    SCENES = {a.scene: SCENES[a.scene]}
 frames = {k: synth.make_frames(B, H, W, num_classes=C, objects_per_image=4, seed=5,
                                extents=synth.models()["linemod_extents"], with_depth=True, voxel=voxel,
                                depth_background=v) for k, v in SCENES.items()}
@@ -73,10 +77,19 @@ for name, fr in frames.items():
     # the window passes the depth test)
     gather = hit * nvox * 9 * (CH + C + 1) * 4
     fwd_bytes = nvox * (2 * CH + C) * 4 + (1 - hit) * nvox * C * 4 + gather
-    bwd_bytes = B * H * W * CH * 4 * (1 + ingrid)
-    res[name] = {"fwd_us": round(fwd, 1), "fwd_TBps_written+label3d+gather": round(fwd_bytes / fwd / 1e6, 3),
+    # backward: bottom_diff written (B H W Ch 4, the HBM floor) + one top_diff
+    # row per in-grid pixel.  Pixels that map to one voxel re-read its row,
+    # mostly from L2, so the row term over-counts HBM reads: this is an
+    # algorithmic-bytes rate, not an HBM rate (scripts/bp_pmc.py adds the
+    # rocprofv3 counter bytes and their rate beside it).
+    bwd_write = B * H * W * CH * 4
+    bwd_bytes = bwd_write * (1 + ingrid)
+    res[name] = {"fwd_us": round(fwd, 1), "fwd_algorithmic_bytes": round(fwd_bytes),
+                 "fwd_algorithmic_TBps": round(fwd_bytes / fwd / 1e6, 3),
                  "fwd_gather_bytes_upper": round(gather), "bwd_us": round(bwd, 1),
-                 "bwd_TBps_rw": round(bwd_bytes / bwd / 1e6, 3), "hit_fraction": round(hit, 4),
+                 "bwd_algorithmic_bytes": round(bwd_bytes),
+                 "bwd_algorithmic_TBps": round(bwd_bytes / bwd / 1e6, 3),
+                 "bwd_write_TBps": round(bwd_write / bwd / 1e6, 3), "hit_fraction": round(hit, 4),
                  "hit_voxels": int(round(hit * nvox)), "bwd_ingrid_fraction": round(ingrid, 4),
                  "depth": "objects over a floor plane 1.0 -> 2.0 m" if SCENES[name] else "objects only (holes)"}
 print(json.dumps({"B": B, "G": G, "Ch": CH, "NC": C, **res}))

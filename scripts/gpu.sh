@@ -13,6 +13,7 @@
 #   micro NAME          scripts/NAME.py microbench (gemm_bench, roi_bench, hough_bench, label_bench, pcie_rate)
 #   microab NAME V1,... alternating scripts/NAME.py $MICRO_ARGS runs of the tree vs scratch/V.so (two rounds)
 #   sqmicro NAME ARGS V1,...  the two SQ counter passes over scripts/NAME.py ARGS, tree and each scratch/V.so
+#   bppmc               back-projection bench + FETCH / WRITE passes -> bp_bench_pmc.json (scripts/bp_pmc.py)
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 O=$R/gpurun_out
 mkdir -p $O
@@ -28,7 +29,7 @@ while [ $# -gt 0 ]; do
   case $task in
     test)
       args=(tests)
-      if [ $# -gt 0 ] && [[ $1 != test && $1 != smoke && $1 != bench && $1 != prof && $1 != pmc && $1 != sq && $1 != ab && $1 != micro && $1 != microab && $1 != sqmicro ]]; then
+      if [ $# -gt 0 ] && [[ $1 != test && $1 != smoke && $1 != bench && $1 != prof && $1 != pmc && $1 != sq && $1 != ab && $1 != micro && $1 != microab && $1 != sqmicro && $1 != bppmc ]]; then
         args=($1); shift
       fi
       timeout -k 10 900 python -u -m pytest "${args[@]}" -m gpu -x -v --timeout 120 --timeout-method thread \
@@ -88,6 +89,16 @@ while [ $# -gt 0 ]; do
              -d $O/sq_${v}_$pass -o run -- python3 $R/scripts/$n.py $margs > $O/sq_${v}_$pass.log 2>&1) || exit 1
         done
       done ;;
+    bppmc)  # back-projection bench + its rocprofv3 FETCH / WRITE passes per scene -> bp_bench_pmc.json
+      timeout -k 10 300 python scripts/bp_bench.py > $O/bp_bench.json 2> $O/bp_bench.err || exit 1
+      for sc in scene objects; do
+        for c in FETCH_SIZE WRITE_SIZE; do
+          n=fetch; [ $c = WRITE_SIZE ] && n=write
+          (cd /tmp && timeout -s KILL 180 rocprofv3 --pmc $c --kernel-trace --output-format csv -d $O/bp_${sc}_$n \
+             -o run -- python3 $R/scripts/bp_bench.py --scene $sc --iters 5 > $O/bp_${sc}_$n.log 2>&1) || exit 1
+        done
+      done
+      python scripts/bp_pmc.py $O $O/bp_bench.json > $O/bp_bench_pmc.json || exit 1 ;;
     micro)
       n=$1; shift
       timeout -k 10 300 python scripts/$n.py > $O/$n.log 2>&1 || exit 1 ;;

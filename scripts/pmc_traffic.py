@@ -31,6 +31,18 @@ HOUGH = ("k_label_hist", "k_label_place", "k_voter_setup", "k_hough_vote", "k_ho
          "k_hough_emit", "k_hough_nms_cand", "k_hough_cand_data", "k_hough_nms_select")
 
 
+def base(name):
+    """Kernel name without its template arguments: the trace key of the vote
+    is e.g. `k_hough_vote<4, 512>`, which must count as `k_hough_vote`."""
+    return name.split("<", 1)[0]
+
+
+def hough_keys(d):
+    """The keys of d that are Hough-op kernels, matched on the base name (every
+    template instantiation counts)."""
+    return sorted(k for k in d if base(k) in HOUGH)
+
+
 def short(name):
     m = re.search(r"(k_\w+(?:<[^>]*>)?)", name)
     return m.group(1) if m else name.split("(")[0]
@@ -63,7 +75,7 @@ def summarize(fetch_csv, write_csv):
                   "dispatches": len(fv)}
     for v in out.values():
         v["traffic_bytes"] = v["read_bytes"] + v["write_bytes"]
-    hk = [k for k in HOUGH if k in out]
+    hk = hough_keys(out)
     if hk:
         out["hough_voting_gpu op"] = {"traffic_bytes": sum(out[k]["traffic_bytes"] for k in hk),
                                       "kernels": hk}
@@ -83,7 +95,7 @@ def valu_busy(path):
         per[k].append(float(row["Counter_Value"]))
         dur[k].append(int(row["End_Timestamp"]) - int(row["Start_Timestamp"]))
     out = {k: sum(v) / len(v) for k, v in per.items()}
-    hk = [k for k in HOUGH if k in out]
+    hk = hough_keys(out)
     if hk:
         tot = sum(sum(dur[k]) / len(dur[k]) for k in hk)
         out["hough_voting_gpu op"] = sum(out[k] * sum(dur[k]) / len(dur[k]) for k in hk) / tot

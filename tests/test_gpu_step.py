@@ -141,3 +141,33 @@ def test_step_side_prep_placement_is_bitwise_neutral(hip):
         for a, b in zip(a_step, b_step):
             assert torch.equal(a, b)
     assert not torch.equal(outs[0][0][1], outs[0][1][1])  # the second step drew new masks
+
+
+def test_forward_alone_draws_masks_in_mask_kernel_mode(hip):
+    """with drop_in_reduce=False the keep masks come from
+    draw_drop_masks(); forward() called on its own (after a vote, without
+    step()) must draw this pass's masks itself rather than use the zeroed
+    buffers (every unit dropped) or the previous pass's masks."""
+    fr = synth.make_frames(B, H=H, W=W, num_classes=C, objects_per_image=4, seed=93)
+    g = torch.Generator().manual_seed(6)
+    conv4 = torch.randn((B, H // 8, W // 8, CH), generator=g).to(D)
+    conv5 = torch.randn((B, H // 16, W // 16, CH), generator=g).to(D)
+    pts, sym = synth.rescaled_points(C)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(D)
+    step = PoseStep(B, H, W, C, D, channels=CH, units=UNITS, is_train=1, skip_pixels=3, drop_in_reduce=False,
+                    backward=False)
+    assert step.keep == 0.5
+    step.vote(t(fr["label"]), t(fr["vertex"]), t(fr["extents"]), t(fr["meta"]), t(fr["gt"]))
+    drawn = []
+    for _ in range(2):
+        step.forward(conv4, conv5, t(pts), t(sym))
+        torch.cuda.synchronize()
+        n = int(step.hough["num_rois"][1].item())
+        m6 = step.drop6[:n].double()
+        assert abs(float(m6.mean()) - 0.5) < 0.03  # drawn (zeroed buffers would read 0)
+        x = step.pool[:n].reshape(n, -1).double()
+        w = step.weights
+        y6 = torch.relu(x @ w.w6.double() + w.b6.double()) / 0.5 * m6
+        _close(step.y6[:n].cpu().numpy(), y6.cpu().numpy())
+        drawn.append(step.drop6[:n].clone())
+    assert not torch.equal(drawn[0], drawn[1])  # each forward pass draws its own masks
