@@ -96,7 +96,12 @@ int pcnn_hough_voting_grad(float* grad_label, float* grad_vertex, int B, int H, 
 /* Diagnostic counters of the last pcnn_hough_voting call on `workspace`:
  * copies [0] = count mismatches between the interval vote and the exact
  * per-voter re-check at emitted maxima (must be 0), [1] = NMS candidate
- * overflows, [2..3] reserved. Synchronous (reads device memory). */
+ * overflows, [2] = RoI rows past the output capacity, [3] = maxima whose
+ * distance sum took the one-lane serial chain (hough_peak.hip: the in-order
+ * fp32 sum is rebuilt in parallel and verified; the serial chain is the
+ * fallback when a verification fails; same bits either way).  Synchronous
+ * (reads device memory).  The environment variable PCNN_HOUGH_SUM=serial
+ * forces the serial chain for every maximum (A/B and test knob). */
 int pcnn_hough_voting_diag(const void* workspace, int B, int H, int W, int C, int skip_pixels, float vote_thr,
                            int32_t* diag_host4, void* stream);
 

@@ -381,10 +381,10 @@ __global__ void k_hough_peak(int B, int H, int W, int C, float inlier, const flo
                              const float* __restrict__ gt, int num_gt, float* __restrict__ top_box,
                              float* __restrict__ top_pose, float* __restrict__ top_target,
                              float* __restrict__ top_weight, int32_t* __restrict__ top_domain,
-                             int32_t* __restrict__ num_rois, int cap);
+                             int32_t* __restrict__ num_rois, int cap, int psum);
 __global__ void k_hough_nms_cand(int H, int W, int C, float vote_thr, HoughWs ws);
 __global__ void k_hough_cand_data(int H, int W, int C, float inlier, const float* __restrict__ extents,
-                                  const float* __restrict__ meta, int num_meta, HoughWs ws);
+                                  const float* __restrict__ meta, int num_meta, HoughWs ws, int psum);
 __global__ void k_hough_nms_select(int H, int W, int C, float per_thr, int index_size, HoughWs ws);
 
 }  // namespace pcnn_hough

@@ -12,6 +12,8 @@
 //                      ascending slot / flat order, capacity-sized outputs and a
 //                      device-side row count (+ dummy row, hough_voting_gpu_op.cc:382-383)
 #include "hough_common.h"
+#include <stdlib.h>
+#include <string.h>
 #include <algorithm>
 #include <cmath>
 
@@ -92,6 +94,12 @@ static int hough_voting_impl(const int32_t* label, const float* prob, int32_t* l
   hipStream_t st = (hipStream_t)stream;
   const int index_size = PCNN_MAX_ROI / global_batch;  // cu.cc:734
   const int HW = H * W;
+  // Sigma d at the maxima (hough_peak.hip): the in-order fp32 sum rebuilt in
+  // parallel (default), or the one-lane serial chain everywhere when the
+  // environment sets PCNN_HOUGH_SUM=serial (a test / A-B knob; both give the
+  // same bits)
+  const char* sum_mode = getenv("PCNN_HOUGH_SUM");
+  const int psum = (sum_mode && strcmp(sum_mode, "serial") == 0) ? 0 : 1;
 
   if (label) {
     hipLaunchKernelGGL(k_label_hist, dim3(ws.nblk, B), dim3(kCompactThreads), 0, st, label, HW, C, H, ws);
@@ -126,12 +134,12 @@ static int hough_voting_impl(const int32_t* label, const float* prob, int32_t* l
     if (!nms) {
       hipLaunchKernelGGL(k_hough_peak, dim3(slots, B), dim3(kPeakThreads), 0, st, B, H, W, C, inlier_thr, extents,
                          meta, num_meta, ws, is_train, batch_base, gt, num_gt, top_box, top_pose, top_target,
-                         top_weight, top_domain, num_rois, cap);
+                         top_weight, top_domain, num_rois, cap, psum);
     } else {
       hipLaunchKernelGGL(k_hough_nms_cand, dim3((HW + 255) / 256 < 64 ? (HW + 255) / 256 : 64, C - 1, B),
                          dim3(256), 0, st, H, W, C, vote_thr, ws);
       hipLaunchKernelGGL(k_hough_cand_data, dim3(128, B), dim3(kPeakThreads), 0, st, H, W, C, inlier_thr, extents,
-                         meta, num_meta, ws);
+                         meta, num_meta, ws, psum);
       hipLaunchKernelGGL(k_hough_nms_select, dim3(B), dim3(1024), 0, st, H, W, C, per_thr, index_size, ws);
       if (debug_counts &&
           hipMemcpyAsync(debug_counts, ws.counts, (size_t)B * (C - 1) * HW * sizeof(int32_t),

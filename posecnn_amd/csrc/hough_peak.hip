@@ -135,6 +135,324 @@ __device__ PeakOut exact_cell(int cx, int cy, int cls, float count_f, const floa
   return o;
 }
 
+// ---------------------------------------------------------------------------
+// The same cell, with the reference's in-order fp32 sum (cu.cc:269-291)
+// computed in parallel and bit for bit (round 5).  The serial chain
+// s_k = fl(s_{k-1} + d_k) over the voting voters is one dependent add per
+// term; here every thread holds a contiguous run of the voters in registers
+// and the chain is rebuilt from three facts about fp32 addition of a
+// non-negative term to a non-negative running sum:
+//  - while s stays in one binade [2^E, 2^(E+1)), s is an integer S times
+//    u = 2^(E-23) and fl(s + d) = (S + r) u, where r = round(d / u) to nearest
+//    and, on an exact half, r is chosen so that S + r is even: r depends on S
+//    only through its parity.  A term is a two-entry "transducer" (the
+//    increment for S even / odd), and transducers compose associatively, so
+//    a run of terms in one binade is one block scan;
+//  - the binade of every partial sum is predicted from the exact prefix sums
+//    (double); each term where the predicted binade changes (a crossing, and
+//    the first term) is an event, added by one lane with the real fp32 add
+//    from the exact running sum, so its rounding is the reference's;
+//  - every prediction is then verified: each in-binade term must keep
+//    S in [2^23, 2^24) and each event must land in the binade predicted for
+//    the run that follows it.  If all hold, the partial sums are the serial
+//    ones by induction; if one fails (a prefix within rounding of a power of
+//    two, a non-finite term, more than kPsumEvents events or more than
+//    kPsumPer voters per thread), the caller falls back to exact_cell's
+//    serial chain.  The bb pass then uses the cached cone flags and |dx|,
+//    |dy| (no second read of the voters).
+// diag[3] counts the maxima that took that fallback.
+constexpr int kPsumPer = 24;      // voters per thread held in registers (nv <= kPsumPer * kPeakThreads)
+constexpr int kPsumEvents = 256;  // crossing events per cell
+
+struct PsumTr {  // running-sum transducer: increment for S even / odd; has = the run starts at an event
+  int i0, i1, has;
+};
+__device__ __forceinline__ PsumTr psum_id() { return PsumTr{0, 0, 0}; }
+// a then b
+__device__ __forceinline__ PsumTr psum_cat(const PsumTr& a, const PsumTr& b) {
+  if (b.has) return b;
+  PsumTr c;
+  c.i0 = a.i0 + (((a.i0) & 1) ? b.i1 : b.i0);
+  c.i1 = a.i1 + (((1 + a.i1) & 1) ? b.i1 : b.i0);
+  c.has = a.has;
+  return c;
+}
+// the transducer of adding q = d / u (exact) to an integer S (no binade change)
+__device__ __forceinline__ PsumTr psum_term(float q) {
+  const float fl = floorf(q), fr = q - fl;
+  const int f = (int)fl;
+  PsumTr t;
+  t.has = 0;
+  if (fr > 0.5f) {
+    t.i0 = t.i1 = f + 1;
+  } else if (fr < 0.5f) {
+    t.i0 = t.i1 = f;
+  } else {  // exact half: the even sum
+    t.i0 = f + (f & 1);
+    t.i1 = f + ((f + 1) & 1);
+  }
+  return t;
+}
+__device__ __forceinline__ int f32_binade(float s) {  // E of a positive normal float, -1000 otherwise
+  const unsigned b = __float_as_uint(s);
+  const int e = (int)((b >> 23) & 0xFF);
+  return (e == 0 || e == 255 || (b >> 31)) ? -1000 : e - 127;
+}
+
+struct PsumShared {
+  float ev_d[kPsumEvents];
+  int ev_E[kPsumEvents], ev_i0[kPsumEvents], ev_i1[kPsumEvents], ev_S[kPsumEvents];
+  PsumTr wtr[kPeakThreads / 64];
+  int wcnt[kPeakThreads / 64], wev[kPeakThreads / 64];
+  double wsum[kPeakThreads / 64];
+  int fail, total_cnt, total_ev, bbw, bbh;
+  float dist;
+  PsumTr final_tr;
+};
+
+// Returns true with o filled, or false (block-uniform) when the caller must
+// take exact_cell's serial path.
+__device__ bool exact_cell_par(int cx, int cy, int cls, float count_f, const float4* __restrict__ vd,
+                               const int32_t* __restrict__ vp, int nv, int W, float inlier,
+                               const float* __restrict__ extents, const float* __restrict__ meta, PsumShared& sh,
+                               PeakOut& o) {
+  const int nt = blockDim.x, t = threadIdx.x, lane = pcnn::lane_id(), wave = t >> 6, nw = nt >> 6;
+  const int m = (nv + nt - 1) / nt;
+  if (m > kPsumPer) return false;  // block-uniform
+  const int j0 = t * m;
+  // phase A: the thread's voters -> voting flags, d, and the cone voters' |dx|, |dy|
+  float dd[kPsumPer];
+  unsigned pk[kPsumPer];
+  unsigned vbits = 0;
+  bool bad = false;
+#pragma unroll
+  for (int i = 0; i < kPsumPer; i++) {
+    dd[i] = 0.f;
+    pk[i] = 0xFFFFFFFFu;
+    const int j = j0 + i;
+    if (i < m && j < nv) {
+      const float4 q = vd[j];
+      const int p = vp[j];
+      const int x = p % W, y = p / W;
+      if (cone_pred(cx, cy, x, y, q.x, q.y, inlier)) {
+        const int adx = abs(x - cx), ady = abs(y - cy);
+        pk[i] = (unsigned)adx | ((unsigned)ady << 16);
+        if ((float)adx < q.w && (float)ady < q.w) {  // cu.cc:285-288
+          vbits |= 1u << i;
+          dd[i] = q.z;
+          bad |= !(q.z >= 0.f) || !isfinite(q.z);
+        }
+      }
+    }
+  }
+  // scan 1: voting counts and exact-ish prefix sums (double) -> binade predictions
+  int c = __popc(vbits);
+  double D = 0.0;
+#pragma unroll
+  for (int i = 0; i < kPsumPer; i++) D += (double)dd[i];
+  int ci = c;
+  double Di = D;
+#pragma unroll
+  for (int k = 1; k < 64; k <<= 1) {
+    const int cy_ = __shfl_up(ci, k, 64);
+    const double dy_ = __shfl_up(Di, k, 64);
+    if (lane >= k) { ci += cy_; Di += dy_; }
+  }
+  if (lane == 63) { sh.wcnt[wave] = ci; sh.wsum[wave] = Di; }
+  if (t == 0) sh.fail = 0;
+  __syncthreads();
+  int cbase = ci - c;
+  double Pbase = Di - D;
+  for (int w = 0; w < wave; w++) { cbase += sh.wcnt[w]; Pbase += sh.wsum[w]; }
+  if (t == nt - 1) sh.total_cnt = cbase + c;
+  // phase B: events and the thread's tail transducer (terms after its last event)
+  PsumTr tail = psum_id();
+  int nev = 0;
+  {
+    double P = Pbase;
+    int Eprev = cbase > 0 ? ilogb(Pbase) : -100000;
+#pragma unroll
+    for (int i = 0; i < kPsumPer; i++) {
+      if (vbits & (1u << i)) {
+        P += (double)dd[i];
+        const int E = P > 0.0 ? ilogb(P) : -100000;
+        if (E != Eprev) {  // first term or a predicted crossing: an event
+          nev++;
+          tail = PsumTr{0, 0, 1};
+        } else {
+          const float q = ldexpf(dd[i], 23 - E);
+          bad |= !(q < 8388608.f);
+          tail = psum_cat(tail, psum_term(q));
+        }
+        Eprev = E;
+      }
+    }
+  }
+  // scan 2: event counts and the segmented transducer composition
+  PsumTr ti = tail;
+  int ei = nev;
+#pragma unroll
+  for (int k = 1; k < 64; k <<= 1) {
+    PsumTr y;
+    y.i0 = __shfl_up(ti.i0, k, 64);
+    y.i1 = __shfl_up(ti.i1, k, 64);
+    y.has = __shfl_up(ti.has, k, 64);
+    const int ey = __shfl_up(ei, k, 64);
+    if (lane >= k) { ti = psum_cat(y, ti); ei += ey; }
+  }
+  if (lane == 63) { sh.wtr[wave] = ti; sh.wev[wave] = ei; }
+  if (bad) sh.fail = 1;
+  __syncthreads();
+  PsumTr X = psum_id();
+  int ebase = 0;
+  for (int w = 0; w < wave; w++) { X = psum_cat(X, sh.wtr[w]); ebase += sh.wev[w]; }
+  {  // exclusive within the wave
+    PsumTr y;
+    y.i0 = __shfl_up(ti.i0, 1, 64);
+    y.i1 = __shfl_up(ti.i1, 1, 64);
+    y.has = __shfl_up(ti.has, 1, 64);
+    const int ey = __shfl_up(ei, 1, 64);
+    if (lane >= 1) { X = psum_cat(X, y); ebase += ey; }
+  }
+  if (t == nt - 1) {
+    sh.final_tr = psum_cat(X, tail);
+    sh.total_ev = ebase + nev;
+  }
+  // phase C: event records (d, predicted binade, the transducer of the run before it)
+  {
+    PsumTr tr = X;
+    double P = Pbase;
+    int Eprev = cbase > 0 ? ilogb(Pbase) : -100000;
+    int e = ebase;
+#pragma unroll
+    for (int i = 0; i < kPsumPer; i++) {
+      if (vbits & (1u << i)) {
+        P += (double)dd[i];
+        const int E = P > 0.0 ? ilogb(P) : -100000;
+        if (E != Eprev) {
+          if (e < kPsumEvents) {
+            sh.ev_d[e] = dd[i];
+            sh.ev_E[e] = E;
+            sh.ev_i0[e] = tr.i0;
+            sh.ev_i1[e] = tr.i1;
+          }
+          e++;
+          tr = psum_id();
+        } else {
+          tr = psum_cat(tr, psum_term(ldexpf(dd[i], 23 - E)));
+        }
+        Eprev = E;
+      }
+    }
+  }
+  __syncthreads();
+  const int total = sh.total_cnt;
+  o.mismatch = ((float)total != count_f) ? 1 : 0;
+  o.count = count_f;
+  o.distance = 0.f;
+  o.bbh2 = 0.f;
+  o.bbw2 = 0.f;
+  if (!(count_f > 0.f)) return true;  // hough_data stays memset-zero (cu.cc:296, :698-708)
+  if (total == 0 || sh.fail || sh.total_ev > kPsumEvents) return false;
+  // the walk: one lane adds the events with the real fp32 add from the exact running sum
+  if (t == 0) {
+    float s = 0.f;
+    int fail = 0;
+    const int ne = sh.total_ev;
+    for (int e = 0; e < ne && !fail; e++) {
+      if (e > 0) {
+        const int E = sh.ev_E[e - 1];
+        int S = sh.ev_S[e - 1];
+        S += (S & 1) ? sh.ev_i1[e] : sh.ev_i0[e];
+        fail |= !(S >= (1 << 23) && S < (1 << 24));
+        s = ldexpf((float)S, E - 23);
+      }
+      s = s + sh.ev_d[e];  // cu.cc:291, in the reference's order
+      const int E = sh.ev_E[e];
+      fail |= f32_binade(s) != E;
+      sh.ev_S[e] = (int)ldexpf(s, 23 - E);
+    }
+    if (!fail && ne > 0) {
+      const int E = sh.ev_E[ne - 1];
+      int S = sh.ev_S[ne - 1];
+      const PsumTr ft = sh.final_tr;
+      S += (S & 1) ? ft.i1 : ft.i0;
+      fail |= !(S >= (1 << 23) && S < (1 << 24));
+      s = ldexpf((float)S, E - 23);
+    }
+    fail |= ne == 0;
+    sh.fail = fail;
+    sh.dist = s / count_f;  // cu.cc:298
+    sh.bbw = -1;
+    sh.bbh = -1;
+  }
+  __syncthreads();
+  if (sh.fail) return false;
+  // phase D: verify every in-binade term of the thread (S stays in [2^23, 2^24))
+  {
+    bool ok = true;
+    if (c > 0) {
+      int S = 0, E = 0;
+      double P = Pbase;
+      int Eprev = cbase > 0 ? ilogb(Pbase) : -100000;
+      if (cbase > 0 && ebase > 0) {  // the run continues from the last event before this thread
+        S = sh.ev_S[ebase - 1];
+        E = sh.ev_E[ebase - 1];
+        S += (S & 1) ? X.i1 : X.i0;  // X: the terms between that event and this thread
+        ok &= S >= (1 << 23) && S < (1 << 24);
+      } else if (cbase > 0) {
+        ok = false;
+      }
+      int e = ebase;
+#pragma unroll
+      for (int i = 0; i < kPsumPer; i++) {
+        if (vbits & (1u << i)) {
+          P += (double)dd[i];
+          const int Ep = P > 0.0 ? ilogb(P) : -100000;
+          if (Ep != Eprev) {
+            S = sh.ev_S[e];
+            E = sh.ev_E[e];
+            e++;
+          } else {
+            const PsumTr tr = psum_term(ldexpf(dd[i], 23 - E));
+            S += (S & 1) ? tr.i1 : tr.i0;
+            ok &= S >= (1 << 23) && S < (1 << 24);
+          }
+          Eprev = Ep;
+        }
+      }
+    }
+    if (!ok) sh.fail = 1;
+  }
+  __syncthreads();
+  if (sh.fail) return false;
+  // bb extent with T(distance) over the cached cone voters (cu.cc:300-330)
+  const float distance = sh.dist;
+  const float Tm = project_box(cls, extents, meta, distance, 0.6f);  // cu.cc:317
+  int bw = -1, bh = -1;
+#pragma unroll
+  for (int i = 0; i < kPsumPer; i++) {
+    if (pk[i] != 0xFFFFFFFFu) {
+      const int adx = (int)(pk[i] & 0xFFFFu), ady = (int)(pk[i] >> 16);
+      if ((float)adx < Tm && (float)ady < Tm) {
+        bw = max(bw, adx);
+        bh = max(bh, ady);
+      }
+    }
+  }
+  bw = pcnn::wave_max(bw);
+  bh = pcnn::wave_max(bh);
+  if (lane == 0 && bw >= 0) atomicMax(&sh.bbw, bw);
+  if (lane == 0 && bh >= 0) atomicMax(&sh.bbh, bh);
+  __syncthreads();
+  o.distance = distance;
+  o.bbw2 = 2 * (float)sh.bbw;
+  o.bbh2 = 2 * (float)sh.bbh;
+  __syncthreads();  // sh is reused by the caller's next cell
+  (void)nw;
+  return true;
+}
+
 // Default path: one workgroup per (slot, image) = one maximum.  Exact
 // hough_data at the argmax, then the slot's RoI rows (emit_max) at output row
 // (rows of images < b) + slot * rpm: image-major, ascending slot order.
@@ -149,11 +467,12 @@ __global__ void __launch_bounds__(kPeakThreads) k_hough_peak(int B, int H, int W
                                                               float* __restrict__ top_target,
                                                               float* __restrict__ top_weight,
                                                               int32_t* __restrict__ top_domain,
-                                                              int32_t* __restrict__ num_rois, int cap) {
+                                                              int32_t* __restrict__ num_rois, int cap, int psum) {
   __shared__ __attribute__((aligned(16))) float sh_d[kPeakChunk + 4];
   __shared__ float sh_red[2 * (kPeakThreads / 64)];
   __shared__ int s_off[2];
   __shared__ EmitShared esh;
+  __shared__ PsumShared psh;
   const int b = blockIdx.y, slot = blockIdx.x;
   const int rpm = is_train ? 9 : 1;
   if (slot == 0 && b == 0) {  // batch row count: sum over images of nvote * rpm
@@ -181,8 +500,13 @@ __global__ void __launch_bounds__(kPeakThreads) k_hough_peak(int B, int H, int W
   const int vb = ws.vbase[(size_t)b * C + cls];
   const int nv = ws.vcount[(size_t)b * C + cls];
   const float* mb = meta + (size_t)b * num_meta;
-  PeakOut o = exact_cell(cx, cy, cls, (float)cnt, ws.vdat + (size_t)b * ws.vcap + vb,
-                         ws.vpos + (size_t)b * ws.vcap + vb, nv, W, inlier, extents, mb, sh_d, sh_red);
+  const float4* vd = ws.vdat + (size_t)b * ws.vcap + vb;
+  const int32_t* vpp = ws.vpos + (size_t)b * ws.vcap + vb;
+  PeakOut o;
+  if (!(psum && exact_cell_par(cx, cy, cls, (float)cnt, vd, vpp, nv, W, inlier, extents, mb, psh, o))) {
+    o = exact_cell(cx, cy, cls, (float)cnt, vd, vpp, nv, W, inlier, extents, mb, sh_d, sh_red);
+    if (psum && threadIdx.x == 0) atomicAdd(&ws.diag[3], 1);  // took the serial chain
+  }
   if (threadIdx.x == 0) {
     float* pk = ws.peak + ((size_t)b * ws.pks + slot) * 8;
     pk[0] = o.count;
@@ -223,9 +547,10 @@ __global__ void __launch_bounds__(256) k_hough_nms_cand(int H, int W, int C, flo
 __global__ void __launch_bounds__(kPeakThreads) k_hough_cand_data(int H, int W, int C, float inlier,
                                                                    const float* __restrict__ extents,
                                                                    const float* __restrict__ meta, int num_meta,
-                                                                   HoughWs ws) {
+                                                                   HoughWs ws, int psum) {
   __shared__ __attribute__((aligned(16))) float sh_d[kPeakChunk + 4];
   __shared__ float sh_red[2 * (kPeakThreads / 64)];
+  __shared__ PsumShared psh;
   const int b = blockIdx.y;
   const int ncand = min(ws.ncand[b], kCandCap);
   const int HW = H * W;
@@ -236,9 +561,14 @@ __global__ void __launch_bounds__(kPeakThreads) k_hough_cand_data(int H, int W, 
     const int vb = ws.vbase[(size_t)b * C + cls];
     const int nv = ws.vcount[(size_t)b * C + cls];
     const float cnt = (float)ws.counts[((size_t)b * (C - 1) + slot) * (size_t)HW + cell];
-    PeakOut o = exact_cell(cell % W, cell / W, cls, cnt, ws.vdat + (size_t)b * ws.vcap + vb,
-                           ws.vpos + (size_t)b * ws.vcap + vb, nv, W, inlier, extents,
-                           meta + (size_t)b * num_meta, sh_d, sh_red);
+    const float4* vd = ws.vdat + (size_t)b * ws.vcap + vb;
+    const int32_t* vpp = ws.vpos + (size_t)b * ws.vcap + vb;
+    const float* mb = meta + (size_t)b * num_meta;
+    PeakOut o;
+    if (!(psum && exact_cell_par(cell % W, cell / W, cls, cnt, vd, vpp, nv, W, inlier, extents, mb, psh, o))) {
+      o = exact_cell(cell % W, cell / W, cls, cnt, vd, vpp, nv, W, inlier, extents, mb, sh_d, sh_red);
+      if (psum && threadIdx.x == 0) atomicAdd(&ws.diag[3], 1);
+    }
     if (threadIdx.x == 0) {
       float* cd = ws.cand_data + ((size_t)b * kCandCap + q) * 4;
       cd[0] = o.count;
