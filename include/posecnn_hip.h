@@ -327,18 +327,18 @@ int pcnn_philox_check(const uint32_t* ctr, const uint32_t* key, int n, uint32_t*
  * synthesizer.pyx:74-82 estimate_poses_2d, called from lib/fcn/test.py:1364).
  *  label (H,W) int32, vertmap (H,W,3C) object coordinates scaled to [0,1] by the
  *  class extents (getMode3D, :1052-1071), extents (C,3), pinhole fx fy px py.
- *  Preemptive RANSAC: n_hyp (256 in the reference) hypotheses, each from 4
- *  pixels of one object (> 400 pixels) through P3P; attempt a of hypothesis h
- *  draws on its own Philox stream (h, a) of `seed`, h keeps its first accepted
- *  attempt (at most max_iter attempts); 8 rounds of inlier counting (< 10 px)
- *  over the reference's negative-binomial pixel subsets, keeping the better
+ *  Preemptive RANSAC: n_hyp (1..256; 256 = the reference's ransacIterations,
+ *  :1601) hypotheses, each from 4 pixels of one object (> 400 pixels) through
+ *  P3P; attempt a of hypothesis h draws on its own Philox stream (h, a) of
+ *  `seed`, h keeps its first accepted attempt (at most max_iter attempts); 8
+ *  rounds of inlier counting (< 10 px) over pixel subsets with the
+ *  reference's skip law max(1, G), G geometric with p = 1000 r / N (drawn
+ *  from Philox streams (j, class, round) of `seed`), keeping the better
  *  half.  Outputs (device): poses_out (3,4,C) [R | t] per class (the reference's
  *  layout; classes without a hypothesis 0); hyps_out (n_hyp,13) [objID or -1 |
  *  R | t]; hyp_px (n_hyp,4) sampled pixel indices; inl_out (n_hyp,8) inliers per
  *  round (-1: not queued); final_out (C,3) [h, inliers, hypotheses] (-1: none).
- *  Synchronises `stream` (the class sizes decide the objects and the subsets,
- *  drawn on up to 16 host threads with the reference's std::mt19937 /
- *  negative_binomial while the sampling kernels run). */
+ *  Asynchronous on `stream`: object lists and subsets are built on the device. */
 size_t pcnn_pose2d_workspace_size(int H, int W, int C, int n_hyp);
 int pcnn_pose2d(const int32_t* label, const float* vertmap, const float* extents, int H, int W, int C, float fx,
                 float fy, float px, float py, uint64_t seed, int n_hyp, int max_iter, float* poses_out,
@@ -451,6 +451,30 @@ int pcnn_icp_center(const float* live, const int32_t* label, const int32_t* obj_
                     const float* pred_vertices, const float* pred_normals, int H, int W, float max_error,
                     const float* pose_in, float* out, float* pose_out, void* workspace, size_t workspace_bytes,
                     void* stream);
+/* Nelder-Mead on optEnergy on the device (round 5): solveICP's refinePose
+ * search (synthesize.cpp:2221-2250 -> poseWithOpt :2529-2573, NLopt
+ * LN_NELDERMEAD over 7 parameters, optEnergy :2476-2526).
+ *  pcnn_energy_records: for problem i (N), the pixels with label ==
+ *  prob_obj[i] whose live vertex (live (n_live,H,W,3)[prob_live[i]]) has z in
+ *  (znear, zfar), in raster order, as records (rendered vertex
+ *  pred_vertices (N,H,W,4)[i] xyz, live xyz) -> records (N, H*W, 6), counts (N).
+ *  pcnn_energy_rec: optEnergy of K poses (K,7), pose k over problem
+ *  pose_prob[k]'s records (stride = records per problem, H*W).
+ *  pcnn_nelder_mead_energy: N bounded Nelder-Mead searches (x0, lb, ub (N,7)
+ *  float64, at most max_eval evaluations; the operation order of
+ *  posecnn_amd/synthesize/icp.py nelder_mead_steps), one workgroup each, the
+ *  energy of every trial point as pcnn_energy_rec computes it (the same bits)
+ *  -> x_out (N,7), f_out (N) float64, nev_out (N). Asynchronous. */
+size_t pcnn_energy_records_workspace_size(int N, int H, int W);
+int pcnn_energy_records(const float* live, int n_live, const int32_t* label, const float* pred_vertices, int H, int W,
+                        float znear, float zfar, int N, const int32_t* prob_obj, const int32_t* prob_live,
+                        float* records, int32_t* counts, void* workspace, size_t workspace_bytes, void* stream);
+int pcnn_energy_rec(const float* records, const int32_t* counts, int stride, const float* poses,
+                    const int32_t* pose_prob, int K, float znear, float zfar, float* energy, void* stream);
+int pcnn_nelder_mead_energy(const float* records, const int32_t* counts, int stride, int N, const double* x0,
+                            const double* lb, const double* ub, int max_eval, float znear, float zfar, double* x_out,
+                            double* f_out, int32_t* nev_out, void* stream);
+
 /* pcnn_icp_score: the SegICP hypothesis score of solveICP (synthesize.cpp:2288-2330):
  *   over the object's pixels with depth > 0 and a finite vertmap, each model
  *   point (vertmap, class offset dropped) moved by hypothesis j takes its

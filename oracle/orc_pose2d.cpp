@@ -11,8 +11,9 @@
 //   getMode3D (:1052-1071), pointLineDistance (:1074-1080),
 //   samplePoint2D (:1084-1104), hypothesis sampling (:1616-1688),
 //   getBB2D (detection.h:78-109), the preemptive loop (:1693-1727) with
-//   countInliers2D (:1171-1214; std::mt19937 default seed and
-//   std::negative_binomial_distribution<int>(1, maxPixels / N) pixel skips),
+//   countInliers2D (:1171-1214: pixel skips max(1, G), G ~
+//   negative_binomial(1, maxPixels / N), i.e. geometric -- see the RNG
+//   choice below),
 //   getWorkingQueue (:1150-1160), and the output layout (:1729-1764).
 // Deliberate, documented choices (parity unpinned: OpenCV, NLopt absent):
 //   * RNG: attempt a of hypothesis h draws from its own Philox4x32-10 stream
@@ -21,6 +22,16 @@
 //     evaluates a batch of them at once); the
 //     reference's per-thread mt19937 streams (thread_rand.cpp) are assigned
 //     to hypotheses by the OpenMP schedule, i.e. nondeterministically.
+//   * The rounds' pixel subsets: the reference draws G from a default-seeded
+//     std::mt19937 per countInliers2D call (the same subset for every
+//     hypothesis of a round).  Here G_j of round r of class c comes from the
+//     Philox4x32-10 block (j, c, 'SUB0' + r, 0) under key seed: U =
+//     (x 2^21 + (y >> 11) + 0.5) 2^-53 from its first two words and G = the
+//     largest k with U < q^k, q = 1 - p (inverse CDF of the geometric law
+//     on repeated double products, bit-reproducible on the GPU).  Same
+//     distribution; the draws themselves are unpinned (round 5: the host
+//     replay of libstdc++'s negative_binomial pinned nothing, because the
+//     hypotheses already come from Philox streams).
 //   * Hypotheses are stored in ascending h (the reference appends in
 //     completion order under omp critical); the per-round sort is stable
 //     (inliers descending, then h): one legal order of std::sort's ties.
@@ -62,6 +73,20 @@ U4 philox(U4 c, uint32_t k0, uint32_t k1) {
     k1 += 0xBB67AE85u;
   }
   return c;
+}
+
+// max(1, G) of one pixel skip (see the RNG notes above; the GPU's p2d_gap)
+int subset_gap(uint64_t seed, int c, int r, int j, double q) {
+  const U4 b = philox(U4{{(uint32_t)j, (uint32_t)c, 0x53554230u + (uint32_t)r, 0u}}, (uint32_t)seed,
+                      (uint32_t)(seed >> 32));
+  const double U = ((double)b.v[0] * 2097152.0 + (double)(b.v[1] >> 11) + 0.5) * 0x1p-53;
+  int k = 0;
+  double t = q;
+  while (t > U) {
+    k++;
+    t = t * q;
+  }
+  return k > 1 ? k : 1;
 }
 
 struct Stream {
@@ -374,13 +399,12 @@ ORC_API int orc_pose2d(const int* label, const float* vertmap, const float* exte
     const int N = (int)L.size();
     for (int round = 1; round <= 8; round++) {
       const int maxPixels = 1000 * round;
-      const float rate = maxPixels / (float)N;
+      const float rate = maxPixels / (float)N;  // :1191
       std::vector<int> sub;
-      std::mt19937 gen;
-      std::negative_binomial_distribution<int> nb(1, rate < 1 ? rate : 0.5f);
-      for (int i = 0; i < N;) {
+      const double q = 1.0 - (double)rate;
+      for (int i = 0, j = 0; i < N; j++) {
         sub.push_back(i);
-        if (rate < 1) i += std::max(1, nb(gen));
+        if (rate < 1) i += subset_gap(seed, c, round - 1, j, q);
         else i++;
       }
       for (auto& hy : hs) {

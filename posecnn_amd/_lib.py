@@ -113,6 +113,13 @@ _SIGS = {
     "pcnn_icp_score_workspace_size": (c_size_t, [c_int, c_int, c_int]),
     "pcnn_icp_score": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_float, c_void_p,
                                c_void_p, c_void_p, c_size_t, c_void_p]),
+    "pcnn_energy_records_workspace_size": (c_size_t, [c_int, c_int, c_int]),
+    "pcnn_energy_records": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_float, c_float, c_int,
+                                    c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "pcnn_energy_rec": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_float, c_float, c_void_p,
+                                c_void_p]),
+    "pcnn_nelder_mead_energy": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int,
+                                        c_float, c_float, c_void_p, c_void_p, c_void_p, c_void_p]),
     "pcnn_pose_energy_batch": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_float,
                                        c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t,
                                        c_void_p]),

@@ -1119,3 +1119,326 @@ extern "C" int pcnn_icp_score(const float* live, const int32_t* label, int obj, 
   PCNN_CHECK_LAUNCH();
   return PCNN_OK;
 }
+
+// ---------------------------------------------------------------------------
+// Nelder-Mead on optEnergy, on the device (round 5).  solveICP's refinePose
+// (synthesize.cpp:2221-2250 -> poseWithOpt :2529-2573, NLopt LN_NELDERMEAD,
+// 7 parameters, bounds +-0.1 / +-0.01 / +-0.1, at most `iterations`
+// evaluations of optEnergy :2476-2526) used to run as Python generators with
+// one energy launch and one host read per simplex step.  Here:
+//   k_rec_count / k_rec_scatter  the object's pixels whose live vertex lies in
+//       the depth range (the pose-independent half of optEnergy's test), in
+//       raster order, as (rendered vertex, live vertex) records per problem;
+//   energy_rec  optEnergy of one pose over a problem's records by one
+//       1024-thread workgroup, a fixed summation order (thread-strided float
+//       sums, then a fixed wave / workgroup tree): k_energy_rec evaluates K
+//       poses, and k_nm runs whole searches, one workgroup per problem, with
+//       no host read until the end.  The search is the bounded Nelder-Mead of
+//       posecnn_amd/synthesize/icp.py nelder_mead_steps, operation for
+//       operation in double (NLopt is absent: its trajectory is unpinned), so
+//       the device search and the host search over k_energy_rec give the
+//       same bits.
+namespace pcnn_refine {
+
+constexpr int kNmThreads = 1024;
+constexpr int kNmDim = 7;
+
+__global__ void __launch_bounds__(kBlk) k_rec_count(const float* __restrict__ live_all, int n_live,
+                                                    const int32_t* __restrict__ label, int HW, float znear, float zfar,
+                                                    const int32_t* __restrict__ prob_obj,
+                                                    const int32_t* __restrict__ prob_live, int nseg,
+                                                    int32_t* __restrict__ segcnt) {
+  __shared__ int sh[kBlk / 64];
+  const int p = blockIdx.y, seg = blockIdx.x;
+  const int obj = prob_obj[p], li = prob_live[p];
+  const bool ok_live = li >= 0 && li < n_live;
+  const float* __restrict__ live = live_all + (ok_live ? (size_t)li * HW * 3 : 0);
+  int c = 0;
+  for (int i = threadIdx.x; i < kSeg; i += kBlk) {
+    const int j = seg * kSeg + i;
+    if (ok_live && j < HW && label[j] == obj) {
+      const float lz = live[(size_t)j * 3 + 2];
+      c += (lz > znear && lz < zfar) ? 1 : 0;  // :2514
+    }
+  }
+  c = block_sum_int<kBlk>(c, sh);
+  if (threadIdx.x == 0) segcnt[(size_t)p * nseg + seg] = c;
+}
+
+__global__ void __launch_bounds__(kBlk) k_rec_scatter(const float* __restrict__ live_all, int n_live,
+                                                      const int32_t* __restrict__ label,
+                                                      const float* __restrict__ pv_all, int HW, float znear,
+                                                      float zfar, const int32_t* __restrict__ prob_obj,
+                                                      const int32_t* __restrict__ prob_live, int nseg,
+                                                      const int32_t* __restrict__ segcnt, float* __restrict__ rec,
+                                                      int32_t* __restrict__ count) {
+  __shared__ int sh[kBlk / 64];
+  __shared__ int wc[kBlk / 64];
+  const int p = blockIdx.y, seg = blockIdx.x;
+  const int obj = prob_obj[p], li = prob_live[p];
+  const bool ok_live = li >= 0 && li < n_live;
+  const float* __restrict__ live = live_all + (ok_live ? (size_t)li * HW * 3 : 0);
+  const float* __restrict__ pv = pv_all + (size_t)p * HW * 4;
+  const int32_t* sc = segcnt + (size_t)p * nseg;
+  int o = 0, tot = 0;
+  for (int s = threadIdx.x; s < nseg; s += kBlk) {
+    o += s < seg ? sc[s] : 0;
+    tot += sc[s];
+  }
+  int off = block_sum_int<kBlk>(o, sh);
+  const int total = block_sum_int<kBlk>(tot, sh);
+  if (seg == 0 && threadIdx.x == 0) count[p] = total;
+  float* out = rec + (size_t)p * HW * 6;
+  const int wave = threadIdx.x >> 6;
+  for (int i0 = 0; i0 < kSeg; i0 += kBlk) {
+    const int j = seg * kSeg + i0 + threadIdx.x;
+    bool ok = false;
+    if (ok_live && j < HW && label[j] == obj) {
+      const float lz = live[(size_t)j * 3 + 2];
+      ok = lz > znear && lz < zfar;
+    }
+    const uint64_t m = __ballot(ok);
+    if (pcnn::lane_id() == 0) wc[wave] = __popcll(m);
+    __syncthreads();
+    int base = off;
+    for (int w = 0; w < wave; w++) base += wc[w];
+    if (ok) {
+      float* r = out + (size_t)(base + __popcll(m & pcnn::lanemask_lt())) * 6;
+      r[0] = pv[(size_t)j * 4 + 0];
+      r[1] = pv[(size_t)j * 4 + 1];
+      r[2] = pv[(size_t)j * 4 + 2];
+      r[3] = live[(size_t)j * 3 + 0];
+      r[4] = live[(size_t)j * 3 + 1];
+      r[5] = live[(size_t)j * 3 + 2];
+    }
+    for (int w = 0; w < kBlk / 64; w++) off += wc[w];
+    __syncthreads();
+  }
+}
+
+// optEnergy (:2476-2526) of pose P (float, quaternion normalised as
+// k_pose_energy does) over n records; every thread of a 1024-thread
+// workgroup calls it and gets the value
+__device__ float energy_rec(const float* __restrict__ r, int n, const float (&P)[7], float znear, float zfar,
+                            float* sh) {
+  const float qn = sqrtf(P[0] * P[0] + P[1] * P[1] + P[2] * P[2] + P[3] * P[3]);
+  const Quat q = {P[0] / qn, P[1] / qn, P[2] / qn, P[3] / qn};
+  float s = 0.f, c = 0.f;
+  for (int i = threadIdx.x; i < n; i += kNmThreads) {
+    const float* x = r + (size_t)i * 6;
+    float p0, p1, p2;
+    rotate(q, x[0], x[1], x[2], p0, p1, p2);
+    p0 = p0 + P[4];
+    p1 = p1 + P[5];
+    p2 = p2 + P[6];
+    if (!isnan(p0) && !isnan(p1) && !isnan(p2) && p2 > znear && p2 < zfar) {  // :2514 (the live half: records)
+      const float dx = p0 - x[3], dy = p1 - x[4], dz = p2 - x[5];
+      s += sqrtf(dx * dx + dy * dy + dz * dz);
+      c += 1.f;
+    }
+  }
+  s = pcnn::wave_sum(s);
+  c = pcnn::wave_sum(c);
+  const int wave = threadIdx.x >> 6;
+  if (pcnn::lane_id() == 0) {
+    sh[2 * wave] = s;
+    sh[2 * wave + 1] = c;
+  }
+  __syncthreads();
+  float S = 0.f, Cn = 0.f;
+  for (int w = 0; w < kNmThreads / 64; w++) {
+    S += sh[2 * w];
+    Cn += sh[2 * w + 1];
+  }
+  __syncthreads();
+  return Cn > 0.f ? S / Cn : 0.f;  // distance /= c (:2520-2521)
+}
+
+__global__ void __launch_bounds__(kNmThreads) k_energy_rec(const float* __restrict__ rec,
+                                                           const int32_t* __restrict__ count, int stride,
+                                                           const float* __restrict__ poses,
+                                                           const int32_t* __restrict__ pose_prob, float znear,
+                                                           float zfar, float* __restrict__ energy) {
+  __shared__ float sh[2 * kNmThreads / 64];
+  const int k = blockIdx.x;
+  const int p = pose_prob[k];
+  float P[7];
+  for (int e = 0; e < 7; e++) P[e] = poses[(size_t)k * 7 + e];
+  const float v = energy_rec(rec + (size_t)p * stride * 6, count[p], P, znear, zfar, sh);
+  if (threadIdx.x == 0) energy[k] = v;
+}
+
+// Bounded Nelder-Mead (icp.py nelder_mead_steps, in its operation order):
+// simplex x0 + step_i e_i with step = min(0.25 (ub - lb), 0.75 (ub - x0),
+// 0.75 (x0 - lb)); each iteration a stable sort, the centroid of the best n
+// (a sequential sum / n), reflection, expansion, contraction (outside /
+// inside), shrink toward the best; trial points clamped to the bounds; at
+// most max_eval evaluations.  One workgroup per problem: thread 0 keeps the
+// simplex in LDS, every thread evaluates.
+__global__ void __launch_bounds__(kNmThreads) k_nm(const float* __restrict__ rec, const int32_t* __restrict__ count,
+                                                   int stride, const double* __restrict__ x0_all,
+                                                   const double* __restrict__ lb_all,
+                                                   const double* __restrict__ ub_all, int max_eval, float znear,
+                                                   float zfar, double* __restrict__ x_out, double* __restrict__ f_out,
+                                                   int32_t* __restrict__ nev_out) {
+  constexpr int n = kNmDim;
+  __shared__ double pts[n + 1][n], vals[n + 1], lb[n], ub[n], xq[n], xr[n], cen[n];
+  __shared__ double fres;
+  __shared__ float sh[2 * kNmThreads / 64];
+  const int p = blockIdx.x, t = threadIdx.x;
+  const float* r = rec + (size_t)p * stride * 6;
+  const int nr = count[p];
+  auto eval = [&]() -> double {  // every thread; the point is xq (LDS)
+    __syncthreads();
+    float P[7];
+    for (int e = 0; e < n; e++) P[e] = (float)xq[e];  // the host path evaluates float32 points
+    const float v = energy_rec(r, nr, P, znear, zfar, sh);
+    return (double)v;
+  };
+  auto clampq = [&](int e, double v) { return fmin(fmax(v, lb[e]), ub[e]); };  // np.minimum(np.maximum(p, lb), ub)
+  if (t == 0) {
+    for (int e = 0; e < n; e++) {
+      lb[e] = lb_all[(size_t)p * n + e];
+      ub[e] = ub_all[(size_t)p * n + e];
+      pts[0][e] = x0_all[(size_t)p * n + e];
+    }
+    for (int i = 0; i < n; i++) {
+      const double x0 = pts[0][i];
+      const double step = fmin(0.25 * (ub[i] - lb[i]), fmin(0.75 * (ub[i] - x0), 0.75 * (x0 - lb[i])));
+      for (int e = 0; e < n; e++) pts[i + 1][e] = pts[0][e] + (e == i ? step : 0.0);
+    }
+  }
+  for (int i = 0; i <= n; i++) {  // the initial simplex (one batch on the host: the same values)
+    if (t == 0)
+      for (int e = 0; e < n; e++) xq[e] = pts[i][e];
+    const double v = eval();
+    if (t == 0) vals[i] = v;
+  }
+  int nev = n + 1;
+  while (nev < max_eval) {  // nev is identical in every thread
+    if (t == 0) {
+      for (int i = 1; i <= n; i++) {  // stable insertion sort (np.argsort kind="stable")
+        for (int j = i; j > 0 && vals[j] < vals[j - 1]; j--) {
+          const double tv = vals[j];
+          vals[j] = vals[j - 1];
+          vals[j - 1] = tv;
+          for (int e = 0; e < n; e++) {
+            const double tp = pts[j][e];
+            pts[j][e] = pts[j - 1][e];
+            pts[j - 1][e] = tp;
+          }
+        }
+      }
+      for (int e = 0; e < n; e++) {  // np.mean(pts[:-1], axis=0): rows added in order, then / n
+        double s = pts[0][e];
+        for (int i = 1; i < n; i++) s = s + pts[i][e];
+        cen[e] = s / (double)n;
+      }
+      for (int e = 0; e < n; e++) {
+        xr[e] = clampq(e, cen[e] + (cen[e] - pts[n][e]));
+        xq[e] = xr[e];
+      }
+    }
+    const double fr = eval();
+    nev++;
+    __syncthreads();
+    const double v0 = vals[0], vn1 = vals[n - 1], vn = vals[n];
+    if (fr < v0 && nev < max_eval) {
+      if (t == 0)
+        for (int e = 0; e < n; e++) xq[e] = clampq(e, cen[e] + 2.0 * (cen[e] - pts[n][e]));
+      const double fe = eval();
+      nev++;
+      if (t == 0) {
+        const bool take_e = fe < fr;
+        for (int e = 0; e < n; e++) pts[n][e] = take_e ? xq[e] : xr[e];
+        vals[n] = take_e ? fe : fr;
+      }
+    } else if (fr < vn1) {
+      if (t == 0) {
+        for (int e = 0; e < n; e++) pts[n][e] = xr[e];
+        vals[n] = fr;
+      }
+    } else if (nev < max_eval) {
+      if (t == 0)
+        for (int e = 0; e < n; e++)
+          xq[e] = fr >= vn ? clampq(e, cen[e] + 0.5 * (pts[n][e] - cen[e])) : clampq(e, cen[e] + 0.5 * (xr[e] - cen[e]));
+      const double fc = eval();
+      nev++;
+      if (fc < fmin(fr, vn)) {
+        if (t == 0) {
+          for (int e = 0; e < n; e++) pts[n][e] = xq[e];
+          vals[n] = fc;
+        }
+      } else {
+        const int m = min(n, max_eval - nev);
+        for (int i = 1; i <= m; i++) {  // shrink toward the best (one batch on the host)
+          if (t == 0)
+            for (int e = 0; e < n; e++) xq[e] = clampq(e, pts[0][e] + 0.5 * (pts[i][e] - pts[0][e]));
+          const double fv = eval();
+          if (t == 0) {
+            for (int e = 0; e < n; e++) pts[i][e] = xq[e];
+            vals[i] = fv;
+          }
+        }
+        nev += m > 0 ? m : 0;
+      }
+    }
+    __syncthreads();
+  }
+  if (t == 0) {
+    int b = 0;
+    for (int i = 1; i <= n; i++)
+      if (vals[i] < vals[b]) b = i;  // np.argmin: the first minimum
+    for (int e = 0; e < n; e++) x_out[(size_t)p * n + e] = pts[b][e];
+    f_out[p] = vals[b];
+    nev_out[p] = nev;
+  }
+  (void)fres;
+}
+
+}  // namespace pcnn_refine
+
+extern "C" size_t pcnn_energy_records_workspace_size(int N, int H, int W) {
+  if (N <= 0 || H <= 0 || W <= 0) return 256;
+  const int nseg = (H * W + kSeg - 1) / kSeg;
+  return (size_t)N * nseg * sizeof(int32_t) + 256;
+}
+
+extern "C" int pcnn_energy_records(const float* live, int n_live, const int32_t* label, const float* pred_vertices,
+                                   int H, int W, float znear, float zfar, int N, const int32_t* prob_obj,
+                                   const int32_t* prob_live, float* records, int32_t* counts, void* workspace,
+                                   size_t workspace_bytes, void* stream) {
+  PCNN_REQUIRE(live && label && pred_vertices && prob_obj && prob_live && records && counts && workspace);
+  PCNN_REQUIRE(N > 0 && H > 0 && W > 0 && n_live > 0 && (long)H * W < (1l << 30));
+  const int HW = H * W, nseg = (HW + kSeg - 1) / kSeg;
+  if (workspace_bytes < (size_t)N * nseg * sizeof(int32_t)) return PCNN_ECAPACITY;
+  int32_t* segcnt = (int32_t*)workspace;
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(k_rec_count, dim3(nseg, N), dim3(kBlk), 0, st, live, n_live, label, HW, znear, zfar, prob_obj,
+                     prob_live, nseg, segcnt);
+  hipLaunchKernelGGL(k_rec_scatter, dim3(nseg, N), dim3(kBlk), 0, st, live, n_live, label, pred_vertices, HW, znear,
+                     zfar, prob_obj, prob_live, nseg, segcnt, records, counts);
+  PCNN_CHECK_LAUNCH();
+  return PCNN_OK;
+}
+
+extern "C" int pcnn_energy_rec(const float* records, const int32_t* counts, int stride, const float* poses,
+                               const int32_t* pose_prob, int K, float znear, float zfar, float* energy, void* stream) {
+  PCNN_REQUIRE(records && counts && poses && pose_prob && energy && K > 0 && stride > 0);
+  hipLaunchKernelGGL(k_energy_rec, dim3(K), dim3(kNmThreads), 0, (hipStream_t)stream, records, counts, stride, poses,
+                     pose_prob, znear, zfar, energy);
+  PCNN_CHECK_LAUNCH();
+  return PCNN_OK;
+}
+
+extern "C" int pcnn_nelder_mead_energy(const float* records, const int32_t* counts, int stride, int N,
+                                       const double* x0, const double* lb, const double* ub, int max_eval,
+                                       float znear, float zfar, double* x_out, double* f_out, int32_t* nev_out,
+                                       void* stream) {
+  PCNN_REQUIRE(records && counts && x0 && lb && ub && x_out && f_out && nev_out && N > 0 && stride > 0);
+  PCNN_REQUIRE(max_eval >= 0 && max_eval <= (1 << 20));
+  hipLaunchKernelGGL(k_nm, dim3(N), dim3(kNmThreads), 0, (hipStream_t)stream, records, counts, stride, x0, lb, ub,
+                     max_eval, znear, zfar, x_out, f_out, nev_out);
+  PCNN_CHECK_LAUNCH();
+  return PCNN_OK;
+}

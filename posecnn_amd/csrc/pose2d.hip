@@ -11,18 +11,26 @@
 //   k_p2d_colcount / k_p2d_scan / k_p2d_scatter  the per-class pixel lists in
 //       the reference's column-major order (getLabels, :1010-1031): per-column
 //       class counts, a per-class scan over columns, an ordered scatter;
-//   host: the class counts come back once (object_ids need > 400 pixels), and
-//       the 8 rounds' pixel subsets of each object are drawn with the
-//       reference's own generator (a default-seeded std::mt19937 and
-//       std::negative_binomial_distribution<int>(1, maxPixels / N) per round,
-//       :1183-1213 -- identical for every hypothesis of the round) and copied
-//       up once;
+//   k_p2d_objs: object_ids (classes with > 400 pixels, :1027) and the list
+//       offsets, on the device: no host round trip anywhere in the call;
+//   k_p2d_subset: the 8 rounds' pixel subsets of each object (countInliers2D,
+//       :1183-1213 -- identical for every hypothesis of a round).  The
+//       reference skips max(1, G) pixels, G ~ negative_binomial(1, p) =
+//       geometric with p = maxPixels / N, drawn from a default-seeded
+//       std::mt19937.  Here G is drawn from a Philox stream per (class, round)
+//       by inverse CDF on exact double products (G = the largest k with
+//       U < q^k, q = 1 - p): the same distribution, computed identically by
+//       the oracle; one workgroup per (object, round) draws 1024 gaps at a
+//       time and places them by a block scan (round 5; the earlier host
+//       replay of mt19937 draws cost 5.6 of the 6.2 ms per frame and pinned
+//       nothing, since the hypotheses already use Philox streams);
 //   k_p2d_attempts / k_p2d_pick: the rejection-sampling loop (samplePoint2D
 //       x 4, degeneracy tests, Grunert P3P in double, the reprojection and
 //       getBB2D area checks) as independent attempts, each on its own Philox
 //       stream: the first 32 attempts of every hypothesis run at once (one
 //       lane each), then one lane per hypothesis keeps its first accepted
-//       attempt (further attempts one by one if none of the 32 was);
+//       attempt (one wave per hypothesis: 64 further attempts at a time, the
+//       first accepted in attempt order, if none of the 32 was);
 //   k_p2d_collect / k_p2d_count / k_p2d_select / k_p2d_finish: the 8 rounds
 //       as launches: per round one workgroup per (surviving hypothesis,
 //       object) counts inliers over the round's subset (double projections),
@@ -36,15 +44,12 @@
 #include "pcnn_common.h"
 #include <climits>
 #include <algorithm>
-#include <atomic>
-#include <random>
-#include <thread>
-#include <vector>
 
 namespace {
 
 constexpr int kRounds = 8;       // <= 256 hypotheses halve to one in <= 8 rounds; refIt = 8 (:1601)
 constexpr int kMaxHypBlock = 1024;
+constexpr int kMaxHyp = 256;     // ransacIterations (:1601)
 constexpr int kAttempts = 32;  // sampling attempts per hypothesis evaluated in one launch
 constexpr int kAttRec = 17;    // attempt record: obj (-1 rejected), R (9), t (3), pixels (4)
 
@@ -315,10 +320,11 @@ struct P2dWs {
   int32_t* coloff;   // (C, W) exclusive scan over columns
   int32_t* count;    // (C)
   int32_t* lists;    // (H W) per-class pixel lists, column-major, classes concatenated
-  int32_t* listoff;  // (C) list offsets (host-computed)
-  int32_t* objs;     // (C) object ids (host-computed)
-  int32_t* sub;      // subsets: indices into the class list, rounds concatenated per object
-  int32_t* suboff;   // (n_obj, kRounds + 1)
+  int32_t* listoff;  // (C) list offsets (k_p2d_objs)
+  int32_t* objs;     // (C) object ids (k_p2d_objs)
+  int32_t* nobj;     // (1) number of objects (k_p2d_objs)
+  int32_t* sub;      // subsets: indices into the class list; class c round r at kRounds listoff[c] + r count[c]
+  int32_t* subcnt;   // (C, kRounds) subset sizes
   double* hyp;       // (n_hyp, 16): obj, R (9), t (3)
   double* att;       // (n_hyp, kAttempts, kAttRec) attempt records
   int32_t* rl;       // (C, kMaxHypBlock) surviving hypotheses per object, in rank order
@@ -369,6 +375,82 @@ __global__ void __launch_bounds__(1024) k_p2d_scan(const int32_t* __restrict__ c
   if (threadIdx.x == 0) count[c] = carry;
 }
 
+// object_ids and list offsets (getLabels, :1010-1031): classes c >= 1 with
+// more than minArea = 400 pixels, ascending
+__global__ void __launch_bounds__(64) k_p2d_objs(int C, P2dWs ws) {
+  if (threadIdx.x != 0) return;
+  int acc = 0, n = 0;
+  for (int c = 0; c < C; c++) {
+    ws.listoff[c] = acc;
+    const int cnt = ws.count[c];
+    acc += cnt;
+    if (c >= 1 && (float)cnt > 400.0f) ws.objs[n++] = c;
+  }
+  *ws.nobj = n;
+}
+
+// the subset of round r (0-based; maxPixels = 1000 (r + 1)) of class c's
+// list: indices 0 = s_0 < s_1 < ... < N with s_{j+1} = s_j + max(1, G_j)
+// (countInliers2D's skip, :1210-1213), G_j geometric with success
+// probability p = maxPixels / (float)N, drawn from the Philox4x32-10 block
+// (j, c, 'SUB0' + r, 0) under key seed: U = (x 2^21 + (y >> 11) + 0.5) 2^-53
+// in (0, 1) from its first two words, G = the largest k with U < q^k,
+// q = 1 - p, the powers by repeated double products (the oracle restates
+// the same operations).  p >= 1: every index.
+__device__ __forceinline__ int p2d_gap(uint64_t seed, int c, int r, int j, double q) {
+  const U4 b = philox(U4{(uint32_t)j, (uint32_t)c, 0x53554230u + (uint32_t)r, 0u}, (uint32_t)seed,
+                      (uint32_t)(seed >> 32));
+  const double U = ((double)b.x * 2097152.0 + (double)(b.y >> 11) + 0.5) * 0x1p-53;
+  int k = 0;
+  double t = q;
+  while (t > U) {  // q^(k+1) > U: G > k; at most 53 ln 2 / -ln q steps
+    k++;
+    t = t * q;
+  }
+  return k > 1 ? k : 1;
+}
+
+__global__ void __launch_bounds__(1024) k_p2d_subset(uint64_t seed, P2dWs ws) {
+  __shared__ int wsum[16];
+  __shared__ int carry_s;
+  const int c = blockIdx.x, r = blockIdx.y, t = threadIdx.x, lane = pcnn::lane_id(), wave = t >> 6;
+  const int N = ws.count[c];
+  if (c == 0 || !((float)N > 400.0f)) return;  // not an object (block-uniform)
+  int* S = ws.sub + (size_t)kRounds * ws.listoff[c] + (size_t)r * N;
+  const int maxPixels = 1000 * (r + 1);
+  const float rate = maxPixels / (float)N;  // :1191
+  if (!(rate < 1)) {  // every pixel (:1212-1213)
+    for (int i = t; i < N; i += blockDim.x) S[i] = i;
+    if (t == 0) ws.subcnt[c * kRounds + r] = N;
+    return;
+  }
+  const double q = 1.0 - (double)rate;
+  int carry = 0;  // s_{j0}
+  for (int j0 = 0;; j0 += 1024) {
+    const int g = p2d_gap(seed, c, r, j0 + t, q);
+    int incl = g;  // block inclusive scan of the gaps
+#pragma unroll
+    for (int k = 1; k < 64; k <<= 1) {
+      const int y = __shfl_up(incl, k, 64);
+      if (lane >= k) incl += y;
+    }
+    if (lane == 63) wsum[wave] = incl;
+    __syncthreads();
+    int wb = 0, tot = 0;
+    for (int w = 0; w < 16; w++) {
+      if (w < wave) wb += wsum[w];
+      tot += wsum[w];
+    }
+    const long pos = (long)carry + wb + incl - g;  // s_{j0 + t}
+    if (pos < N) S[j0 + t] = (int)pos;
+    if (pos < N && pos + g >= N) ws.subcnt[c * kRounds + r] = j0 + t + 1;  // the last index below N
+    __syncthreads();  // wsum is rewritten by the next chunk
+    if ((long)carry + tot >= N) break;  // block-uniform
+    carry += tot;
+  }
+  (void)carry_s;
+}
+
 // one wave per column: 64 rows at a time; the lanes of one class take their
 // ranks by ballot (classes peeled one at a time, usually 1-3 per chunk), so
 // each class list keeps the column's ascending row order
@@ -403,7 +485,7 @@ __device__ bool p2d_attempt(const float* __restrict__ vm, const float* __restric
                             const Cam& k, uint64_t seed, int h, int a, int n_obj, const P2dWs& ws, int& obj_out,
                             int* px_out, Pose& P) {
   Stream rs(seed, (uint32_t)h, (uint32_t)a);
-  const int obj = ws.objs[rs.uniform(n_obj)];
+  const int obj = ws.objs[rs.uniform(n_obj)];  // n_obj > 0
   const int* L = ws.lists + ws.listoff[obj];
   const int N = ws.count[obj];
   float m[4][2];
@@ -453,10 +535,11 @@ __device__ bool p2d_attempt(const float* __restrict__ vm, const float* __restric
 // the reference's loop runs attempts until one is accepted, and attempts are
 // independent (each its own stream), so they need not wait for each other.
 __global__ void __launch_bounds__(64) k_p2d_attempts(const float* __restrict__ vm, const float* __restrict__ ext,
-                                                     int H, int W, int C, Cam k, uint64_t seed, int n_hyp,
-                                                     int n_obj, int T, P2dWs ws) {
+                                                     int H, int W, int C, Cam k, uint64_t seed, int n_hyp, int T,
+                                                     P2dWs ws) {
   const int id = blockIdx.x * blockDim.x + threadIdx.x;
-  if (id >= n_hyp * T) return;
+  const int n_obj = *ws.nobj;
+  if (id >= n_hyp * T || n_obj == 0) return;
   const int h = id % n_hyp, a = id / n_hyp;
   double* rec = ws.att + (size_t)(h * T + a) * kAttRec;
   int obj, px4[4];
@@ -471,40 +554,64 @@ __global__ void __launch_bounds__(64) k_p2d_attempts(const float* __restrict__ v
   for (int i = 0; i < 4; i++) rec[13 + i] = px4[i];
 }
 
-// One lane per hypothesis: its first accepted attempt (the batch above, then
-// -- rarely -- further attempts one by one), written out as :1682-1686 stores it.
+// One wave per hypothesis: its first accepted attempt in attempt order --
+// the batch above, then (rarely) 64 further attempts at a time, each lane
+// one attempt, the lowest accepted lane kept -- written out as :1682-1686
+// stores it.  max_iter bounds the attempts (the reference: 10,000,000).
 __global__ void __launch_bounds__(64) k_p2d_pick(const float* __restrict__ vm, const float* __restrict__ ext, int H,
-                                                 int W, int C, Cam k, uint64_t seed, int n_hyp, int n_obj,
-                                                 int max_iter, int T, P2dWs ws, float* __restrict__ hyps_out,
+                                                 int W, int C, Cam k, uint64_t seed, int n_hyp, int max_iter, int T,
+                                                 P2dWs ws, float* __restrict__ hyps_out,
                                                  int32_t* __restrict__ hyp_px) {
-  const int h = blockIdx.x * blockDim.x + threadIdx.x;
+  const int h = blockIdx.x, lane = pcnn::lane_id();
   if (h >= n_hyp) return;
-  double* hr = ws.hyp + (size_t)h * 16;
-  hr[0] = -1;
-  hyps_out[(size_t)h * 13] = -1.f;
-  for (int i = 1; i < 13; i++) hyps_out[(size_t)h * 13 + i] = 0.f;
-  for (int i = 0; i < 4; i++) hyp_px[h * 4 + i] = -1;
-  if (n_obj == 0) return;
-  int obj = -1, px4[4];
+  const int n_obj = *ws.nobj;
+  // the batch: lane a < T reads attempt a's record; the first accepted one wins
+  int a_hit = -1;
+  {
+    const bool acc = lane < T && n_obj > 0 && ws.att[(size_t)(h * T + lane) * kAttRec] >= 0;
+    const uint64_t b = __ballot(acc);
+    if (b) a_hit = __ffsll((unsigned long long)b) - 1;
+  }
+  int obj = -1, px4[4] = {-1, -1, -1, -1};
   Pose P;
-  for (int a = 0; a < T && obj < 0; a++) {
-    const double* rec = ws.att + (size_t)(h * T + a) * kAttRec;
-    if (rec[0] < 0) continue;
+  if (a_hit >= 0) {
+    const double* rec = ws.att + (size_t)(h * T + a_hit) * kAttRec;
     obj = (int)rec[0];
     for (int i = 0; i < 9; i++) P.R[i] = rec[1 + i];
     for (int i = 0; i < 3; i++) P.t[i] = rec[10 + i];
     for (int i = 0; i < 4; i++) px4[i] = (int)rec[13 + i];
+  } else if (n_obj > 0) {
+    for (int a0 = T; a0 < max_iter; a0 += 64) {  // wave-uniform loop
+      const int a = a0 + lane;
+      int o = -1, q4[4];
+      Pose Q;
+      const bool acc = a < max_iter && p2d_attempt(vm, ext, H, W, C, k, seed, h, a, n_obj, ws, o, q4, Q);
+      const uint64_t b = __ballot(acc);
+      if (b) {
+        const int src = __ffsll((unsigned long long)b) - 1;  // the lowest accepted attempt
+        obj = __shfl(o, src);
+        for (int i = 0; i < 4; i++) px4[i] = __shfl(q4[i], src);
+        for (int i = 0; i < 9; i++) P.R[i] = __shfl(Q.R[i], src);
+        for (int i = 0; i < 3; i++) P.t[i] = __shfl(Q.t[i], src);
+        break;
+      }
+    }
   }
-  for (int a = T; a < max_iter && obj < 0; a++)
-    if (!p2d_attempt(vm, ext, H, W, C, k, seed, h, a, n_obj, ws, obj, px4, P)) obj = -1;
-  if (obj < 0) return;
+  if (lane != 0) return;
+  double* hr = ws.hyp + (size_t)h * 16;
+  float* ho = hyps_out + (size_t)h * 13;
   hr[0] = obj;
+  ho[0] = (float)obj;
+  for (int i = 0; i < 12; i++) ho[1 + i] = 0.f;
+  for (int i = 0; i < 4; i++) hyp_px[h * 4 + i] = obj >= 0 ? px4[i] : -1;
+  if (obj < 0) {
+    hr[0] = -1;
+    return;
+  }
   for (int i = 0; i < 9; i++) hr[1 + i] = P.R[i];
   for (int i = 0; i < 3; i++) hr[10 + i] = P.t[i];
-  hyps_out[(size_t)h * 13] = (float)obj;
-  for (int i = 0; i < 9; i++) hyps_out[(size_t)h * 13 + 1 + i] = (float)P.R[i];
-  for (int i = 0; i < 3; i++) hyps_out[(size_t)h * 13 + 10 + i] = (float)P.t[i];
-  for (int i = 0; i < 4; i++) hyp_px[h * 4 + i] = px4[i];
+  for (int i = 0; i < 9; i++) ho[1 + i] = (float)P.R[i];
+  for (int i = 0; i < 3; i++) ho[10 + i] = (float)P.t[i];
 }
 
 // The preemptive rounds of :1693-1727 as launches over (surviving
@@ -516,6 +623,7 @@ __global__ void __launch_bounds__(64) k_p2d_pick(const float* __restrict__ vm, c
 // output of :1729-1764.
 __global__ void __launch_bounds__(64) k_p2d_collect(int n_hyp, P2dWs ws) {  // one wave per object
   const int oi = blockIdx.x, lane = pcnn::lane_id();
+  if (oi >= *ws.nobj) return;
   const double obj = ws.objs[oi];
   int m = 0;
   for (int h0 = 0; h0 < n_hyp; h0 += 64) {  // ballot compaction keeps ascending h
@@ -532,12 +640,12 @@ __global__ void __launch_bounds__(256) k_p2d_count(const float* __restrict__ vm,
                                                    int C, Cam k, P2dWs ws, int r, int32_t* __restrict__ inl_out) {
   __shared__ int part[4];
   const int j = blockIdx.x, oi = blockIdx.y;
-  if (j >= ws.rm[oi]) return;  // block-uniform
+  if (oi >= *ws.nobj || j >= ws.rm[oi]) return;  // block-uniform
   const int obj = ws.objs[oi];
   const int* L = ws.lists + ws.listoff[obj];
   const int h = ws.rl[oi * kMaxHypBlock + j];
-  const int* S = ws.sub + ws.suboff[oi * (kRounds + 1) + r];
-  const int ns = ws.suboff[oi * (kRounds + 1) + r + 1] - ws.suboff[oi * (kRounds + 1) + r];
+  const int* S = ws.sub + (size_t)kRounds * ws.listoff[obj] + (size_t)r * ws.count[obj];
+  const int ns = ws.subcnt[obj * kRounds + r];
   const double* hr = ws.hyp + (size_t)h * 16;
   Pose P;
   for (int i = 0; i < 9; i++) P.R[i] = hr[1 + i];
@@ -565,6 +673,7 @@ __global__ void __launch_bounds__(256) k_p2d_count(const float* __restrict__ vm,
 __global__ void __launch_bounds__(1024) k_p2d_select(P2dWs ws) {
   __shared__ int hl[kMaxHypBlock], hc[kMaxHypBlock], tmp[kMaxHypBlock];
   const int oi = blockIdx.x;
+  if (oi >= *ws.nobj) return;
   const int m = ws.rm[oi];
   if (m <= 1) return;
   for (int j = threadIdx.x; j < m; j += blockDim.x) {
@@ -589,7 +698,7 @@ __global__ void __launch_bounds__(1024) k_p2d_select(P2dWs ws) {
 __global__ void __launch_bounds__(64) k_p2d_finish(int C, int n_hyp, P2dWs ws, int32_t* __restrict__ final_out,
                                                    float* __restrict__ poses_out) {
   const int oi = blockIdx.x, lane = pcnn::lane_id();  // one wave per object
-  if (ws.rm[oi] == 0) return;
+  if (oi >= *ws.nobj || ws.rm[oi] == 0) return;
   const int obj = ws.objs[oi];
   const int h = ws.rl[oi * kMaxHypBlock];
   int nh = 0;
@@ -605,7 +714,7 @@ __global__ void __launch_bounds__(64) k_p2d_finish(int C, int n_hyp, P2dWs ws, i
 }
 
 struct Layout {
-  size_t colcnt, coloff, count, lists, listoff, objs, suboff, hyp, att, rl, rc, rm, sub, total;
+  size_t colcnt, coloff, count, lists, listoff, objs, nobj, subcnt, hyp, att, rl, rc, rm, sub, total;
 };
 
 Layout layout(int H, int W, int C, int n_hyp) {
@@ -624,7 +733,8 @@ Layout layout(int H, int W, int C, int n_hyp) {
   l.lists = take((size_t)H * W * sizeof(int32_t));
   l.listoff = take((size_t)C * sizeof(int32_t));
   l.objs = take((size_t)C * sizeof(int32_t));
-  l.suboff = take((size_t)C * (kRounds + 1) * sizeof(int32_t));
+  l.nobj = take(sizeof(int32_t));
+  l.subcnt = take((size_t)C * kRounds * sizeof(int32_t));
   l.hyp = take((size_t)n_hyp * 16 * sizeof(double));
   l.att = take((size_t)n_hyp * kAttempts * kAttRec * sizeof(double));
   l.rl = take((size_t)C * kMaxHypBlock * sizeof(int32_t));
@@ -648,7 +758,10 @@ extern "C" int pcnn_pose2d(const int32_t* label, const float* vertmap, const flo
                            float* poses_out, float* hyps_out, int32_t* hyp_px, int32_t* inl_out, int32_t* final_out,
                            void* workspace, size_t workspace_bytes, void* stream) {
   PCNN_REQUIRE(label && vertmap && extents && poses_out && hyps_out && hyp_px && inl_out && final_out);
-  PCNN_REQUIRE(H > 0 && W > 0 && C > 1 && C <= 64 && n_hyp > 0 && n_hyp <= kMaxHypBlock && max_iter > 0);
+  // n_hyp <= 256: the reference's ransacIterations (:1601), so that 8 halving
+  // rounds leave one hypothesis per object, as getWorkingQueue (:1150-1160)
+  // stops at
+  PCNN_REQUIRE(H > 0 && W > 0 && C > 1 && C <= 64 && n_hyp > 0 && n_hyp <= kMaxHyp && max_iter > 0);
   PCNN_REQUIRE((long)H * W < (1l << 28));
   const Layout l = layout(H, W, C, n_hyp);
   if (!workspace || workspace_bytes < l.total) return PCNN_ECAPACITY;
@@ -660,7 +773,8 @@ extern "C" int pcnn_pose2d(const int32_t* label, const float* vertmap, const flo
   ws.lists = (int32_t*)(base + l.lists);
   ws.listoff = (int32_t*)(base + l.listoff);
   ws.objs = (int32_t*)(base + l.objs);
-  ws.suboff = (int32_t*)(base + l.suboff);
+  ws.nobj = (int32_t*)(base + l.nobj);
+  ws.subcnt = (int32_t*)(base + l.subcnt);
   ws.hyp = (double*)(base + l.hyp);
   ws.att = (double*)(base + l.att);
   ws.rl = (int32_t*)(base + l.rl);
@@ -671,108 +785,28 @@ extern "C" int pcnn_pose2d(const int32_t* label, const float* vertmap, const flo
   if (hipMemsetAsync(poses_out, 0, (size_t)12 * C * sizeof(float), st) != hipSuccess) return PCNN_EHIP;
   if (hipMemsetAsync(inl_out, 0xFF, (size_t)n_hyp * kRounds * sizeof(int32_t), st) != hipSuccess) return PCNN_EHIP;
   if (hipMemsetAsync(final_out, 0xFF, (size_t)C * 3 * sizeof(int32_t), st) != hipSuccess) return PCNN_EHIP;
+  if (hipMemsetAsync(ws.rm, 0, (size_t)C * sizeof(int32_t), st) != hipSuccess) return PCNN_EHIP;
+  const Cam k{fx, fy, px, py};
+  // every count, object list and subset stays on the device: the call is
+  // asynchronous on `stream` (round 5; it used to read the class counts
+  // back and draw the subsets on host threads)
   hipLaunchKernelGGL(k_p2d_colcount, dim3((W + 3) / 4), dim3(256), 0, st, label, H, W, C, ws.colcnt);
   hipLaunchKernelGGL(k_p2d_scan, dim3(C), dim3(1024), 0, st, ws.colcnt, W, ws.coloff, ws.count);
-  PCNN_CHECK_LAUNCH();
-  // the class sizes decide object_ids (> minArea = 400, :1027) and the
-  // subsets: one host round trip, as the reference is host code throughout
-  std::vector<int32_t> cnt(C);
-  if (hipMemcpyAsync(cnt.data(), ws.count, C * sizeof(int32_t), hipMemcpyDeviceToHost, st) != hipSuccess ||
-      hipStreamSynchronize(st) != hipSuccess)
-    return PCNN_EHIP;
-  std::vector<int32_t> listoff(C), objs;
-  int acc = 0;
-  for (int c = 0; c < C; c++) {
-    listoff[c] = acc;
-    acc += cnt[c];
-    if (c >= 1 && (float)cnt[c] > 400.0f) objs.push_back(c);
-  }
-  const int n_obj = (int)objs.size();
-  if (n_obj == 0) {  // no object: hypotheses stay empty (:1586-1587)
-    hipLaunchKernelGGL(k_p2d_pick, dim3((n_hyp + 63) / 64), dim3(64), 0, st, vertmap, extents, H, W, C,
-                       Cam{fx, fy, px, py}, seed, n_hyp, 0, 0, 0, ws, hyps_out, hyp_px);
-    PCNN_CHECK_LAUNCH();
-    return PCNN_OK;
-  }
-  if (hipMemcpyAsync(ws.listoff, listoff.data(), C * sizeof(int32_t), hipMemcpyHostToDevice, st) != hipSuccess ||
-      hipMemcpyAsync(ws.objs, objs.data(), n_obj * sizeof(int32_t), hipMemcpyHostToDevice, st) != hipSuccess)
-    return PCNN_EHIP;
-  const Cam k{fx, fy, px, py};
-  // the class lists and the hypotheses run on the GPU while the host draws
-  // the rounds' pixel subsets below
+  hipLaunchKernelGGL(k_p2d_objs, dim3(1), dim3(64), 0, st, C, ws);
   hipLaunchKernelGGL(k_p2d_scatter, dim3((W + 3) / 4), dim3(256), 0, st, label, H, W, C, ws);
+  hipLaunchKernelGGL(k_p2d_subset, dim3(C, kRounds), dim3(1024), 0, st, seed, ws);
   const int T = max_iter < kAttempts ? max_iter : kAttempts;
   hipLaunchKernelGGL(k_p2d_attempts, dim3((n_hyp * T + 63) / 64), dim3(64), 0, st, vertmap, extents, H, W, C, k, seed,
-                     n_hyp, n_obj, T, ws);
-  hipLaunchKernelGGL(k_p2d_pick, dim3((n_hyp + 63) / 64), dim3(64), 0, st, vertmap, extents, H, W, C, k, seed, n_hyp,
-                     n_obj, max_iter, T, ws, hyps_out, hyp_px);
-  PCNN_CHECK_LAUNCH();
-  // countInliers2D's pixel subsets of the 8 rounds (the same for every
-  // hypothesis of a round: a fresh default-seeded std::mt19937 per call,
-  // :1183-1213), one (object, round) per task: std::negative_binomial_
-  // distribution draws (a gamma and a Poisson variate each) are the costly
-  // part, so the 8 n_obj independent streams run on host threads
-  const int n_task = n_obj * kRounds;
-  std::vector<std::vector<int32_t>> part(n_task);
-  auto draw = [&](int t) {
-    const int N = cnt[objs[t / kRounds]];
-    const int r = t % kRounds + 1;
-    const int maxPixels = 1000 * r;
-    const float rate = maxPixels / (float)N;
-    std::mt19937 gen;
-    std::negative_binomial_distribution<int> nb(1, rate < 1 ? rate : 0.5f);
-    std::vector<int32_t>& out = part[t];
-    for (int i = 0; i < N;) {
-      out.push_back(i);
-      if (rate < 1) i += std::max(1, nb(gen));
-      else i++;
-    }
-  };
-  {
-    // largest first (a task draws about min(N, 1000 r) variates) from a
-    // shared counter: the makespan is close to the total over the threads,
-    // not three round-8 tasks on one thread
-    std::vector<int> order(n_task);
-    for (int t = 0; t < n_task; t++) order[t] = t;
-    auto cost = [&](int t) {
-      const int N = cnt[objs[t / kRounds]], r = t % kRounds + 1;
-      return 1000 * r < N ? 1000 * r : 0;
-    };
-    std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return cost(a) > cost(b); });
-    std::atomic<int> next{0};
-    auto work = [&] {
-      for (int i; (i = next.fetch_add(1)) < n_task;) draw(order[i]);
-    };
-    const unsigned hw = std::thread::hardware_concurrency();
-    const int nthr = std::max(1, std::min(n_task, (int)std::min(hw ? hw : 1u, 16u)));
-    std::vector<std::thread> pool;
-    for (int w = 1; w < nthr; w++) pool.emplace_back(work);
-    work();
-    for (auto& th : pool) th.join();
-  }
-  std::vector<int32_t> sub, suboff;
-  for (int oi = 0; oi < n_obj; oi++) {
-    for (int r = 0; r < kRounds; r++) {
-      suboff.push_back((int32_t)sub.size());
-      const auto& v = part[oi * kRounds + r];
-      sub.insert(sub.end(), v.begin(), v.end());
-    }
-    suboff.push_back((int32_t)sub.size());
-  }
-  if (sub.size() > (size_t)kRounds * H * W) return PCNN_ECAPACITY;
-  if (hipMemcpyAsync(ws.suboff, suboff.data(), suboff.size() * sizeof(int32_t), hipMemcpyHostToDevice, st) !=
-          hipSuccess ||
-      hipMemcpyAsync(ws.sub, sub.data(), sub.size() * sizeof(int32_t), hipMemcpyHostToDevice, st) != hipSuccess)
-    return PCNN_EHIP;
-  hipLaunchKernelGGL(k_p2d_collect, dim3(n_obj), dim3(64), 0, st, n_hyp, ws);
+                     n_hyp, T, ws);
+  hipLaunchKernelGGL(k_p2d_pick, dim3(n_hyp), dim3(64), 0, st, vertmap, extents, H, W, C, k, seed, n_hyp, max_iter, T,
+                     ws, hyps_out, hyp_px);
+  hipLaunchKernelGGL(k_p2d_collect, dim3(C), dim3(64), 0, st, n_hyp, ws);
   for (int r = 0; r < kRounds; r++) {
     const int gx = std::max(1, n_hyp >> r);  // survivors halve each round (one stays one)
-    hipLaunchKernelGGL(k_p2d_count, dim3(gx, n_obj), dim3(256), 0, st, vertmap, extents, W, C, k, ws, r, inl_out);
-    hipLaunchKernelGGL(k_p2d_select, dim3(n_obj), dim3(1024), 0, st, ws);
+    hipLaunchKernelGGL(k_p2d_count, dim3(gx, C), dim3(256), 0, st, vertmap, extents, W, C, k, ws, r, inl_out);
+    hipLaunchKernelGGL(k_p2d_select, dim3(C), dim3(1024), 0, st, ws);
   }
-  hipLaunchKernelGGL(k_p2d_finish, dim3(n_obj), dim3(64), 0, st, C, n_hyp, ws, final_out, poses_out);
+  hipLaunchKernelGGL(k_p2d_finish, dim3(C), dim3(64), 0, st, C, n_hyp, ws, final_out, poses_out);
   PCNN_CHECK_LAUNCH();
-  // the host vectors above are the sources of the async copies
-  if (hipStreamSynchronize(st) != hipSuccess) return PCNN_EHIP;
   return PCNN_OK;
 }

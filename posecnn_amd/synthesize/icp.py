@@ -152,6 +152,74 @@ def pose_energy_batch(live, label, pose_obj, pose_live, pred_vertices, pose_pv, 
     return energy
 
 
+def energy_records(live, label, prob_obj, prob_live, pred_vertices, depth_range=(0.25, 6.0), stream=None):
+    """optEnergy's inputs of N problems compacted on the device: problem i's
+    object pixels (label == prob_obj[i]) whose live vertex (live
+    (L,H,W,3)[prob_live[i]]) lies inside depth_range, in raster order, as
+    (rendered vertex (pred_vertices (N,H,W,4)[i]), live vertex) records.
+    Returns (records (N, H*W, 6), counts (N,) int32)."""
+    _lib.require_gpu(live, label, pred_vertices)
+    lv, pv = _f(live), _f(pred_vertices)
+    if lv.dim() != 4 or pv.dim() != 4 or lv.shape[3] != 3 or pv.shape[3] != 4 or pv.shape[1:3] != lv.shape[1:3]:
+        raise ValueError("energy_records: live (L,H,W,3), pred_vertices (N,H,W,4)")
+    N, H, W = pv.shape[0], pv.shape[1], pv.shape[2]
+    dev = lv.device
+    po = torch.as_tensor(prob_obj).to(device=dev, dtype=torch.int32).contiguous()
+    pl = torch.as_tensor(prob_live).to(device=dev, dtype=torch.int32).contiguous()
+    if po.numel() != N or pl.numel() != N:
+        raise ValueError("energy_records: one object id and live index per problem")
+    rec = torch.empty((N, H * W, 6), dtype=torch.float32, device=dev)
+    cnt = torch.empty((N,), dtype=torch.int32, device=dev)
+    lib = _lib.load()
+    ws = _lib.workspace(lib.pcnn_energy_records_workspace_size(N, H, W), dev, "icp_records", stream)
+    rc = lib.pcnn_energy_records(_lib.ptr(lv), lv.shape[0], _lib.ptr(label.contiguous().to(torch.int32)), _lib.ptr(pv),
+                                 H, W, float(depth_range[0]), float(depth_range[1]), N, _lib.ptr(po), _lib.ptr(pl),
+                                 _lib.ptr(rec), _lib.ptr(cnt), _lib.ptr(ws), ws.numel(), _lib.stream_ptr(stream))
+    _lib.check(rc, "energy_records")
+    return rec, cnt
+
+
+def pose_energy_records(records, counts, poses, pose_prob, depth_range=(0.25, 6.0), stream=None):
+    """optEnergy of K poses (K,7), pose k over problem pose_prob[k]'s records
+    (energy_records): one 1024-thread workgroup per pose, the same summation
+    as nelder_mead_device's evaluations."""
+    _lib.require_gpu(records, counts, poses)
+    P = _f(poses)
+    K = P.shape[0]
+    pp = torch.as_tensor(pose_prob).to(device=records.device, dtype=torch.int32).contiguous()
+    if P.dim() != 2 or P.shape[1] != 7 or pp.numel() != K:
+        raise ValueError("pose_energy_records: poses (K,7), one problem index per pose")
+    energy = torch.empty((K,), dtype=torch.float32, device=records.device)
+    rc = _lib.load().pcnn_energy_rec(_lib.ptr(records), _lib.ptr(counts), records.shape[1], _lib.ptr(P), _lib.ptr(pp),
+                                     K, float(depth_range[0]), float(depth_range[1]), _lib.ptr(energy),
+                                     _lib.stream_ptr(stream))
+    _lib.check(rc, "pose_energy_records")
+    return energy
+
+
+def nelder_mead_device(records, counts, x0, lb, ub, max_eval, depth_range=(0.25, 6.0), stream=None):
+    """The bounded Nelder-Mead of nelder_mead_steps on optEnergy, for N
+    problems at once on the device (one workgroup each, no host read until
+    the end): x0 / lb / ub (N,7) float64.  Returns (x (N,7), f (N,), nev (N,))
+    as device tensors; the same bits as nelder_mead over pose_energy_records."""
+    _lib.require_gpu(records, counts)
+    dev = records.device
+    d64 = dict(dtype=torch.float64, device=dev)
+    x0_, lb_, ub_ = (torch.as_tensor(a).to(**d64).contiguous() for a in (x0, lb, ub))
+    N = records.shape[0]
+    if x0_.shape != (N, 7) or lb_.shape != (N, 7) or ub_.shape != (N, 7):
+        raise ValueError("nelder_mead_device: x0, lb, ub (N,7), one row per problem")
+    x = torch.empty((N, 7), **d64)
+    f = torch.empty((N,), **d64)
+    nev = torch.empty((N,), dtype=torch.int32, device=dev)
+    rc = _lib.load().pcnn_nelder_mead_energy(_lib.ptr(records), _lib.ptr(counts), records.shape[1], N, _lib.ptr(x0_),
+                                             _lib.ptr(lb_), _lib.ptr(ub_), int(max_eval), float(depth_range[0]),
+                                             float(depth_range[1]), _lib.ptr(x), _lib.ptr(f), _lib.ptr(nev),
+                                             _lib.stream_ptr(stream))
+    _lib.check(rc, "nelder_mead_device")
+    return x, f, nev
+
+
 def icp_score(live, label, obj, vertmap, hyps, radius=0.01, stream=None):
     """SegICP score of J hypotheses (synthesize.cpp:2288-2330) -> (score (J,), choose (1,) int32)."""
     _lib.require_gpu(live, label, vertmap, hyps)
@@ -275,7 +343,7 @@ def nelder_mead_batch(fbatch, starts, lb, ub, max_eval):
 
 
 def solve_icp(labelmap, depth, parameters, rois, poses, render, max_error=0.01, nm_evals=50, icp_iterations=8,
-              min_pixels=400, stream=None):
+              min_pixels=400, nm_device=True, stream=None):
     """Synthesizer::solveICP (synthesize.cpp:2052-2395) on the GPU ops above,
     batched over the RoIs (the reference refines them one after another; no
     state passes between RoIs, :2090-2392).
@@ -289,8 +357,11 @@ def solve_icp(labelmap, depth, parameters, rois, poses, render, max_error=0.01, 
     skipped RoIs stay zero.  The steps, each one launch for all RoIs: live
     vertices of every RoI's object; the >= min_pixels test (one host read);
     the translation re-centring (one host read); the Nelder-Mead search on
-    optEnergy in lock step (nm_evals evaluations each, 0 skips it: every round
-    of requests is one batched energy launch and one host read); the eight
+    optEnergy (nm_evals evaluations each, 0 skips it): every RoI's search in
+    one launch on the device, one host read at its end (nm_device=False: the
+    same searches driven from the host, one energy launch and one host read
+    per lock-step round -- the reference driver its tests compare against,
+    bit for bit); the eight
     depth hypotheses of every RoI refined by one 8-iteration ICP launch; the
     SegICP score per RoI, its choice read once at the end."""
     import numpy as np
@@ -331,24 +402,27 @@ def solve_icp(labelmap, depth, parameters, rois, poses, render, max_error=0.01, 
         if c_h[k] > 0:
             T[k] = Tc_h[k]
     nm = [k for k in range(n) if c_h[k] > 0] if nm_evals > 0 else []
-    if nm:  # refinePose(..., 0): optEnergy over a correction of each re-rendered pose, in lock step
+    if nm:  # refinePose(..., 0): optEnergy over a correction of each re-rendered pose (:2221-2250)
         pv0 = torch.stack([render(objs[k], T[k])[1] for k in nm])
         x0 = np.array([1, 0, 0, 0, 0, 0, 0], np.float64)
-        r = np.array([0.1, 0.1, 0.1, 0.1, 0.01, 0.01, 0.1])
-        obj_of = torch.tensor([objs[k] for k in nm], dtype=torch.int32)
-        live_of = torch.tensor(nm, dtype=torch.int32)
-
-        def energies(items):  # every search's pending points: one launch, one host read
-            P = np.concatenate([pts for _, pts in items]).astype(np.float32)
-            who = np.concatenate([np.full(len(pts), j, np.int64) for j, pts in items])
-            e = pose_energy_batch(live, lab, obj_of[who], live_of[who], pv0, torch.from_numpy(who.astype(np.int32)),
-                                  torch.from_numpy(P).to(dev), (znear, zfar), stream).cpu().numpy()
-            out_, o = [], 0
-            for _, pts in items:
-                out_.append(e[o:o + len(pts)].astype(np.float64))
-                o += len(pts)
-            return out_
-        res = nelder_mead_batch(energies, [x0] * len(nm), [x0 - r] * len(nm), [x0 + r] * len(nm), nm_evals)
+        r = np.array([0.1, 0.1, 0.1, 0.1, 0.01, 0.01, 0.1])  # poseWithOpt's bounds (:2535-2558)
+        rec, cnt = energy_records(live, lab, [objs[k] for k in nm], nm, pv0, (znear, zfar), stream)
+        X0 = np.repeat(x0[None], len(nm), 0)
+        if nm_device:
+            xs, _, _ = nelder_mead_device(rec, cnt, X0, X0 - r, X0 + r, nm_evals, (znear, zfar), stream)
+            res = [(x, None) for x in xs.cpu().numpy()]
+        else:
+            def energies(items):  # every search's pending points: one launch, one host read
+                P = np.concatenate([pts for _, pts in items]).astype(np.float32)
+                who = np.concatenate([np.full(len(pts), j, np.int32) for j, pts in items])
+                e = pose_energy_records(rec, cnt, torch.from_numpy(P).to(dev), torch.from_numpy(who), (znear, zfar),
+                                        stream).cpu().numpy()
+                out_, o = [], 0
+                for _, pts in items:
+                    out_.append(e[o:o + len(pts)].astype(np.float64))
+                    o += len(pts)
+                return out_
+            res = nelder_mead_batch(energies, [x0] * len(nm), [x0 - r] * len(nm), [x0 + r] * len(nm), nm_evals)
         for j, k in enumerate(nm):
             x = res[j][0]
             T[k] = _se3_mul(np.concatenate([x[:4] / np.linalg.norm(x[:4]), x[4:]]), T[k]).astype(np.float32)

@@ -43,8 +43,8 @@ def estimate_poses_2d(labels, vertmap, extents, poses, num_classes, fx, fy, px, 
         raise ValueError("estimate_poses_2d: vertmap (H, W, 3 num_classes), extents (num_classes, 3)")
     if tuple(poses.shape) != (3, 4, C):
         raise ValueError("estimate_poses_2d: poses must be (3, 4, num_classes)")
-    if not 0 < n_hyp <= 1024:
-        raise ValueError("estimate_poses_2d: n_hyp in 1..1024")
+    if not 0 < n_hyp <= 256:  # the reference's ransacIterations (synthesize.cpp:1601): 8 rounds halve to one
+        raise ValueError("estimate_poses_2d: n_hyp in 1..256")
     f32 = dict(dtype=torch.float32, device=dev)
     i32 = dict(dtype=torch.int32, device=dev)
     out = torch.zeros((3, 4, C), **f32)

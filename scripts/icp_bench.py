@@ -96,20 +96,48 @@ params = list(CAMERA) + [0.25, 6.0, 10000.0]
 half = sc["half"]
 render = lambda o, p: render_box_torch(np.asarray(p, np.float64), half, o)  # noqa: E731
 e2e = {}
+
+
+def wall(fn, reps=3):
+    fn()  # warm-up
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / reps * 1e3
+
+
 for nroi in (1, 4):
     rois = np.tile(np.array([[0, sc["cls"], 0, 0, 1, 1]], np.float32), (nroi, 1))
     poses = np.tile(sc["init"].astype(np.float32)[None], (nroi, 1))
     for nm in (0, 50):
-        R.solve_icp(lab, depth, params, rois, poses, render, max_error=0.02, nm_evals=nm)  # warm-up
-        torch.cuda.synchronize()
-        reps = 3
-        t0 = time.perf_counter()
-        for _ in range(reps):
-            R.solve_icp(lab, depth, params, rois, poses, render, max_error=0.02, nm_evals=nm)
-        torch.cuda.synchronize()
-        e2e[f"rois{nroi}_nm{nm}_ms"] = round((time.perf_counter() - t0) / reps * 1e3, 2)
-res["solve_icp_end_to_end"] = {**e2e, "note": "wall time per solve_icp call (host orchestration, renders, all "
-                                               "launches and host reads); rois share one frame"}
+        e2e[f"rois{nroi}_nm{nm}_ms"] = round(wall(lambda: R.solve_icp(lab, depth, params, rois, poses, render,
+                                                                       max_error=0.02, nm_evals=nm)), 2)
+        if nm:  # the host-driven searches (one energy launch + host read per lock-step round), for comparison
+            e2e[f"rois{nroi}_nm{nm}_host_search_ms"] = round(wall(lambda: R.solve_icp(
+                lab, depth, params, rois, poses, render, max_error=0.02, nm_evals=nm, nm_device=False)), 2)
+        # the caller's renders alone (1 initial + 1 for the search + 8 hypotheses per RoI): the reference's
+        # OpenGL pass, here a torch ray-caster, outside the path
+        n_render = nroi * (1 + (1 if nm else 0) + 8)
+        e2e[f"rois{nroi}_nm{nm}_renders_ms"] = round(wall(lambda: [render(sc["cls"], sc["init"]) for _ in
+                                                                    range(n_render)]), 2)
+        e2e[f"rois{nroi}_nm{nm}_minus_renders_ms"] = round(e2e[f"rois{nroi}_nm{nm}_ms"] -
+                                                           e2e[f"rois{nroi}_nm{nm}_renders_ms"], 2)
+# the Nelder-Mead searches alone (pcnn_nelder_mead_energy: one workgroup per RoI, 50 evaluations)
+pv0 = render(sc["cls"], sc["init"])[1]
+for nroi in (1, 4):
+    rec, cnt = R.energy_records(lv[:1].contiguous(), lab, [sc["cls"]] * nroi,
+                                [0] * nroi, pv0[None].expand(nroi, -1, -1, -1).contiguous())
+    X0 = np.tile(np.array([[1, 0, 0, 0, 0, 0, 0]], np.float64), (nroi, 1))
+    r_ = np.array([0.1, 0.1, 0.1, 0.1, 0.01, 0.01, 0.1])
+    e2e[f"nelder_mead_device_rois{nroi}_us"] = round(
+        wall(lambda: R.nelder_mead_device(rec, cnt, X0, X0 - r_, X0 + r_, 50), reps=10) * 1e3, 1)
+res["solve_icp_end_to_end"] = {**e2e, "records_per_roi": int(cnt[0].item()),
+                               "note": "wall time per solve_icp call (host orchestration, renders, all launches and "
+                                       "host reads); rois share one frame; *_renders_ms = the caller's renders alone, "
+                                       "*_minus_renders_ms the rest; *_host_search_ms the searches driven from the "
+                                       "host (nm_device=False)"}
 if not a.no_cpu:
     from oracle import oracle
     ref_lv = oracle.icp_live_vertices(sc["live"]["depth"], sc["live"]["label"], sc["cls"], 10000.0, CAMERA)

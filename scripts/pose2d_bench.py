@@ -63,7 +63,7 @@ out = {"metric": "estimatePose2D frames/s (256 hypotheses, 8 preemptive rounds, 
        "value": round(1e3 / gpu_ms, 2), "unit": "frames/s", "ms_per_frame": round(gpu_ms, 3),
        "objects": a.objects, "classes": C, "objects_found": found,
        "max_centre_error_px": round(max(err), 3) if err else None,
-       "timing": "wall clock per call (host class counts and round subsets, all launches, one sync)",
+       "timing": "wall clock per call (all launches on the device, one sync)",
        "data": f"synthetic (ray-cast boxes, tests/pose2d_scene.py, coordinate noise {a.noise})"}
 if not a.no_cpu:
     from oracle import oracle  # CPU baseline leg only

@@ -242,3 +242,73 @@ def test_solve_icp_batched_over_rois(hip):
     np.testing.assert_array_equal(pnew[0], pnew[2])
     for i, c in enumerate((3, 5)):
         assert np.linalg.norm(picp[i, 4:] - trues[c][4:]) < 5e-3
+
+
+@pytest.mark.parametrize("max_eval", [5, 12, 50])
+def test_nelder_mead_device_matches_host(hip, orc, max_eval):
+    """refinePose's Nelder-Mead (poseWithOpt, synthesize.cpp:2529-2573) run
+    wholly on the device, one workgroup per problem (pcnn_nelder_mead_energy),
+    against the host search (icp.py nelder_mead) over the same record-based
+    optEnergy (pcnn_energy_rec): the same points, values and evaluation counts,
+    bit for bit, for max_eval below the initial simplex (5), with shrinks (12)
+    and at solveICP's 50.  The record energy is optEnergy over the pixels of
+    the full-frame kernel (pcnn_pose_energy, parity-tested against the
+    oracle), summed in another fixed order."""
+    from posecnn_amd.synthesize import icp as R
+    scs = [scene(s, perturb_deg=3.0, perturb_t=0.01) for s in (7, 8)]
+    lvs = [_live(sc, orc)[0] for sc in scs]
+    live = torch.cat(lvs)
+    lab = t(scs[0]["live"]["label"])
+    # problems: the two scenes' objects (live maps 0 / 1) and scene 0 again with a shifted start
+    pv = torch.stack([t(scs[0]["pred"]["pred_v"]), t(scs[1]["pred"]["pred_v"]), t(scs[0]["pred"]["pred_v"])])
+    objs = [scs[0]["cls"], scs[1]["cls"], scs[0]["cls"]]
+    labs = [scs[0]["live"]["label"], scs[1]["live"]["label"]]
+    if not np.array_equal(labs[0], labs[1]):  # one label map for all problems: use scene 0's
+        live = torch.cat([lvs[0], lvs[0]])
+    rec, cnt = R.energy_records(live, lab, objs, [0, 1, 0], pv, (0.25, 6.0))
+    assert int(cnt.min()) > 1000
+    x0 = np.array([[1, 0, 0, 0, 0, 0, 0], [1, 0, 0, 0, 0, 0, 0], [0.99, 0.02, -0.01, 0.0, 0.002, -0.001, 0.01]],
+                  np.float64)
+    r = np.array([0.1, 0.1, 0.1, 0.1, 0.01, 0.01, 0.1])
+    x, f, nev = R.nelder_mead_device(rec, cnt, x0, x0 - r, x0 + r, max_eval)
+    x, f, nev = x.cpu().numpy(), f.cpu().numpy(), nev.cpu().numpy()
+    for i in range(3):
+        def fn(p, i=i):
+            e = R.pose_energy_records(rec, cnt, torch.from_numpy(np.asarray(p, np.float32)[None]).to(D),
+                                      torch.tensor([i], dtype=torch.int32))
+            return float(e.cpu().numpy()[0])
+        hx, hf = R.nelder_mead(fn, x0[i], x0[i] - r, x0[i] + r, max_eval)
+        np.testing.assert_array_equal(x[i], hx)
+        assert f[i] == hf
+        assert nev[i] == max(8, max_eval)
+    # the record energy against the full-frame optEnergy kernel (oracle-pinned) on the same poses
+    P = torch.from_numpy(np.concatenate([x0[:1], x[:1]]).astype(np.float32)).to(D)
+    e_rec = R.pose_energy_records(rec, cnt, P, torch.zeros(2, dtype=torch.int32)).cpu().numpy()
+    e_ff = R.pose_energy(live[0], lab, objs[0], pv[0], P).cpu().numpy()
+    np.testing.assert_allclose(e_rec, e_ff, rtol=2e-5)
+    if max_eval == 50:
+        assert f[0] < e_rec[0]  # the search lowered the energy
+
+
+def test_solve_icp_device_search_matches_host_driver(hip):
+    """solve_icp with the Nelder-Mead searches on the device (the default)
+    against the host-driven lock-step searches (nm_device=False): identical
+    poses_new and poses_icp."""
+    from posecnn_amd.synthesize import icp as R
+    from refine_scene import render_box
+    sc = scene(9, perturb_deg=2.0, perturb_t=0.01)
+
+    def render(obj, pose):
+        m = render_box(np.asarray(pose, np.float64), sc["half"], obj)
+        return t(m["vertmap"]), t(m["pred_v"]), t(m["pred_n"])
+
+    params = list(CAMERA) + [0.25, 6.0, 10000.0]
+    rois = np.array([[0, sc["cls"], 0, 0, 1, 1], [0, sc["cls"], 0, 0, 1, 1]], np.float32)
+    poses = np.stack([sc["init"], sc["init"] * np.array([1, 1, 1, 1, 1.0, 1.0, 1.01])]).astype(np.float32)
+    depth = t(sc["live"]["depth"].astype(np.int32)).to(torch.uint16)
+    a = R.solve_icp(t(sc["live"]["label"]), depth, params, rois, poses, render, max_error=0.02, nm_evals=50)
+    b = R.solve_icp(t(sc["live"]["label"]), depth, params, rois, poses, render, max_error=0.02, nm_evals=50,
+                    nm_device=False)
+    np.testing.assert_array_equal(a[0], b[0])
+    np.testing.assert_array_equal(a[1], b[1])
+    assert np.linalg.norm(a[1][0, 4:] - sc["true"][4:]) < 5e-3

@@ -44,15 +44,19 @@ def test_pose2d_matches_oracle(hip, noise, seed):
         got = np.array([fx * t[0] / t[2] + px, fy * t[1] / t[2] + py])
         want = np.array([fx * p["t"][0] / p["t"][2] + px, fy * p["t"][1] / p["t"][2] + py])
         # the known answer: exact coordinates put the centre on the truth; noisy
-        # ones (a 4-point P3P survivor, no refinement) within a few pixels
-        assert np.abs(got - want).max() < (0.1 if noise == 0.0 else 5.0)
+        # ones (a 4-point P3P survivor, no refinement) within 3 px on these
+        # scenes (the GPU equals the oracle, so this is a property of the
+        # scene: 0.2-2.6 px here; over eight 1 %-noise scenes the oracle's
+        # centres land at 0.7-3.2 px with one 26 px outlier)
+        assert np.abs(got - want).max() < (0.1 if noise == 0.0 else 3.0)
 
 
 @pytest.mark.parametrize("max_iter", [3, 40])
 def test_pose2d_attempt_limit_matches_oracle(hip, max_iter):
     """max_iter bounds each hypothesis's attempts: 3 (< the 32 evaluated at
-    once: some hypotheses stay empty) and 40 (attempts past the batch run one
-    by one); hypotheses, survivors and poses against the oracle."""
+    once: some hypotheses stay empty) and 40 (attempts past the batch run 64
+    at a time, one wave per hypothesis, the first accepted in attempt order);
+    hypotheses, survivors and poses against the oracle."""
     sc = make_scene(seed=6, coord_noise=0.01)
     poses, d = _run(sc, max_iter=max_iter)
     r = oracle.pose2d(sc["label"], sc["vertmap"], sc["extents"], *sc["camera"], max_iter=max_iter)
@@ -81,3 +85,13 @@ def test_pose2d_device_inputs_and_no_object(hip):
     with pytest.raises(ValueError):
         pose2d.estimate_poses_2d(lab, sc["vertmap"], sc["extents"], np.zeros((3, 4, 2), np.float32), sc["C"],
                                  *sc["camera"])
+
+
+def test_pose2d_hypothesis_limit(hip):
+    """n_hyp is at most the reference's ransacIterations = 256
+    (synthesize.cpp:1601): eight halving rounds then leave one hypothesis per
+    object, where getWorkingQueue (:1150-1160) stops."""
+    sc = make_scene(seed=4, n_obj=2)
+    with pytest.raises(ValueError):
+        pose2d.estimate_poses_2d(sc["label"], sc["vertmap"], sc["extents"], np.zeros((3, 4, sc["C"]), np.float32),
+                                 sc["C"], *sc["camera"], n_hyp=257)
