@@ -345,6 +345,33 @@ int pcnn_pose2d(const int32_t* label, const float* vertmap, const float* extents
                 float* hyps_out, int32_t* hyp_px, int32_t* inl_out, int32_t* final_out, void* workspace,
                 size_t workspace_bytes, void* stream);
 
+/* ---------------------------------------------------------------------------
+ * Depth-based pose estimation (the cfg.TEST.VERTEX_REG_3D
+ * branch).  Replaces Synthesizer::estimatePose3D (lib/synthesize/synthesize.cpp:
+ * 1769-1965; synthesizer.pyx:86-95 estimate_poses_3d, called from
+ * lib/fcn/test.py:1385, its poses then refined by solveICP, test.py:1403-1416).
+ *  label, vertmap, extents, fx fy px py as pcnn_pose2d; depth (H,W) uint16 raw
+ *  depth, camera coordinates = pxToEye (:1372-1389) with depth_factor.
+ *  Preemptive RANSAC over 3-D / 3-D correspondences: n_hyp (1..256) hypotheses,
+ *  each from 3 pixels of one object with depth through the rigid (Kabsch)
+ *  transform, 1 cm reconstruction and 400 px box-area checks (attempt a of
+ *  hypothesis h on Philox stream (h, 'P3D', a)); 8 rounds of inlier counting
+ *  (< 1 cm) over hole-skipping pixel subsets (the pcnn_pose2d skip law), the
+ *  better half kept, then updateHyp3D's refit on at most 1000 inliers
+ *  (filterInliers3D picks on streams (h, 'F3D', 1024 r + k)); the survivor with
+ *  more than 10 inliers refined by a bounded Nelder-Mead (nm_evals evaluations,
+ *  100 in the reference) of optEnergy3D over (Rodrigues vector, t).
+ *  Outputs (device): poses_out (3,4,C); hyps_out (n_hyp,13); hyp_px (n_hyp,3);
+ *  inl_out (n_hyp,8); final_out (C,3) as pcnn_pose2d; energy_out (C) the
+ *  refined optEnergy3D (0: not refined); eye_out (H,W,3) camera coordinates,
+ *  optional (NULL: not written).  Asynchronous on `stream`. */
+size_t pcnn_pose3d_workspace_size(int H, int W, int C, int n_hyp);
+int pcnn_pose3d(const int32_t* label, const uint16_t* depth, const float* vertmap, const float* extents, int H, int W,
+                int C, float fx, float fy, float px, float py, float depth_factor, uint64_t seed, int n_hyp,
+                int max_iter, int nm_evals, float* poses_out, float* hyps_out, int32_t* hyp_px, int32_t* inl_out,
+                int32_t* final_out, float* energy_out, float* eye_out, void* workspace, size_t workspace_bytes,
+                void* stream);
+
 /* Column sums over the first min(*M_dev, M) rows: out[n] = sum_m X[m, n] (bias gradients). */
 int pcnn_colsum(const float* X, int M, int N, int ldx, const int32_t* M_dev, float* out, void* stream);
 

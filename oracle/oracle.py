@@ -387,3 +387,35 @@ def pose2d(label, vertmap, extents, fx, fy, px, py, seed=1305, n_hyp=256, max_it
                          hyps.ctypes.data_as(F32P), hpx.ctypes.data_as(I32P), inl.ctypes.data_as(I32P),
                          fin.ctypes.data_as(I32P))
     return dict(poses=poses, hyps=hyps, hyp_px=hpx, inliers=inl, final=fin, n_obj=n)
+
+
+def pose3d(label, depth, vertmap, extents, fx, fy, px, py, depth_factor, seed=1305, n_hyp=256, max_iter=100000,
+           nm_evals=100):
+    """Synthesizer::estimatePose3D restated (orc_pose2d.cpp, orc_pose3d).
+    depth (H, W) uint16 raw depth.  Returns dict: poses (3, 4, C) in the
+    reference's output layout, eye (H, W, 3) camera coordinates, hyps
+    (n_hyp, 13) [objID | R | t], hyp_px (n_hyp, 3), inliers (n_hyp, 8) per
+    preemptive round, final (C, 3) [h, inliers, hypotheses], energy (C)
+    optEnergy3D at the refined pose, n_obj."""
+    label, lp = _i(label)
+    depth = np.ascontiguousarray(depth, np.uint16)
+    vertmap, vp = _f(vertmap)
+    extents, ep = _f(extents)
+    H, W = label.shape
+    assert depth.shape == (H, W)
+    C = extents.shape[0]
+    poses = np.zeros((3, 4, C), np.float32)
+    eye = np.zeros((H, W, 3), np.float32)
+    hyps = np.zeros((n_hyp, 13), np.float32)
+    hpx = np.zeros((n_hyp, 3), np.int32)
+    inl = np.zeros((n_hyp, 8), np.int32)
+    fin = np.zeros((C, 3), np.int32)
+    en = np.zeros(C, np.float32)
+    lib().orc_pose3d.restype = ctypes.c_int
+    n = lib().orc_pose3d(lp, depth.ctypes.data_as(ctypes.POINTER(ctypes.c_uint16)), vp, ep, H, W, C,
+                         ctypes.c_float(fx), ctypes.c_float(fy), ctypes.c_float(px), ctypes.c_float(py),
+                         ctypes.c_float(depth_factor), ctypes.c_uint64(seed), n_hyp, max_iter, nm_evals,
+                         poses.ctypes.data_as(F32P), eye.ctypes.data_as(F32P), hyps.ctypes.data_as(F32P),
+                         hpx.ctypes.data_as(I32P), inl.ctypes.data_as(I32P), fin.ctypes.data_as(I32P),
+                         en.ctypes.data_as(F32P))
+    return dict(poses=poses, eye=eye, hyps=hyps, hyp_px=hpx, inliers=inl, final=fin, energy=en, n_obj=n)

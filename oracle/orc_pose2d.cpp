@@ -437,3 +437,534 @@ ORC_API int orc_pose2d(const int* label, const float* vertmap, const float* exte
   }
   return (int)objs.size();
 }
+
+// ===========================================================================
+// Depth-based pose estimation: Synthesizer::estimatePose3D
+// (lib/synthesize/synthesize.cpp:1769-1965), reached through synthesizer.pyx:
+// 86-95 estimate_poses_3d from lib/fcn/test.py:1385 (cfg.TEST.VERTEX_REG_3D;
+// its poses then go to refine_poses, test.py:1403-1416).  Restated pieces:
+//   getEye / pxToEye (:1383-1410): camera coordinates of the depth map;
+//   getLabels (as estimatePose2D), samplePoint3D (:1105-1134) x 3,
+//   Hypothesis(pts3D) = calcRigidBodyTransform (Hypothesis.cpp:178-246:
+//   centroids, the 3x3 covariance, SVD, the sign fix, R = V D U^T,
+//   t = cB - R cA), the reconstruction check (< 1 cm), getBB2D area >= 400;
+//   the preemptive loop (:1889-1926) with countInliers3D (:1227-1280: depth
+//   holes step to the next pixel without a draw; inliers < 1 cm), the stable
+//   halving, updateHyp3D (:1347-1370: >= 4 inliers, filterInliers3D
+//   (:1308-1322) then the refit); the final refineWithOpt(.., 100, is_3D)
+//   (:1510-1567) over optEnergy3D (:1464-1507) when inliers > 10, and the
+//   output layout (:1941-1963).
+// Deliberate, documented choices (parity unpinned: OpenCV, NLopt absent):
+//   * RNG: Philox streams as estimatePose2D: attempt a of hypothesis h on
+//     (draw, h, 'P3D', a); the rounds' pixel skips on (j, class, 'SUB0' + r)
+//     with the inverse-CDF geometric law of the 2-D restatement (the same
+//     streams); filterInliers3D's picks (irand with replacement) on
+//     (draw, h, 'F3D', 1024 r + k) for pick k, r = the round (0-7) or 8 for
+//     the final filter.
+//   * cv::SVD of the covariance is restated as a one-sided Jacobi (fixed
+//     pivot order, rotations skipped below 1e-15 relative, at most 16
+//     sweeps), singular values sorted descending, the third left vector the
+//     cross product of the first two when its singular value is below 1e-9 of
+//     the first (three-point covariances have rank two): R = V D U^T does
+//     not depend on the SVD's sign conventions.  The centroid and covariance
+//     sums run in the GPU wave's fold64 order (OpenCV: sequential).
+//   * sin, cos, acos (Rodrigues) from + - * / sqrt only (dsincos, dacos), so
+//     the GPU reproduces them bit for bit; libm differs in the last ulp.
+//   * Hypothesis poses stay (R, t) between steps; the reference round-trips
+//     them through Rodrigues vectors (our2cv / cv2our), a change at rounding
+//     level.
+//   * refineWithOpt's NLopt LN_NELDERMEAD is the bounded Nelder-Mead of
+//     posecnn_amd/synthesize/icp.py nelder_mead_steps (6 parameters: Rodrigues
+//     vector and translation, +-10 deg / +-0.1 / +-0.1 / +-0.5 m bounds, 100
+//     evaluations); optEnergy3D's float sum of double distances is taken as
+//     64 strided float partial sums folded by halving (i < off: p[i] +=
+//     p[i + off]), the order the GPU's wave uses.
+namespace {
+
+struct TStream {  // Philox words of the stream (draw, h, tag, a)
+  uint32_t k0, k1, h, tag, a, ctr = 0;
+  int word = 4;
+  U4 buf;
+  TStream(uint64_t seed, uint32_t hyp, uint32_t tg, uint32_t attempt)
+      : k0((uint32_t)seed), k1((uint32_t)(seed >> 32)), h(hyp), tag(tg), a(attempt) {}
+  uint32_t next() {
+    if (word == 4) {
+      buf = philox(U4{{ctr++, h, tag, a}}, k0, k1);
+      word = 0;
+    }
+    return buf.v[word++];
+  }
+  int uniform(int n) {
+    const uint32_t un = (uint32_t)n;
+    const uint32_t lim = (uint32_t)(0x100000000ull - (0x100000000ull % un));
+    uint32_t x;
+    do { x = next(); } while (lim != 0 && x >= lim);
+    return (int)(x % un);
+  }
+};
+constexpr uint32_t kTagP3D = 0x50334400u, kTagF3D = 0x46334400u;
+
+// one-sided Jacobi SVD of a 3x3 (row-major): A = U diag(S) V^T, S descending
+void svd3(const double* A, double* U, double* S, double* V) {
+  double M[9], Vm[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+  for (int i = 0; i < 9; i++) M[i] = A[i];
+  const int pq[3][2] = {{0, 1}, {0, 2}, {1, 2}};
+  for (int sweep = 0; sweep < 16; sweep++) {
+    bool rot = false;
+    for (int k = 0; k < 3; k++) {
+      const int p = pq[k][0], q = pq[k][1];
+      double al = 0, be = 0, ga = 0;
+      for (int r = 0; r < 3; r++) {
+        al = al + M[r * 3 + p] * M[r * 3 + p];
+        be = be + M[r * 3 + q] * M[r * 3 + q];
+        ga = ga + M[r * 3 + p] * M[r * 3 + q];
+      }
+      if (ga == 0.0 || std::fabs(ga) <= 1e-15 * std::sqrt(al * be)) continue;
+      const double zeta = (be - al) / (2.0 * ga);
+      const double t = (zeta >= 0 ? 1.0 : -1.0) / (std::fabs(zeta) + std::sqrt(1.0 + zeta * zeta));
+      const double c = 1.0 / std::sqrt(1.0 + t * t), s = c * t;
+      for (int r = 0; r < 3; r++) {
+        const double mp = M[r * 3 + p], mq = M[r * 3 + q];
+        M[r * 3 + p] = c * mp - s * mq;
+        M[r * 3 + q] = s * mp + c * mq;
+        const double vp = Vm[r * 3 + p], vq = Vm[r * 3 + q];
+        Vm[r * 3 + p] = c * vp - s * vq;
+        Vm[r * 3 + q] = s * vp + c * vq;
+      }
+      rot = true;
+    }
+    if (!rot) break;
+  }
+  double sv[3];
+  for (int i = 0; i < 3; i++) {
+    double a = 0;
+    for (int r = 0; r < 3; r++) a = a + M[r * 3 + i] * M[r * 3 + i];
+    sv[i] = std::sqrt(a);
+  }
+  int o[3] = {0, 1, 2};  // descending, stable
+  for (int i = 1; i < 3; i++)
+    for (int j = i; j > 0 && sv[o[j]] > sv[o[j - 1]]; j--) std::swap(o[j], o[j - 1]);
+  for (int k = 0; k < 3; k++) {
+    S[k] = sv[o[k]];
+    for (int r = 0; r < 3; r++) {
+      V[r * 3 + k] = Vm[r * 3 + o[k]];
+      U[r * 3 + k] = S[k] > 0 ? M[r * 3 + o[k]] / S[k] : 0.0;
+    }
+  }
+  if (!(S[2] > 1e-9 * S[0])) {  // rank two: complete U
+    U[0 * 3 + 2] = U[1 * 3 + 0] * U[2 * 3 + 1] - U[2 * 3 + 0] * U[1 * 3 + 1];
+    U[1 * 3 + 2] = U[2 * 3 + 0] * U[0 * 3 + 1] - U[0 * 3 + 0] * U[2 * 3 + 1];
+    U[2 * 3 + 2] = U[0 * 3 + 0] * U[1 * 3 + 1] - U[1 * 3 + 0] * U[0 * 3 + 1];
+  }
+}
+
+double det3(const double* m) {
+  return m[0] * (m[4] * m[8] - m[5] * m[7]) - m[1] * (m[3] * m[8] - m[5] * m[6]) + m[2] * (m[3] * m[7] - m[4] * m[6]);
+}
+
+// 64 strided partial sums folded by halving -- the order of a wave that
+// gives lane l the elements l, l + 64, ... and then adds p[i + off] into p[i]
+// for off = 32, 16, ..., 1 (posecnn_amd/csrc/pose2d.hip fold64)
+template <class F>
+double fold64(F x, int n) {
+  double p[64];
+  for (int l = 0; l < 64; l++) {
+    p[l] = 0.0;
+    for (int i = l; i < n; i += 64) p[l] = p[l] + x(i);
+  }
+  for (int off = 32; off >= 1; off >>= 1)
+    for (int i = 0; i < off; i++) p[i] = p[i] + p[i + off];
+  return p[0];
+}
+
+// calcRigidBodyTransform (Hypothesis.cpp:186-241): b ~ R a + t.  The
+// centroid and covariance sums in fold64 order (OpenCV: sequential).
+Pose kabsch(const V3* a, const V3* b, int n) {
+  const double inv = 1.0 / (double)n;
+  const V3 cA{fold64([&](int i) { return a[i].x; }, n) * inv, fold64([&](int i) { return a[i].y; }, n) * inv,
+              fold64([&](int i) { return a[i].z; }, n) * inv};
+  const V3 cB{fold64([&](int i) { return b[i].x; }, n) * inv, fold64([&](int i) { return b[i].y; }, n) * inv,
+              fold64([&](int i) { return b[i].z; }, n) * inv};
+  double H[9];  // pointsA * pointsB^T
+  for (int r = 0; r < 3; r++)
+    for (int c = 0; c < 3; c++)
+      H[r * 3 + c] = fold64(
+          [&](int i) {
+            const double pa = r == 0 ? a[i].x - cA.x : r == 1 ? a[i].y - cA.y : a[i].z - cA.z;
+            const double pb = c == 0 ? b[i].x - cB.x : c == 1 ? b[i].y - cB.y : b[i].z - cB.z;
+            return pa * pb;
+          },
+          n);
+  double U[9], S[3], V[9];
+  svd3(H, U, S, V);
+  double VU[9];  // V U^T
+  for (int r = 0; r < 3; r++)
+    for (int c = 0; c < 3; c++) VU[r * 3 + c] = V[r * 3 + 0] * U[c * 3 + 0] + V[r * 3 + 1] * U[c * 3 + 1] + V[r * 3 + 2] * U[c * 3 + 2];
+  const double sg = det3(VU) < 0 ? -1.0 : 1.0;
+  Pose P;
+  for (int r = 0; r < 3; r++)  // V diag(1, 1, sg) U^T
+    for (int c = 0; c < 3; c++)
+      P.R[r * 3 + c] = V[r * 3 + 0] * U[c * 3 + 0] + V[r * 3 + 1] * U[c * 3 + 1] + (V[r * 3 + 2] * sg) * U[c * 3 + 2];
+  const double ca[3] = {cA.x, cA.y, cA.z}, cb[3] = {cB.x, cB.y, cB.z};
+  for (int r = 0; r < 3; r++) P.t[r] = -(P.R[r * 3 + 0] * ca[0] + P.R[r * 3 + 1] * ca[1] + P.R[r * 3 + 2] * ca[2]) + cb[r];
+  return P;
+}
+
+V3 xform(const Pose& P, V3 p) {  // Hypothesis::transform
+  return {P.R[0] * p.x + P.R[1] * p.y + P.R[2] * p.z + P.t[0], P.R[3] * p.x + P.R[4] * p.y + P.R[5] * p.z + P.t[1],
+          P.R[6] * p.x + P.R[7] * p.y + P.R[8] * p.z + P.t[2]};
+}
+
+// sin / cos / acos from + - * / and sqrt only, so that the device computes
+// the same bits (posecnn_amd/csrc/pose2d.hip): quadrant reduction by a
+// two-part pi/2, the fdlibm kernel polynomials; acos by the half-angle
+// identity and 6 Newton steps on asin
+void dsincos(double x, double& s, double& c) {
+  const double n = std::floor(x * 0.63661977236758134308 + 0.5);
+  const double y = (x - n * 1.57079632673412561417e+00) - n * 6.07710050650619224932e-11;
+  const double z = y * y;
+  const double ks = y + y * z * (-1.66666666666666324348e-01 + z * (8.33333333332248946124e-03 + z * (-1.98412698298579493134e-04 +
+                        z * (2.75573137070700676789e-06 + z * (-2.50507602534068634195e-08 + z * 1.58969099521155010221e-10)))));
+  const double kc = 1.0 - (0.5 * z - z * z * (4.16666666666666019037e-02 + z * (-1.38888888888741095749e-03 + z * (2.48015872894767294178e-05 +
+                        z * (-2.75573143513906633035e-07 + z * (2.08757232129817482790e-09 + z * -1.13596475577881948265e-11))))));
+  const int q = ((int)n) & 3;
+  s = q == 0 ? ks : q == 1 ? kc : q == 2 ? -ks : -kc;
+  c = q == 0 ? kc : q == 1 ? -ks : q == 2 ? -kc : ks;
+}
+
+double dasin_small(double x) {  // |x| <= sqrt(1/2)
+  double y = x;
+  for (int i = 0; i < 6; i++) {
+    double s, c;
+    dsincos(y, s, c);
+    y = y - (s - x) / c;
+  }
+  return y;
+}
+
+double dacos(double c) {  // c in [-1, 1]
+  if (c >= 0) return 2.0 * dasin_small(std::sqrt((1.0 - c) * 0.5));
+  return 3.14159265358979311600 - 2.0 * dasin_small(std::sqrt((1.0 + c) * 0.5));
+}
+
+// cv::Rodrigues, vector -> matrix
+void rod_v2m(const double* r, double* R) {
+  const double th = std::sqrt(r[0] * r[0] + r[1] * r[1] + r[2] * r[2]);
+  if (th < DBL_EPSILON) {
+    for (int i = 0; i < 9; i++) R[i] = (i % 4 == 0) ? 1.0 : 0.0;
+    return;
+  }
+  double s, c;
+  dsincos(th, s, c);
+  const double c1 = 1.0 - c, it = 1.0 / th;
+  const double x = r[0] * it, y = r[1] * it, z = r[2] * it;
+  const double rrt[9] = {x * x, x * y, x * z, x * y, y * y, y * z, x * z, y * z, z * z};
+  const double rx[9] = {0, -z, y, z, 0, -x, -y, x, 0};
+  for (int i = 0; i < 9; i++) R[i] = c * ((i % 4 == 0) ? 1.0 : 0.0) + c1 * rrt[i] + s * rx[i];
+}
+
+// cv::Rodrigues, matrix -> vector (cvRodrigues2 without its SVD re-orthonormalisation)
+void rod_m2v(const double* R, double* r) {
+  double rx = R[7] - R[5], ry = R[2] - R[6], rz = R[3] - R[1];
+  const double s = std::sqrt((rx * rx + ry * ry + rz * rz) * 0.25);
+  double c = (R[0] + R[4] + R[8] - 1) * 0.5;
+  c = c > 1. ? 1. : c < -1. ? -1. : c;
+  double th = dacos(c);
+  if (s < 1e-5) {
+    if (c > 0) {
+      rx = ry = rz = 0;
+    } else {
+      double t = (R[0] + 1) * 0.5;
+      rx = std::sqrt(std::max(t, 0.));
+      t = (R[4] + 1) * 0.5;
+      ry = std::sqrt(std::max(t, 0.)) * (R[1] < 0 ? -1. : 1.);
+      t = (R[8] + 1) * 0.5;
+      rz = std::sqrt(std::max(t, 0.)) * (R[2] < 0 ? -1. : 1.);
+      if (std::fabs(rx) < std::fabs(ry) && std::fabs(rx) < std::fabs(rz) && (R[5] > 0) != (ry * rz > 0)) rz = -rz;
+      th /= std::sqrt(rx * rx + ry * ry + rz * rz);
+      rx *= th;
+      ry *= th;
+      rz *= th;
+    }
+  } else {
+    double vth = 1 / (2 * s);
+    vth *= th;
+    rx *= vth;
+    ry *= vth;
+    rz *= vth;
+  }
+  r[0] = rx;
+  r[1] = ry;
+  r[2] = rz;
+}
+
+struct Corr { F3 obj, eye; };  // an inlier correspondence (obj coordinate, camera coordinate)
+
+// filterInliers3D (:1308-1322): at least maxInliers -> maxInliers picks with
+// replacement; pick k of round r draws from its own stream (draw, h, 'F3D',
+// 1024 r + k), so the picks are independent of each other
+std::vector<Corr> filter3d(const std::vector<Corr>& in, uint64_t seed, int h, int r) {
+  if ((int)in.size() < 1000) return in;
+  std::vector<Corr> out;
+  for (int k = 0; k < 1000; k++) {
+    TStream rs(seed, (uint32_t)h, kTagF3D, (uint32_t)(1024 * r + k));
+    out.push_back(in[rs.uniform((int)in.size())]);
+  }
+  return out;
+}
+
+Pose kabsch_corr(const std::vector<Corr>& v) {
+  std::vector<V3> a(v.size()), b(v.size());
+  for (size_t i = 0; i < v.size(); i++) {
+    a[i] = {v[i].obj.x, v[i].obj.y, v[i].obj.z};
+    b[i] = {v[i].eye.x, v[i].eye.y, v[i].eye.z};
+  }
+  return kabsch(a.data(), b.data(), (int)v.size());
+}
+
+// optEnergy3D (:1464-1507): mean distance of the transformed object
+// coordinates to the camera coordinates; the float sum in the GPU's order
+double energy3d(const double* x, const std::vector<Corr>& v) {
+  double Rd[9];
+  rod_v2m(x, Rd);
+  float Rf[9];
+  for (int i = 0; i < 9; i++) Rf[i] = (float)Rd[i];  // jp::double2float
+  float part[64] = {0};
+  for (size_t i = 0; i < v.size(); i++) {
+    const F3 o = v[i].obj;
+    float tr[3];
+    for (int r = 0; r < 3; r++) {
+      const float m = Rf[r * 3 + 0] * o.x + Rf[r * 3 + 1] * o.y + Rf[r * 3 + 2] * o.z;
+      tr[r] = (float)((double)m + x[3 + r]);
+    }
+    const double dx = (double)tr[0] - (double)v[i].eye.x, dy = (double)tr[1] - (double)v[i].eye.y,
+                 dz = (double)tr[2] - (double)v[i].eye.z;
+    float& p = part[i % 64];
+    p = (float)((double)p + std::sqrt(dx * dx + dy * dy + dz * dz));
+  }
+  for (int off = 32; off >= 1; off >>= 1)
+    for (int i = 0; i < off; i++) part[i] = part[i] + part[i + off];
+  return (double)(part[0] / (float)v.size());
+}
+
+// the bounded Nelder-Mead of icp.py nelder_mead_steps (n parameters)
+template <class F>
+void nelder_mead(F f, int n, const double* x0, const double* lb, const double* ub, int max_eval, double* xbest,
+                 double* fbest) {
+  std::vector<std::vector<double>> pts(n + 1, std::vector<double>(x0, x0 + n));
+  std::vector<double> vals(n + 1);
+  for (int i = 0; i < n; i++) {
+    const double st = std::min(0.25 * (ub[i] - lb[i]), std::min(0.75 * (ub[i] - x0[i]), 0.75 * (x0[i] - lb[i])));
+    pts[i + 1][i] = x0[i] + st;
+    for (int e = 0; e < n; e++)
+      if (e != i) pts[i + 1][e] = x0[e] + 0.0;
+  }
+  for (int i = 0; i <= n; i++) vals[i] = f(pts[i].data());
+  int nev = n + 1;
+  auto clamp = [&](int e, double v) { return std::min(std::max(v, lb[e]), ub[e]); };
+  std::vector<double> c(n), xr(n), xe(n), xc(n);
+  while (nev < max_eval) {
+    for (int i = 1; i <= n; i++)
+      for (int j = i; j > 0 && vals[j] < vals[j - 1]; j--) {
+        std::swap(vals[j], vals[j - 1]);
+        std::swap(pts[j], pts[j - 1]);
+      }
+    for (int e = 0; e < n; e++) {
+      double s = pts[0][e];
+      for (int i = 1; i < n; i++) s = s + pts[i][e];
+      c[e] = s / (double)n;
+    }
+    for (int e = 0; e < n; e++) xr[e] = clamp(e, c[e] + (c[e] - pts[n][e]));
+    const double fr = f(xr.data());
+    nev++;
+    if (fr < vals[0] && nev < max_eval) {
+      for (int e = 0; e < n; e++) xe[e] = clamp(e, c[e] + 2.0 * (c[e] - pts[n][e]));
+      const double fe = f(xe.data());
+      nev++;
+      if (fe < fr) { pts[n] = xe; vals[n] = fe; } else { pts[n] = xr; vals[n] = fr; }
+    } else if (fr < vals[n - 1]) {
+      pts[n] = xr;
+      vals[n] = fr;
+    } else if (nev < max_eval) {
+      for (int e = 0; e < n; e++)
+        xc[e] = fr >= vals[n] ? clamp(e, c[e] + 0.5 * (pts[n][e] - c[e])) : clamp(e, c[e] + 0.5 * (xr[e] - c[e]));
+      const double fc = f(xc.data());
+      nev++;
+      if (fc < std::min(fr, vals[n])) {
+        pts[n] = xc;
+        vals[n] = fc;
+      } else {
+        const int m = std::min(n, max_eval - nev);
+        for (int i = 1; i <= m; i++) {
+          for (int e = 0; e < n; e++) pts[i][e] = clamp(e, pts[0][e] + 0.5 * (pts[i][e] - pts[0][e]));
+          vals[i] = f(pts[i].data());
+        }
+        nev += m > 0 ? m : 0;
+      }
+    }
+  }
+  int b = 0;
+  for (int i = 1; i <= n; i++)
+    if (vals[i] < vals[b]) b = i;
+  for (int e = 0; e < n; e++) xbest[e] = pts[b][e];
+  *fbest = vals[b];
+}
+
+struct Hyp3 { int h, obj, inliers = 0; Pose pose; std::vector<Corr> corr; };
+
+}  // namespace
+
+// eye_out (H, W, 3) camera coordinates; hyps_out (n_hyp, 13) [objID | R | t];
+// hyp_px (n_hyp, 3); inl_out (n_hyp, 8) inliers per round (-1 not queued);
+// final_out (C, 3) [h, inliers, hypotheses]; energy_out (C) optEnergy3D at the
+// refined pose (0 when not refined); poses_out (3, 4, C).  Returns n objects.
+ORC_API int orc_pose3d(const int* label, const uint16_t* depth, const float* vertmap, const float* extents, int H,
+                       int W, int C, float fx, float fy, float px, float py, float depth_factor, uint64_t seed,
+                       int n_hyp, int max_iter, int nm_evals, float* poses_out, float* eye_out, float* hyps_out,
+                       int* hyp_px, int* inl_out, int* final_out, float* energy_out) {
+  const Cam k{fx, fy, px, py};
+  // getEye / pxToEye: float arithmetic, holes (depth 0) at the origin
+  for (int y = 0; y < H; y++)
+    for (int x = 0; x < W; x++) {
+      const int p = y * W + x;
+      const unsigned short d = depth[p];
+      float* e = eye_out + (size_t)p * 3;
+      if (d == 0) {
+        e[0] = e[1] = e[2] = 0.f;
+      } else {
+        e[0] = ((float)x - px) * (float)d / fx / depth_factor;
+        e[1] = ((float)y - py) * (float)d / fy / depth_factor;
+        e[2] = (float)d / depth_factor;
+      }
+    }
+  auto eye_at = [&](int p) { return F3{eye_out[(size_t)p * 3], eye_out[(size_t)p * 3 + 1], eye_out[(size_t)p * 3 + 2]}; };
+  std::vector<std::vector<int>> labels(C);
+  for (int x = 0; x < W; x++)
+    for (int y = 0; y < H; y++) labels[label[y * W + x]].push_back(y * W + x);
+  std::vector<int> objs;
+  for (int c = 1; c < C; c++)
+    if ((float)labels[c].size() > 400.0f) objs.push_back(c);
+  for (int i = 0; i < n_hyp * 13; i++) hyps_out[i] = 0;
+  for (int i = 0; i < n_hyp; i++) hyps_out[i * 13] = -1;
+  for (int i = 0; i < n_hyp * 3; i++) hyp_px[i] = -1;
+  for (int i = 0; i < n_hyp * 8; i++) inl_out[i] = -1;
+  for (int i = 0; i < C * 3; i++) final_out[i] = -1;
+  for (int i = 0; i < C; i++) energy_out[i] = 0.f;
+  for (int i = 0; i < 12 * C; i++) poses_out[i] = 0.f;
+  if (objs.empty()) return 0;
+  std::vector<std::vector<Hyp3>> hypmap(C);
+  for (int h = 0; h < n_hyp; h++) {
+    for (int it = 0; it < max_iter; it++) {
+      TStream rs(seed, (uint32_t)h, kTagP3D, (uint32_t)it);
+      const int obj = objs[rs.uniform((int)objs.size())];
+      const auto& L = labels[obj];
+      F3 E[3], O[3];
+      int px3[3], n = 0;
+      bool ok = true;
+      for (int s = 0; s < 3 && ok; s++) {  // samplePoint3D x 3
+        const int idx = L[rs.uniform((int)L.size())];
+        const F3 eye = eye_at(idx);
+        if (eye.z == 0) { ok = false; break; }
+        double md = -1;
+        for (int q = 0; q < n; q++) md = md < 0 ? norm3f(E[q], eye) : std::min(md, norm3f(E[q], eye));
+        if (md > 0 && md < 0.01) { ok = false; break; }
+        const F3 o = mode3d(vertmap, extents, C, obj, idx);
+        if (o.x == 0 && o.y == 0 && o.z == 0) { ok = false; break; }
+        md = -1;
+        for (int q = 0; q < n; q++) md = md < 0 ? norm3f(O[q], o) : std::min(md, norm3f(O[q], o));
+        if (md > 0 && md < 0.01) { ok = false; break; }
+        E[n] = eye;
+        O[n] = o;
+        px3[n] = idx;
+        n++;
+      }
+      if (!ok) continue;
+      V3 a[3], b[3];
+      for (int q = 0; q < 3; q++) {
+        a[q] = {O[q].x, O[q].y, O[q].z};
+        b[q] = {E[q].x, E[q].y, E[q].z};
+      }
+      const Pose P = kabsch(a, b, 3);
+      bool out = false;
+      for (int q = 0; q < 3 && !out; q++) out = !(nrm(b[q] - xform(P, a[q])) < 0.01);  // :1853-1860
+      if (out) continue;
+      const float e0 = extents[obj * 3] * 0.5f, e1 = extents[obj * 3 + 1] * 0.5f, e2 = extents[obj * 3 + 2] * 0.5f;
+      const F3 bb3[8] = {{e0, e1, e2}, {-e0, e1, e2}, {e0, -e1, e2}, {-e0, -e1, e2},
+                         {e0, e1, -e2}, {-e0, e1, -e2}, {e0, -e1, -e2}, {-e0, -e1, -e2}};
+      if ((float)bb_area(P, bb3, k, W, H) < 400.0f) continue;  // :1871-1875
+      Hyp3 hy;
+      hy.h = h;
+      hy.obj = obj;
+      hy.pose = P;
+      hypmap[obj].push_back(hy);
+      hyps_out[h * 13] = (float)obj;
+      for (int i = 0; i < 9; i++) hyps_out[h * 13 + 1 + i] = (float)P.R[i];
+      for (int i = 0; i < 3; i++) hyps_out[h * 13 + 10 + i] = (float)P.t[i];
+      for (int i = 0; i < 3; i++) hyp_px[h * 3 + i] = px3[i];
+      break;
+    }
+  }
+  for (int c = 0; c < C; c++) {
+    auto& hs = hypmap[c];
+    if (hs.empty()) continue;
+    const auto& L = labels[c];
+    const int N = (int)L.size();
+    for (int round = 1; round <= 8; round++) {
+      const int maxPixels = 1000 * round;
+      const float rate = maxPixels / (float)N;
+      const double q = 1.0 - (double)rate;
+      std::vector<int> sub;  // visited pixels (holes step to the next pixel without a draw)
+      for (int i = 0, j = 0; i < N;) {
+        if (eye_at(L[i]).z == 0) { i++; continue; }
+        sub.push_back(L[i]);
+        if (rate < 1) i += subset_gap(seed, c, round - 1, j++, q);
+        else i++;
+      }
+      for (auto& hy : hs) {
+        hy.corr.clear();
+        for (int p : sub) {
+          const F3 e = eye_at(p);
+          const F3 o = mode3d(vertmap, extents, C, c, p);
+          const V3 d = V3{e.x, e.y, e.z} - xform(hy.pose, V3{o.x, o.y, o.z});
+          if (nrm(d) < 0.01) hy.corr.push_back(Corr{o, e});
+        }
+        hy.inliers = (int)hy.corr.size();
+        inl_out[hy.h * 8 + round - 1] = hy.inliers;
+      }
+      if (hs.size() > 1) {
+        std::stable_sort(hs.begin(), hs.end(), [](const Hyp3& a, const Hyp3& b) { return a.inliers > b.inliers; });
+        hs.erase(hs.begin() + hs.size() / 2, hs.end());
+      }
+      for (auto& hy : hs) {  // updateHyp3D (:1347-1370)
+        if (hy.corr.size() < 4) continue;
+        hy.corr = filter3d(hy.corr, seed, hy.h, round - 1);
+        hy.pose = kabsch_corr(hy.corr);
+      }
+    }
+    Hyp3& w = hs[0];
+    final_out[c * 3] = w.h;
+    final_out[c * 3 + 1] = w.inliers;
+    int nh = 0;
+    for (int h = 0; h < n_hyp; h++) nh += hyps_out[h * 13] == (float)c;
+    final_out[c * 3 + 2] = nh;
+    Pose P = w.pose;
+    if (w.inliers > 10) {  // :1939-1944
+      const std::vector<Corr> v = filter3d(w.corr, seed, w.h, 8);
+      double x0[6], lb[6], ub[6], xb[6], fb;
+      rod_m2v(P.R, x0);
+      for (int i = 0; i < 3; i++) x0[3 + i] = P.t[i];
+      const double rng[6] = {10 * 3.1415926 / 180, 10 * 3.1415926 / 180, 10 * 3.1415926 / 180, 0.1, 0.1, 0.5};
+      for (int i = 0; i < 6; i++) {
+        lb[i] = x0[i] - rng[i];
+        ub[i] = x0[i] + rng[i];
+      }
+      nelder_mead([&](const double* x) { return energy3d(x, v); }, 6, x0, lb, ub, nm_evals, xb, &fb);
+      rod_v2m(xb, P.R);
+      for (int i = 0; i < 3; i++) P.t[i] = xb[3 + i];
+      energy_out[c] = (float)fb;
+    }
+    for (int y = 0; y < 3; y++)
+      for (int x = 0; x < 4; x++) poses_out[c + C * (y * 4 + x)] = x < 3 ? (float)P.R[y * 3 + x] : (float)P.t[y];
+  }
+  return (int)objs.size();
+}

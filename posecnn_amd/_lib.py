@@ -85,6 +85,10 @@ _SIGS = {
     "pcnn_pose2d": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_float, c_float, c_float,
                             ctypes.c_uint64, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                             c_size_t, c_void_p]),
+    "pcnn_pose3d_workspace_size": (c_size_t, [c_int, c_int, c_int, c_int]),
+    "pcnn_pose3d": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_float, c_float,
+                            c_float, c_float, ctypes.c_uint64, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
+                            c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
     "pcnn_tp_bytes": (c_size_t, [c_int, c_int]),
     "pcnn_split_tp": (c_int, [c_void_p, ctypes.c_long, ctypes.c_long, c_int, c_void_p, c_int, c_void_p, c_void_p,
                               c_size_t, c_void_p]),

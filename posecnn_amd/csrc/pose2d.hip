@@ -66,16 +66,18 @@ __device__ __forceinline__ U4 philox(U4 c, uint32_t k0, uint32_t k1) {
   return c;
 }
 
-// attempt a of hypothesis h draws Philox4x32-10 blocks (draw / 4, h, 'P2D', a), words in order
+// attempt a of hypothesis h draws Philox4x32-10 blocks (draw / 4, h, tag, a),
+// words in order; tags 'P2D' (estimatePose2D), 'P3D' / 'F3D' (estimatePose3D)
+constexpr uint32_t kTagP2D = 0x50324400u, kTagP3D = 0x50334400u, kTagF3D = 0x46334400u;
 struct Stream {
-  uint32_t k0, k1, h, a, ctr;
+  uint32_t k0, k1, h, tag, a, ctr;
   int word;
   U4 buf;
-  __device__ Stream(uint64_t seed, uint32_t hyp, uint32_t attempt)
-      : k0((uint32_t)seed), k1((uint32_t)(seed >> 32)), h(hyp), a(attempt), ctr(0), word(4), buf{0, 0, 0, 0} {}
+  __device__ Stream(uint64_t seed, uint32_t hyp, uint32_t tg, uint32_t attempt)
+      : k0((uint32_t)seed), k1((uint32_t)(seed >> 32)), h(hyp), tag(tg), a(attempt), ctr(0), word(4), buf{0, 0, 0, 0} {}
   __device__ uint32_t next() {
     if (word == 4) {
-      buf = philox(U4{ctr++, h, 0x50324400u, a}, k0, k1);
+      buf = philox(U4{ctr++, h, tag, a}, k0, k1);
       word = 0;
     }
     const uint32_t v = word == 0 ? buf.x : word == 1 ? buf.y : word == 2 ? buf.z : buf.w;
@@ -410,22 +412,11 @@ __device__ __forceinline__ int p2d_gap(uint64_t seed, int c, int r, int j, doubl
   return k > 1 ? k : 1;
 }
 
-__global__ void __launch_bounds__(1024) k_p2d_subset(uint64_t seed, P2dWs ws) {
-  __shared__ int wsum[16];
-  __shared__ int carry_s;
-  const int c = blockIdx.x, r = blockIdx.y, t = threadIdx.x, lane = pcnn::lane_id(), wave = t >> 6;
-  const int N = ws.count[c];
-  if (c == 0 || !((float)N > 400.0f)) return;  // not an object (block-uniform)
-  int* S = ws.sub + (size_t)kRounds * ws.listoff[c] + (size_t)r * N;
-  const int maxPixels = 1000 * (r + 1);
-  const float rate = maxPixels / (float)N;  // :1191
-  if (!(rate < 1)) {  // every pixel (:1212-1213)
-    for (int i = t; i < N; i += blockDim.x) S[i] = i;
-    if (t == 0) ws.subcnt[c * kRounds + r] = N;
-    return;
-  }
-  const double q = 1.0 - (double)rate;
-  int carry = 0;  // s_{j0}
+// the gap walk of a class list without depth holes: 1024 gaps at a time,
+// placed by a block scan (block-uniform control flow; wsum: 16 ints of LDS)
+__device__ void subset_nohole(uint64_t seed, int c, int r, int N, double q, int* S, int* subcnt, int* wsum) {
+  const int t = threadIdx.x, lane = pcnn::lane_id(), wave = t >> 6;
+  long carry = 0;  // s_{j0}
   for (int j0 = 0;; j0 += 1024) {
     const int g = p2d_gap(seed, c, r, j0 + t, q);
     int incl = g;  // block inclusive scan of the gaps
@@ -436,19 +427,34 @@ __global__ void __launch_bounds__(1024) k_p2d_subset(uint64_t seed, P2dWs ws) {
     }
     if (lane == 63) wsum[wave] = incl;
     __syncthreads();
-    int wb = 0, tot = 0;
+    long wb = 0, tot = 0;
     for (int w = 0; w < 16; w++) {
       if (w < wave) wb += wsum[w];
       tot += wsum[w];
     }
-    const long pos = (long)carry + wb + incl - g;  // s_{j0 + t}
+    const long pos = carry + wb + incl - g;  // s_{j0 + t}
     if (pos < N) S[j0 + t] = (int)pos;
-    if (pos < N && pos + g >= N) ws.subcnt[c * kRounds + r] = j0 + t + 1;  // the last index below N
+    if (pos < N && pos + g >= N) *subcnt = j0 + t + 1;  // the last index below N
     __syncthreads();  // wsum is rewritten by the next chunk
-    if ((long)carry + tot >= N) break;  // block-uniform
+    if (carry + tot >= N) break;  // block-uniform
     carry += tot;
   }
-  (void)carry_s;
+}
+
+__global__ void __launch_bounds__(1024) k_p2d_subset(uint64_t seed, P2dWs ws) {
+  __shared__ int wsum[16];
+  const int c = blockIdx.x, r = blockIdx.y, t = threadIdx.x;
+  const int N = ws.count[c];
+  if (c == 0 || !((float)N > 400.0f)) return;  // not an object (block-uniform)
+  int* S = ws.sub + (size_t)kRounds * ws.listoff[c] + (size_t)r * N;
+  const int maxPixels = 1000 * (r + 1);
+  const float rate = maxPixels / (float)N;  // :1191
+  if (!(rate < 1)) {  // every pixel (:1212-1213)
+    for (int i = t; i < N; i += blockDim.x) S[i] = i;
+    if (t == 0) ws.subcnt[c * kRounds + r] = N;
+    return;
+  }
+  subset_nohole(seed, c, r, N, 1.0 - (double)rate, S, ws.subcnt + c * kRounds + r, wsum);
 }
 
 // one wave per column: 64 rows at a time; the lanes of one class take their
@@ -484,7 +490,7 @@ __global__ void __launch_bounds__(256) k_p2d_scatter(const int32_t* __restrict__
 __device__ bool p2d_attempt(const float* __restrict__ vm, const float* __restrict__ ext, int H, int W, int C,
                             const Cam& k, uint64_t seed, int h, int a, int n_obj, const P2dWs& ws, int& obj_out,
                             int* px_out, Pose& P) {
-  Stream rs(seed, (uint32_t)h, (uint32_t)a);
+  Stream rs(seed, (uint32_t)h, kTagP2D, (uint32_t)a);
   const int obj = ws.objs[rs.uniform(n_obj)];  // n_obj > 0
   const int* L = ws.lists + ws.listoff[obj];
   const int N = ws.count[obj];
@@ -531,20 +537,304 @@ __device__ bool p2d_attempt(const float* __restrict__ vm, const float* __restric
   return true;
 }
 
+// ---------------------------------------------------------------------------
+// estimatePose3D's pieces shared with the attempt kernels (synthesize.cpp:
+// 1769-1965; the oracle, oracle/orc_pose2d.cpp orc_pose3d, restates the same
+// operations in the same order).
+
+struct AttArgs {  // the sampling attempt's inputs
+  const float* vm;
+  const float* ext;
+  const float* eye;  // (H, W, 3) camera coordinates (estimatePose3D only)
+  int H, W, C;
+  Cam k;
+  uint64_t seed;
+};
+
+__device__ __forceinline__ F3 eye_at(const float* __restrict__ eye, int p) {
+  return {eye[(size_t)p * 3], eye[(size_t)p * 3 + 1], eye[(size_t)p * 3 + 2]};
+}
+
+// one-sided Jacobi SVD of a 3x3 (row-major): A = U diag(S) V^T, S descending;
+// fixed pivot order (0,1), (0,2), (1,2), at most 16 sweeps; U's third column
+// the cross product of the first two when the covariance has rank two
+__device__ void svd3(const double* A, double* U, double* S, double* V) {
+  double M[9], Vm[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+  for (int i = 0; i < 9; i++) M[i] = A[i];
+  for (int sweep = 0; sweep < 16; sweep++) {
+    bool rot = false;
+    for (int kk = 0; kk < 3; kk++) {
+      const int p = kk == 2 ? 1 : 0, q = kk == 0 ? 1 : 2;
+      double al = 0, be = 0, ga = 0;
+      for (int r = 0; r < 3; r++) {
+        al = al + M[r * 3 + p] * M[r * 3 + p];
+        be = be + M[r * 3 + q] * M[r * 3 + q];
+        ga = ga + M[r * 3 + p] * M[r * 3 + q];
+      }
+      if (ga == 0.0 || fabs(ga) <= 1e-15 * sqrt(al * be)) continue;
+      const double zeta = (be - al) / (2.0 * ga);
+      const double t = (zeta >= 0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
+      const double c = 1.0 / sqrt(1.0 + t * t), s = c * t;
+      for (int r = 0; r < 3; r++) {
+        const double mp = M[r * 3 + p], mq = M[r * 3 + q];
+        M[r * 3 + p] = c * mp - s * mq;
+        M[r * 3 + q] = s * mp + c * mq;
+        const double vp = Vm[r * 3 + p], vq = Vm[r * 3 + q];
+        Vm[r * 3 + p] = c * vp - s * vq;
+        Vm[r * 3 + q] = s * vp + c * vq;
+      }
+      rot = true;
+    }
+    if (!rot) break;
+  }
+  double sv[3];
+  for (int i = 0; i < 3; i++) {
+    double a = 0;
+    for (int r = 0; r < 3; r++) a = a + M[r * 3 + i] * M[r * 3 + i];
+    sv[i] = sqrt(a);
+  }
+  int o[3] = {0, 1, 2};  // descending, stable
+  for (int i = 1; i < 3; i++)
+    for (int j = i; j > 0 && sv[o[j]] > sv[o[j - 1]]; j--) {
+      const int tmp = o[j];
+      o[j] = o[j - 1];
+      o[j - 1] = tmp;
+    }
+  for (int kk = 0; kk < 3; kk++) {
+    S[kk] = sv[o[kk]];
+    for (int r = 0; r < 3; r++) {
+      V[r * 3 + kk] = Vm[r * 3 + o[kk]];
+      U[r * 3 + kk] = S[kk] > 0 ? M[r * 3 + o[kk]] / S[kk] : 0.0;
+    }
+  }
+  if (!(S[2] > 1e-9 * S[0])) {
+    U[0 * 3 + 2] = U[1 * 3 + 0] * U[2 * 3 + 1] - U[2 * 3 + 0] * U[1 * 3 + 1];
+    U[1 * 3 + 2] = U[2 * 3 + 0] * U[0 * 3 + 1] - U[0 * 3 + 0] * U[2 * 3 + 1];
+    U[2 * 3 + 2] = U[0 * 3 + 0] * U[1 * 3 + 1] - U[1 * 3 + 0] * U[0 * 3 + 1];
+  }
+}
+
+__device__ __forceinline__ double det3(const double* m) {
+  return m[0] * (m[4] * m[8] - m[5] * m[7]) - m[1] * (m[3] * m[8] - m[5] * m[6]) + m[2] * (m[3] * m[7] - m[4] * m[6]);
+}
+
+// calcRigidBodyTransform (Hypothesis.cpp:217-241) from the centroids and the
+// covariance: R = V diag(1, 1, sign det(V U^T)) U^T, t = -R cA + cB
+__device__ Pose rigid_from_cov(const double* Hc, const double* cA, const double* cB) {
+  double U[9], S[3], V[9];
+  svd3(Hc, U, S, V);
+  double VU[9];
+  for (int r = 0; r < 3; r++)
+    for (int c = 0; c < 3; c++) VU[r * 3 + c] = V[r * 3 + 0] * U[c * 3 + 0] + V[r * 3 + 1] * U[c * 3 + 1] + V[r * 3 + 2] * U[c * 3 + 2];
+  const double sg = det3(VU) < 0 ? -1.0 : 1.0;
+  Pose P;
+  for (int r = 0; r < 3; r++)
+    for (int c = 0; c < 3; c++)
+      P.R[r * 3 + c] = V[r * 3 + 0] * U[c * 3 + 0] + V[r * 3 + 1] * U[c * 3 + 1] + (V[r * 3 + 2] * sg) * U[c * 3 + 2];
+  for (int r = 0; r < 3; r++) P.t[r] = -(P.R[r * 3 + 0] * cA[0] + P.R[r * 3 + 1] * cA[1] + P.R[r * 3 + 2] * cA[2]) + cB[r];
+  return P;
+}
+
+// the 64-lane fold (partials p_l over elements l, l + 64, ...; then p_i +=
+// p_{i + off}, off = 32 .. 1) of n <= 4 elements held by one lane: the same
+// additions, zeros included, as the wave version below
+template <int n>
+__device__ __forceinline__ double fold_small(const double* x) {
+  double p[64];
+#pragma unroll
+  for (int l = 0; l < 64; l++) p[l] = l < n ? 0.0 + x[l] : 0.0;
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1)
+#pragma unroll
+    for (int i = 0; i < off; i++) p[i] = p[i] + p[i + off];
+  return p[0];
+}
+
+// the wave's fold of per-lane partials; the sum is returned on every lane
+__device__ __forceinline__ double fold64(double v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    const double w = __shfl_down(v, off, 64);
+    v = v + w;
+  }
+  return __shfl(v, 0, 64);
+}
+__device__ __forceinline__ float fold64f(float v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    const float w = __shfl_down(v, off, 64);
+    v = v + w;
+  }
+  return __shfl(v, 0, 64);
+}
+
+__device__ __forceinline__ D3 xform(const Pose& P, D3 p) {  // Hypothesis::transform
+  return {P.R[0] * p.x + P.R[1] * p.y + P.R[2] * p.z + P.t[0], P.R[3] * p.x + P.R[4] * p.y + P.R[5] * p.z + P.t[1],
+          P.R[6] * p.x + P.R[7] * p.y + P.R[8] * p.z + P.t[2]};
+}
+
+// One sampling attempt of :1814-1889: samplePoint3D x 3 (:1105-1134: depth
+// hole, 1 cm camera / object spacing, empty prediction), the 3-point rigid
+// transform, the 1 cm reconstruction check, getBB2D area >= 400
+__device__ bool p3d_attempt(const AttArgs& A, int h, int a, int n_obj, const P2dWs& ws, int& obj_out, int* px_out,
+                            Pose& P) {
+  Stream rs(A.seed, (uint32_t)h, kTagP3D, (uint32_t)a);
+  const int obj = ws.objs[rs.uniform(n_obj)];
+  const int* L = ws.lists + ws.listoff[obj];
+  const int N = ws.count[obj];
+  F3 E[3], O[3];
+  int n = 0;
+  for (int s = 0; s < 3; s++) {
+    const int idx = L[rs.uniform(N)];
+    const F3 e = eye_at(A.eye, idx);
+    if (e.z == 0) return false;
+    double md = -1;
+    for (int q = 0; q < n; q++) md = md < 0 ? norm3f(E[q], e) : fmin(md, norm3f(E[q], e));
+    if (md > 0 && md < 0.01) return false;
+    const F3 o = mode3d(A.vm, A.ext, A.C, obj, idx);
+    if (o.x == 0 && o.y == 0 && o.z == 0) return false;
+    md = -1;
+    for (int q = 0; q < n; q++) md = md < 0 ? norm3f(O[q], o) : fmin(md, norm3f(O[q], o));
+    if (md > 0 && md < 0.01) return false;
+    E[n] = e;
+    O[n] = o;
+    px_out[n] = idx;
+    n++;
+  }
+  const double inv = 1.0 / 3.0;
+  double cA[3], cB[3], Hc[9];
+  {
+    double xa[3][3], xb[3][3];  // [coordinate][point]
+    for (int q = 0; q < 3; q++) {
+      xa[0][q] = O[q].x; xa[1][q] = O[q].y; xa[2][q] = O[q].z;
+      xb[0][q] = E[q].x; xb[1][q] = E[q].y; xb[2][q] = E[q].z;
+    }
+    for (int r = 0; r < 3; r++) {
+      cA[r] = fold_small<3>(xa[r]) * inv;
+      cB[r] = fold_small<3>(xb[r]) * inv;
+    }
+    for (int r = 0; r < 3; r++)
+      for (int c = 0; c < 3; c++) {
+        double pr[3];
+        for (int q = 0; q < 3; q++) pr[q] = (xa[r][q] - cA[r]) * (xb[c][q] - cB[c]);
+        Hc[r * 3 + c] = fold_small<3>(pr);
+      }
+  }
+  P = rigid_from_cov(Hc, cA, cB);
+  for (int q = 0; q < 3; q++) {  // :1859-1867
+    const D3 b{E[q].x, E[q].y, E[q].z};
+    if (!(nrm(sub(b, xform(P, D3{O[q].x, O[q].y, O[q].z}))) < 0.01)) return false;
+  }
+  if ((float)bb_area(P, A.ext, obj, A.k, A.W, A.H) < 400.0f) return false;  // :1877-1882
+  obj_out = obj;
+  return true;
+}
+
+// sin / cos / acos from + - * / sqrt only (the oracle's dsincos / dacos):
+// quadrant reduction by a two-part pi/2, the fdlibm kernel polynomials; acos
+// by the half-angle identity and 6 Newton steps on asin
+__device__ void dsincos(double x, double& s, double& c) {
+  const double n = floor(x * 0.63661977236758134308 + 0.5);
+  const double y = (x - n * 1.57079632673412561417e+00) - n * 6.07710050650619224932e-11;
+  const double z = y * y;
+  const double ks = y + y * z * (-1.66666666666666324348e-01 + z * (8.33333333332248946124e-03 + z * (-1.98412698298579493134e-04 +
+                        z * (2.75573137070700676789e-06 + z * (-2.50507602534068634195e-08 + z * 1.58969099521155010221e-10)))));
+  const double kc = 1.0 - (0.5 * z - z * z * (4.16666666666666019037e-02 + z * (-1.38888888888741095749e-03 + z * (2.48015872894767294178e-05 +
+                        z * (-2.75573143513906633035e-07 + z * (2.08757232129817482790e-09 + z * -1.13596475577881948265e-11))))));
+  const int q = ((int)n) & 3;
+  s = q == 0 ? ks : q == 1 ? kc : q == 2 ? -ks : -kc;
+  c = q == 0 ? kc : q == 1 ? -ks : q == 2 ? -kc : ks;
+}
+
+__device__ double dasin_small(double x) {
+  double y = x;
+  for (int i = 0; i < 6; i++) {
+    double s, c;
+    dsincos(y, s, c);
+    y = y - (s - x) / c;
+  }
+  return y;
+}
+
+__device__ double dacos(double c) {
+  if (c >= 0) return 2.0 * dasin_small(sqrt((1.0 - c) * 0.5));
+  return 3.14159265358979311600 - 2.0 * dasin_small(sqrt((1.0 + c) * 0.5));
+}
+
+// cv::Rodrigues vector -> matrix
+__device__ void rod_v2m(const double* r, double* R) {
+  const double th = sqrt(r[0] * r[0] + r[1] * r[1] + r[2] * r[2]);
+  if (th < 2.220446049250313e-16) {
+    for (int i = 0; i < 9; i++) R[i] = (i % 4 == 0) ? 1.0 : 0.0;
+    return;
+  }
+  double s, c;
+  dsincos(th, s, c);
+  const double c1 = 1.0 - c, it = 1.0 / th;
+  const double x = r[0] * it, y = r[1] * it, z = r[2] * it;
+  const double rrt[9] = {x * x, x * y, x * z, x * y, y * y, y * z, x * z, y * z, z * z};
+  const double rx[9] = {0, -z, y, z, 0, -x, -y, x, 0};
+  for (int i = 0; i < 9; i++) R[i] = c * ((i % 4 == 0) ? 1.0 : 0.0) + c1 * rrt[i] + s * rx[i];
+}
+
+// cv::Rodrigues matrix -> vector (without cvRodrigues2's re-orthonormalisation)
+__device__ void rod_m2v(const double* R, double* r) {
+  double rx = R[7] - R[5], ry = R[2] - R[6], rz = R[3] - R[1];
+  const double s = sqrt((rx * rx + ry * ry + rz * rz) * 0.25);
+  double c = (R[0] + R[4] + R[8] - 1) * 0.5;
+  c = c > 1. ? 1. : c < -1. ? -1. : c;
+  double th = dacos(c);
+  if (s < 1e-5) {
+    if (c > 0) {
+      rx = ry = rz = 0;
+    } else {
+      double t = (R[0] + 1) * 0.5;
+      rx = sqrt(fmax(t, 0.));
+      t = (R[4] + 1) * 0.5;
+      ry = sqrt(fmax(t, 0.)) * (R[1] < 0 ? -1. : 1.);
+      t = (R[8] + 1) * 0.5;
+      rz = sqrt(fmax(t, 0.)) * (R[2] < 0 ? -1. : 1.);
+      if (fabs(rx) < fabs(ry) && fabs(rx) < fabs(rz) && (R[5] > 0) != (ry * rz > 0)) rz = -rz;
+      th /= sqrt(rx * rx + ry * ry + rz * rz);
+      rx *= th;
+      ry *= th;
+      rz *= th;
+    }
+  } else {
+    double vth = 1 / (2 * s);
+    vth *= th;
+    rx *= vth;
+    ry *= vth;
+    rz *= vth;
+  }
+  r[0] = rx;
+  r[1] = ry;
+  r[2] = rz;
+}
+
 // The first kAttempts attempts of every hypothesis at once, one lane each:
 // the reference's loop runs attempts until one is accepted, and attempts are
 // independent (each its own stream), so they need not wait for each other.
-__global__ void __launch_bounds__(64) k_p2d_attempts(const float* __restrict__ vm, const float* __restrict__ ext,
-                                                     int H, int W, int C, Cam k, uint64_t seed, int n_hyp, int T,
-                                                     P2dWs ws) {
+// kDepth: estimatePose3D's attempt (3 pixels), else estimatePose2D's (4).
+template <bool kDepth>
+__device__ __forceinline__ bool attempt(const AttArgs& A, int h, int a, int n_obj, const P2dWs& ws, int& obj,
+                                        int* px, Pose& P) {
+  if constexpr (kDepth)
+    return p3d_attempt(A, h, a, n_obj, ws, obj, px, P);
+  else
+    return p2d_attempt(A.vm, A.ext, A.H, A.W, A.C, A.k, A.seed, h, a, n_obj, ws, obj, px, P);
+}
+
+template <bool kDepth>
+__global__ void __launch_bounds__(64) k_attempts(AttArgs A, int n_hyp, int T, P2dWs ws) {
   const int id = blockIdx.x * blockDim.x + threadIdx.x;
   const int n_obj = *ws.nobj;
   if (id >= n_hyp * T || n_obj == 0) return;
   const int h = id % n_hyp, a = id / n_hyp;
   double* rec = ws.att + (size_t)(h * T + a) * kAttRec;
-  int obj, px4[4];
+  int obj, px4[4] = {-1, -1, -1, -1};
   Pose P;
-  if (!p2d_attempt(vm, ext, H, W, C, k, seed, h, a, n_obj, ws, obj, px4, P)) {
+  if (!attempt<kDepth>(A, h, a, n_obj, ws, obj, px4, P)) {
     rec[0] = -1;
     return;
   }
@@ -557,11 +847,12 @@ __global__ void __launch_bounds__(64) k_p2d_attempts(const float* __restrict__ v
 // One wave per hypothesis: its first accepted attempt in attempt order --
 // the batch above, then (rarely) 64 further attempts at a time, each lane
 // one attempt, the lowest accepted lane kept -- written out as :1682-1686
-// stores it.  max_iter bounds the attempts (the reference: 10,000,000).
-__global__ void __launch_bounds__(64) k_p2d_pick(const float* __restrict__ vm, const float* __restrict__ ext, int H,
-                                                 int W, int C, Cam k, uint64_t seed, int n_hyp, int max_iter, int T,
-                                                 P2dWs ws, float* __restrict__ hyps_out,
-                                                 int32_t* __restrict__ hyp_px) {
+// (:1884-1887) store it.  max_iter bounds the attempts (the reference:
+// 10,000,000).
+template <bool kDepth>
+__global__ void __launch_bounds__(64) k_pick(AttArgs A, int n_hyp, int max_iter, int T, P2dWs ws,
+                                             float* __restrict__ hyps_out, int32_t* __restrict__ hyp_px) {
+  constexpr int kPx = kDepth ? 3 : 4;
   const int h = blockIdx.x, lane = pcnn::lane_id();
   if (h >= n_hyp) return;
   const int n_obj = *ws.nobj;
@@ -583,9 +874,9 @@ __global__ void __launch_bounds__(64) k_p2d_pick(const float* __restrict__ vm, c
   } else if (n_obj > 0) {
     for (int a0 = T; a0 < max_iter; a0 += 64) {  // wave-uniform loop
       const int a = a0 + lane;
-      int o = -1, q4[4];
+      int o = -1, q4[4] = {-1, -1, -1, -1};
       Pose Q;
-      const bool acc = a < max_iter && p2d_attempt(vm, ext, H, W, C, k, seed, h, a, n_obj, ws, o, q4, Q);
+      const bool acc = a < max_iter && attempt<kDepth>(A, h, a, n_obj, ws, o, q4, Q);
       const uint64_t b = __ballot(acc);
       if (b) {
         const int src = __ffsll((unsigned long long)b) - 1;  // the lowest accepted attempt
@@ -603,7 +894,7 @@ __global__ void __launch_bounds__(64) k_p2d_pick(const float* __restrict__ vm, c
   hr[0] = obj;
   ho[0] = (float)obj;
   for (int i = 0; i < 12; i++) ho[1 + i] = 0.f;
-  for (int i = 0; i < 4; i++) hyp_px[h * 4 + i] = obj >= 0 ? px4[i] : -1;
+  for (int i = 0; i < kPx; i++) hyp_px[h * kPx + i] = obj >= 0 ? px4[i] : -1;
   if (obj < 0) {
     hr[0] = -1;
     return;
@@ -713,6 +1004,513 @@ __global__ void __launch_bounds__(64) k_p2d_finish(int C, int n_hyp, P2dWs ws, i
     for (int x = 0; x < 4; x++) poses_out[obj + C * (y * 4 + x)] = x < 3 ? (float)hr[1 + y * 3 + x] : (float)hr[10 + y];
 }
 
+// ===========================================================================
+// estimatePose3D (synthesize.cpp:1769-1965) on the device.  The label lists,
+// object ids and hypothesis bookkeeping are estimatePose2D's (above); the
+// 3-D pieces:
+//   k_p3d_eye: getEye / pxToEye (:1372-1407), the camera coordinates of the
+//       raw depth (float arithmetic; holes at the origin);
+//   k_p3d_valid: one bit per class-list position -- depth present -- so
+//       that a round's subset can skip holes the way countInliers3D does
+//       (:1255-1287: a hole advances to the next pixel without a draw);
+//   k_p3d_subset: the rounds' subsets with holes: positions p_{j+1} =
+//       next_valid(p_j + gap_j), the same Philox gaps as estimatePose2D.
+//       A class without holes takes the parallel gap scan; otherwise one wave
+//       walks 64 draws per step from the class's bits in LDS, the lanes up to
+//       the first one landing on a hole accepted at once, that lane moved to
+//       the next valid position (a wave-wide bit search) and the walk resumed;
+//   k_attempts<true> / k_pick<true>: the sampling loop (:1814-1889);
+//   k_p3d_count: countInliers3D over the round's subset (1 cm in double),
+//       inlier bits per hypothesis;
+//   k_p2d_select: the stable halving (as estimatePose2D);
+//   k_p3d_update: updateHyp3D (:1347-1364) for every survivor, one wave
+//       each: filterInliers3D (:1308-1322; pick k of round r on its own
+//       stream (draw, h, 'F3D', 1024 r + k)), the inlier ranks resolved to
+//       subset positions by a popcount prefix, then the rigid transform with
+//       the wave's fold64 sums and the 3x3 Jacobi SVD;
+//   k_p3d_finish: the survivor's output (:1936-1964): when it has more than
+//       minPixels = 10 inliers, filterInliers3D again (r = 8) and
+//       refineWithOpt (:1510-1567) -- the bounded Nelder-Mead over the
+//       Rodrigues vector and translation (+-10 deg, +-0.1, +-0.1, +-0.5 m,
+//       100 evaluations) of optEnergy3D (:1464-1507), one wave per object,
+//       the energy's float sum as 64 strided partials folded by halving.
+
+struct P3dWs {
+  P2dWs b;
+  float* eye;       // (H W 3) camera coordinates
+  uint64_t* valid;  // depth-present bits over the concatenated class lists (+ 2 pad words)
+  uint64_t* imask;  // (n_hyp, mwords) inlier bits over the round's subset
+  int32_t* pick;    // (n_hyp, kMaxInl) pixels of the last refit's correspondences
+  int32_t* npick;   // (n_hyp)
+  int mwords;
+};
+
+constexpr int kMaxInl = 1000;     // maxPixels: filterInliers3D's cap (:1796)
+constexpr int kLdsWords = 5120;   // class-list bits kept in LDS by k_p3d_subset (327,680 positions)
+constexpr int kPrefWords = 2048;  // subset words with an LDS popcount prefix in k_p3d_update
+
+__global__ void __launch_bounds__(256) k_p3d_eye(const uint16_t* __restrict__ depth, int H, int W, float fx, float fy,
+                                                 float px, float py, float factor, float* __restrict__ eye) {
+  const int p = blockIdx.x * 256 + threadIdx.x;
+  if (p >= H * W) return;
+  const int x = p % W, y = p / W;
+  const unsigned short d = depth[p];
+  float e0 = 0.f, e1 = 0.f, e2 = 0.f;
+  if (d != 0) {
+    e0 = ((float)x - px) * (float)d / fx / factor;
+    e1 = ((float)y - py) * (float)d / fy / factor;
+    e2 = (float)d / factor;
+  }
+  eye[(size_t)p * 3] = e0;
+  eye[(size_t)p * 3 + 1] = e1;
+  eye[(size_t)p * 3 + 2] = e2;
+}
+
+// grid valid_blocks(HW): every word a class_word read may touch is written
+inline int valid_blocks(int HW) { return (HW + 64 + 255) / 256; }
+
+__global__ void __launch_bounds__(256) k_p3d_valid(int C, P3dWs w3) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  const int total = w3.b.listoff[C - 1] + w3.b.count[C - 1];
+  const bool v = i < total && w3.eye[(size_t)w3.b.lists[i] * 3 + 2] != 0.f;
+  const uint64_t b = __ballot(v);
+  if (pcnn::lane_id() == 0) w3.valid[i >> 6] = b;
+}
+
+// bits [64 k, 64 k + 64) of the class list starting at global bit o, none past N
+__device__ __forceinline__ uint64_t class_word(const uint64_t* __restrict__ V, long o, int N, long k) {
+  const long b = o + 64 * k;
+  const long w = b >> 6;
+  const int sh = (int)(b & 63);
+  uint64_t v = V[w] >> sh;
+  if (sh) v |= V[w + 1] << (64 - sh);
+  const long rem = (long)N - 64 * k;
+  if (rem < 64) v &= rem <= 0 ? 0ull : ((1ull << rem) - 1);
+  return v;
+}
+
+__global__ void __launch_bounds__(1024) k_p3d_subset(uint64_t seed, P3dWs w3) {
+  __shared__ uint64_t bits[kLdsWords];  // 40 KiB
+  __shared__ int wsum[16];
+  __shared__ long qrel[1024];
+  __shared__ int sh_int[4];
+  const P2dWs& ws = w3.b;
+  const int c = blockIdx.x, r = blockIdx.y, t = threadIdx.x, lane = pcnn::lane_id(), wave = t >> 6;
+  const int N = ws.count[c];
+  if (c == 0 || !((float)N > 400.0f)) return;  // not an object (block-uniform)
+  int* S = ws.sub + (size_t)kRounds * ws.listoff[c] + (size_t)r * N;
+  int* cnt_out = ws.subcnt + c * kRounds + r;
+  const long o = ws.listoff[c];
+  const int nw = (N + 63) / 64;
+  const bool in_lds = nw <= kLdsWords;
+  int nv = 0;
+  for (int k = t; k < nw; k += 1024) {
+    const uint64_t v = class_word(w3.valid, o, N, k);
+    if (in_lds) bits[k] = v;
+    nv += __popcll(v);
+  }
+  nv = pcnn::wave_sum(nv);
+  if (t == 0) sh_int[0] = 0;
+  __syncthreads();
+  if (lane == 0) atomicAdd(&sh_int[0], nv);  // integer: order-free
+  __syncthreads();
+  nv = sh_int[0];
+  auto word = [&](long k) -> uint64_t { return in_lds ? bits[k] : class_word(w3.valid, o, N, k); };
+  const int maxPixels = 1000 * (r + 1);
+  const float rate = maxPixels / (float)N;  // :1250
+  if (!(rate < 1)) {  // every valid pixel in list order (:1283-1286)
+    long carry = 0;
+    for (int base = 0; base < nw; base += 1024) {  // ordered compaction, a word per thread
+      const int k = base + t;
+      const uint64_t v = k < nw ? word(k) : 0ull;
+      const int pc = __popcll(v);
+      int incl = pc;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const int y = __shfl_up(incl, d, 64);
+        if (lane >= d) incl += y;
+      }
+      if (lane == 63) wsum[wave] = incl;
+      __syncthreads();
+      long wb = 0, tot = 0;
+      for (int w = 0; w < 16; w++) {
+        if (w < wave) wb += wsum[w];
+        tot += wsum[w];
+      }
+      long pos = carry + wb + incl - pc;
+      for (uint64_t m = v; m; m &= m - 1) S[pos++] = 64 * k + __ffsll((unsigned long long)m) - 1;
+      __syncthreads();
+      carry += tot;
+    }
+    if (t == 0) *cnt_out = nv;
+    return;
+  }
+  const double q = 1.0 - (double)rate;
+  if (nv == N) {  // no holes: estimatePose2D's subset
+    subset_nohole(seed, c, r, N, q, S, cnt_out, wsum);
+    return;
+  }
+  long carry = 0;  // q_{j0}: the hole-free position of draw j0
+  long D = 0;      // holes skipped so far (wave 0)
+  for (int j0 = 0;; j0 += 1024) {
+    const int g = p2d_gap(seed, c, r, j0 + t, q);
+    int incl = g;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int y = __shfl_up(incl, d, 64);
+      if (lane >= d) incl += y;
+    }
+    if (lane == 63) wsum[wave] = incl;
+    __syncthreads();
+    long wb = 0, tot = 0;
+    for (int w = 0; w < 16; w++) {
+      if (w < wave) wb += wsum[w];
+      tot += wsum[w];
+    }
+    qrel[t] = wb + incl - g;
+    __syncthreads();
+    if (wave == 0) {
+      int done = 0, cnt = 0;
+      for (int sc = 0; sc < 16 && !done; sc++) {
+        const int jl = sc * 64 + lane;
+        const long qj = carry + qrel[jl];
+        int s = 0;
+        for (;;) {  // wave-uniform
+          const long x = qj + D;
+          bool ev = false;
+          if (lane >= s) ev = x >= N || !((word(x >> 6) >> (x & 63)) & 1ull);
+          const uint64_t b = __ballot(ev);
+          const int first = b ? __ffsll((unsigned long long)b) - 1 : 64;
+          if (lane >= s && lane < first) S[j0 + jl] = (int)x;
+          if (first == 64) break;
+          const long xs = __shfl(x, first, 64);
+          long nh = N;
+          if (xs < N) {  // the next valid position at or after xs (wave-wide word search)
+            for (long kb = xs >> 6; kb < nw; kb += 64) {
+              const long k = kb + lane;
+              uint64_t v = k < nw ? word(k) : 0ull;
+              if (k == (xs >> 6)) v &= ~0ull << (xs & 63);
+              const uint64_t hit = __ballot(v != 0ull);
+              if (hit) {
+                const int l = __ffsll((unsigned long long)hit) - 1;
+                const uint64_t vv = __shfl((unsigned long long)v, l, 64);
+                nh = 64 * (kb + l) + __ffsll((unsigned long long)vv) - 1;
+                break;
+              }
+            }
+          }
+          if (nh >= N) {  // the walk leaves the list: draws j0 + sc 64 + first .. are not taken
+            done = 1;
+            cnt = j0 + sc * 64 + first;
+            break;
+          }
+          D += nh - xs;
+          s = first;
+        }
+      }
+      if (lane == 0) {
+        sh_int[1] = done;
+        sh_int[2] = cnt;
+      }
+    }
+    __syncthreads();
+    if (sh_int[1]) {
+      if (t == 0) *cnt_out = sh_int[2];
+      return;
+    }
+    carry += tot;
+  }
+}
+
+__global__ void __launch_bounds__(256) k_p3d_count(const float* __restrict__ vm, const float* __restrict__ ext, int C,
+                                                   P3dWs w3, int r, int32_t* __restrict__ inl_out) {
+  __shared__ int part[4];
+  const P2dWs& ws = w3.b;
+  const int j = blockIdx.x, oi = blockIdx.y, lane = pcnn::lane_id(), wave = threadIdx.x >> 6;
+  if (oi >= *ws.nobj || j >= ws.rm[oi]) return;  // block-uniform
+  const int obj = ws.objs[oi];
+  const int* L = ws.lists + ws.listoff[obj];
+  const int h = ws.rl[oi * kMaxHypBlock + j];
+  const int* S = ws.sub + (size_t)kRounds * ws.listoff[obj] + (size_t)r * ws.count[obj];
+  const int ns = ws.subcnt[obj * kRounds + r];
+  const double* hr = ws.hyp + (size_t)h * 16;
+  Pose P;
+  for (int i = 0; i < 9; i++) P.R[i] = hr[1 + i];
+  for (int i = 0; i < 3; i++) P.t[i] = hr[10 + i];
+  uint64_t* M = w3.imask + (size_t)h * w3.mwords;
+  int cnt = 0;
+  for (int i0 = 0; i0 < ns; i0 += 256) {  // countInliers3D (:1255-1287)
+    const int i = i0 + threadIdx.x;
+    bool in = false;
+    if (i < ns) {
+      const int p = L[S[i]];
+      const F3 e = eye_at(w3.eye, p);
+      const F3 o = mode3d(vm, ext, C, obj, p);
+      in = nrm(sub(D3{e.x, e.y, e.z}, xform(P, D3{o.x, o.y, o.z}))) < 0.01;
+    }
+    const uint64_t b = __ballot(in);
+    if (lane == 0 && i0 + 64 * wave < ns) M[(i0 >> 6) + wave] = b;
+    cnt += in;
+  }
+  cnt = pcnn::wave_sum(cnt);
+  if (lane == 0) part[wave] = cnt;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int c = part[0] + part[1] + part[2] + part[3];
+    ws.rc[oi * kMaxHypBlock + j] = c;
+    inl_out[h * kRounds + r] = c;
+  }
+}
+
+// the subset position of the rank-th set bit of M (pref: exclusive popcount
+// prefix per word when the subset has at most kPrefWords words)
+__device__ __forceinline__ int select_bit(const uint64_t* __restrict__ M, const int* pref, int nw, int rank) {
+  int k = 0;
+  if (nw <= kPrefWords) {
+    int lo = 0, hi = nw - 1;  // the last word with pref <= rank
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (pref[mid] <= rank) lo = mid; else hi = mid - 1;
+    }
+    k = lo;
+    rank -= pref[k];
+  } else {
+    for (;; k++) {
+      const int pc = __popcll(M[k]);
+      if (rank < pc) break;
+      rank -= pc;
+    }
+  }
+  uint64_t v = M[k];
+  for (int i = 0; i < rank; i++) v &= v - 1;
+  return 64 * k + __ffsll((unsigned long long)v) - 1;
+}
+
+// the rigid transform of the correspondences corr[0, m) (pixels): object
+// coordinate -> camera coordinate, fold64 sums; every lane gets the pose
+__device__ Pose wave_rigid(const float* __restrict__ vm, const float* __restrict__ ext, int C, int obj,
+                           const float* __restrict__ eye, const int* corr, int m) {
+  const int lane = pcnn::lane_id();
+  double sa[3] = {0.0, 0.0, 0.0}, sb[3] = {0.0, 0.0, 0.0};
+  for (int k = lane; k < m; k += 64) {
+    const F3 o = mode3d(vm, ext, C, obj, corr[k]);
+    const F3 e = eye_at(eye, corr[k]);
+    sa[0] = sa[0] + (double)o.x; sa[1] = sa[1] + (double)o.y; sa[2] = sa[2] + (double)o.z;
+    sb[0] = sb[0] + (double)e.x; sb[1] = sb[1] + (double)e.y; sb[2] = sb[2] + (double)e.z;
+  }
+  const double inv = 1.0 / (double)m;
+  double cA[3], cB[3];
+  for (int i = 0; i < 3; i++) {
+    cA[i] = fold64(sa[i]) * inv;
+    cB[i] = fold64(sb[i]) * inv;
+  }
+  double sc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  for (int k = lane; k < m; k += 64) {
+    const F3 o = mode3d(vm, ext, C, obj, corr[k]);
+    const F3 e = eye_at(eye, corr[k]);
+    const double pa[3] = {(double)o.x - cA[0], (double)o.y - cA[1], (double)o.z - cA[2]};
+    const double pb[3] = {(double)e.x - cB[0], (double)e.y - cB[1], (double)e.z - cB[2]};
+    for (int rr = 0; rr < 3; rr++)
+      for (int cc = 0; cc < 3; cc++) sc[rr * 3 + cc] = sc[rr * 3 + cc] + pa[rr] * pb[cc];
+  }
+  double Hc[9];
+  for (int i = 0; i < 9; i++) Hc[i] = fold64(sc[i]);
+  return rigid_from_cov(Hc, cA, cB);
+}
+
+__global__ void __launch_bounds__(64) k_p3d_update(const float* __restrict__ vm, const float* __restrict__ ext, int C,
+                                                   uint64_t seed, P3dWs w3, int r) {
+  __shared__ int pref[kPrefWords];
+  __shared__ int corr[kMaxInl];
+  const P2dWs& ws = w3.b;
+  const int j = blockIdx.x, oi = blockIdx.y, lane = pcnn::lane_id();
+  if (oi >= *ws.nobj || j >= ws.rm[oi]) return;  // block-uniform
+  const int n = ws.rc[oi * kMaxHypBlock + j];
+  if (n < 4) return;  // :1350-1351
+  const int obj = ws.objs[oi];
+  const int h = ws.rl[oi * kMaxHypBlock + j];
+  const int* L = ws.lists + ws.listoff[obj];
+  const int* S = ws.sub + (size_t)kRounds * ws.listoff[obj] + (size_t)r * ws.count[obj];
+  const int ns = ws.subcnt[obj * kRounds + r];
+  const int nw = (ns + 63) / 64;
+  const uint64_t* M = w3.imask + (size_t)h * w3.mwords;
+  if (nw <= kPrefWords) {
+    int carry = 0;
+    for (int base = 0; base < nw; base += 64) {
+      const int k = base + lane;
+      const int pc = k < nw ? __popcll(M[k]) : 0;
+      int incl = pc;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const int y = __shfl_up(incl, d, 64);
+        if (lane >= d) incl += y;
+      }
+      if (k < nw) pref[k] = carry + incl - pc;
+      carry += __shfl(incl, 63, 64);
+    }
+  }
+  __syncthreads();
+  const int m = n >= kMaxInl ? kMaxInl : n;  // filterInliers3D (:1308-1322)
+  for (int k = lane; k < m; k += 64) {
+    int rank = k;
+    if (n >= kMaxInl) {
+      Stream rs(seed, (uint32_t)h, kTagF3D, (uint32_t)(1024 * r + k));
+      rank = rs.uniform(n);
+    }
+    const int p = L[S[select_bit(M, pref, nw, rank)]];
+    corr[k] = p;
+    w3.pick[(size_t)h * kMaxInl + k] = p;
+  }
+  if (lane == 0) w3.npick[h] = m;
+  __syncthreads();
+  const Pose P = wave_rigid(vm, ext, C, obj, w3.eye, corr, m);  // Hypothesis::refine (:1359)
+  if (lane != 0) return;
+  double* hr = ws.hyp + (size_t)h * 16;
+  for (int i = 0; i < 9; i++) hr[1 + i] = P.R[i];
+  for (int i = 0; i < 3; i++) hr[10 + i] = P.t[i];
+}
+
+__global__ void __launch_bounds__(64) k_p3d_finish(const float* __restrict__ vm, const float* __restrict__ ext, int C,
+                                                   int n_hyp, uint64_t seed, int nm_evals, P3dWs w3,
+                                                   int32_t* __restrict__ final_out, float* __restrict__ poses_out,
+                                                   float* __restrict__ energy_out) {
+  __shared__ float co[kMaxInl][3], ce[kMaxInl][3];
+  const P2dWs& ws = w3.b;
+  const int oi = blockIdx.x, lane = pcnn::lane_id();  // one wave per object
+  if (oi >= *ws.nobj || ws.rm[oi] == 0) return;
+  const int obj = ws.objs[oi];
+  const int h = ws.rl[oi * kMaxHypBlock];
+  const int n = ws.rc[oi * kMaxHypBlock];
+  int nh = 0;
+  for (int q = lane; q < n_hyp; q += 64) nh += ws.hyp[(size_t)q * 16] == (double)obj;
+  nh = pcnn::wave_sum(nh);
+  if (lane == 0) {
+    final_out[obj * 3] = h;
+    final_out[obj * 3 + 1] = n;
+    final_out[obj * 3 + 2] = nh;
+  }
+  const double* hr = ws.hyp + (size_t)h * 16;
+  Pose P;
+  for (int i = 0; i < 9; i++) P.R[i] = hr[1 + i];
+  for (int i = 0; i < 3; i++) P.t[i] = hr[10 + i];
+  float en = 0.f;
+  if (n > 10) {  // minPixels (:1939)
+    const int mp = w3.npick[h];
+    const int m = mp >= kMaxInl ? kMaxInl : mp;
+    for (int k = lane; k < m; k += 64) {
+      int idx = k;
+      if (mp >= kMaxInl) {
+        Stream rs(seed, (uint32_t)h, kTagF3D, (uint32_t)(1024 * kRounds + k));
+        idx = rs.uniform(mp);
+      }
+      const int p = w3.pick[(size_t)h * kMaxInl + idx];
+      const F3 o = mode3d(vm, ext, C, obj, p);
+      const F3 e = eye_at(w3.eye, p);
+      co[k][0] = o.x; co[k][1] = o.y; co[k][2] = o.z;
+      ce[k][0] = e.x; ce[k][1] = e.y; ce[k][2] = e.z;
+    }
+    __syncthreads();
+    auto energy = [&](const double* x) -> double {  // optEnergy3D (:1464-1507)
+      double Rd[9];
+      rod_v2m(x, Rd);
+      float Rf[9];
+      for (int i = 0; i < 9; i++) Rf[i] = (float)Rd[i];
+      float pt = 0.f;
+      for (int k = lane; k < m; k += 64) {
+        float tr[3];
+        for (int rr = 0; rr < 3; rr++) {
+          const float mm = Rf[rr * 3 + 0] * co[k][0] + Rf[rr * 3 + 1] * co[k][1] + Rf[rr * 3 + 2] * co[k][2];
+          tr[rr] = (float)((double)mm + x[3 + rr]);
+        }
+        const double dx = (double)tr[0] - (double)ce[k][0], dy = (double)tr[1] - (double)ce[k][1],
+                     dz = (double)tr[2] - (double)ce[k][2];
+        pt = (float)((double)pt + sqrt(dx * dx + dy * dy + dz * dz));
+      }
+      return (double)(fold64f(pt) / (float)m);
+    };
+    // refineWithOpt (:1510-1567): every lane runs the same search
+    constexpr int nd = 6;
+    double x0[nd], lb[nd], ub[nd];
+    rod_m2v(P.R, x0);
+    for (int i = 0; i < 3; i++) x0[3 + i] = P.t[i];
+    const double rot = 10 * 3.1415926 / 180;  // rotRange, PI of types.h:33
+    const double rng[nd] = {rot, rot, rot, 0.1, 0.1, 0.5};
+    for (int i = 0; i < nd; i++) {
+      lb[i] = x0[i] - rng[i];
+      ub[i] = x0[i] + rng[i];
+    }
+    double pts[nd + 1][nd], vals[nd + 1];
+    for (int i = 0; i <= nd; i++)
+      for (int e = 0; e < nd; e++) pts[i][e] = x0[e];
+    for (int i = 0; i < nd; i++) {
+      const double st = fmin(0.25 * (ub[i] - lb[i]), fmin(0.75 * (ub[i] - x0[i]), 0.75 * (x0[i] - lb[i])));
+      for (int e = 0; e < nd; e++) pts[i + 1][e] = e == i ? x0[e] + st : x0[e] + 0.0;
+    }
+    for (int i = 0; i <= nd; i++) vals[i] = energy(pts[i]);
+    int nev = nd + 1;
+    auto clampe = [&](int e, double v) { return fmin(fmax(v, lb[e]), ub[e]); };
+    double c[nd], xr[nd], xe[nd], xc[nd];
+    while (nev < nm_evals) {
+      for (int i = 1; i <= nd; i++)
+        for (int jj = i; jj > 0 && vals[jj] < vals[jj - 1]; jj--) {
+          const double tv = vals[jj];
+          vals[jj] = vals[jj - 1];
+          vals[jj - 1] = tv;
+          for (int e = 0; e < nd; e++) {
+            const double tp = pts[jj][e];
+            pts[jj][e] = pts[jj - 1][e];
+            pts[jj - 1][e] = tp;
+          }
+        }
+      for (int e = 0; e < nd; e++) {
+        double sm = pts[0][e];
+        for (int i = 1; i < nd; i++) sm = sm + pts[i][e];
+        c[e] = sm / (double)nd;
+      }
+      for (int e = 0; e < nd; e++) xr[e] = clampe(e, c[e] + (c[e] - pts[nd][e]));
+      const double fr = energy(xr);
+      nev++;
+      if (fr < vals[0] && nev < nm_evals) {
+        for (int e = 0; e < nd; e++) xe[e] = clampe(e, c[e] + 2.0 * (c[e] - pts[nd][e]));
+        const double fe = energy(xe);
+        nev++;
+        const bool ex = fe < fr;
+        for (int e = 0; e < nd; e++) pts[nd][e] = ex ? xe[e] : xr[e];
+        vals[nd] = ex ? fe : fr;
+      } else if (fr < vals[nd - 1]) {
+        for (int e = 0; e < nd; e++) pts[nd][e] = xr[e];
+        vals[nd] = fr;
+      } else if (nev < nm_evals) {
+        for (int e = 0; e < nd; e++)
+          xc[e] = fr >= vals[nd] ? clampe(e, c[e] + 0.5 * (pts[nd][e] - c[e])) : clampe(e, c[e] + 0.5 * (xr[e] - c[e]));
+        const double fc = energy(xc);
+        nev++;
+        if (fc < fmin(fr, vals[nd])) {
+          for (int e = 0; e < nd; e++) pts[nd][e] = xc[e];
+          vals[nd] = fc;
+        } else {
+          const int sm = min(nd, nm_evals - nev);
+          for (int i = 1; i <= sm; i++) {
+            for (int e = 0; e < nd; e++) pts[i][e] = clampe(e, pts[0][e] + 0.5 * (pts[i][e] - pts[0][e]));
+            vals[i] = energy(pts[i]);
+          }
+          nev += sm > 0 ? sm : 0;
+        }
+      }
+    }
+    int bi = 0;
+    for (int i = 1; i <= nd; i++)
+      if (vals[i] < vals[bi]) bi = i;
+    rod_v2m(pts[bi], P.R);
+    for (int i = 0; i < 3; i++) P.t[i] = pts[bi][3 + i];
+    en = (float)vals[bi];
+  }
+  if (lane != 0) return;
+  energy_out[obj] = en;
+  for (int y = 0; y < 3; y++)
+    for (int x = 0; x < 4; x++) poses_out[obj + C * (y * 4 + x)] = x < 3 ? (float)P.R[y * 3 + x] : (float)P.t[y];
+}
+
 struct Layout {
   size_t colcnt, coloff, count, lists, listoff, objs, nobj, subcnt, hyp, att, rl, rc, rm, sub, total;
 };
@@ -796,10 +1594,9 @@ extern "C" int pcnn_pose2d(const int32_t* label, const float* vertmap, const flo
   hipLaunchKernelGGL(k_p2d_scatter, dim3((W + 3) / 4), dim3(256), 0, st, label, H, W, C, ws);
   hipLaunchKernelGGL(k_p2d_subset, dim3(C, kRounds), dim3(1024), 0, st, seed, ws);
   const int T = max_iter < kAttempts ? max_iter : kAttempts;
-  hipLaunchKernelGGL(k_p2d_attempts, dim3((n_hyp * T + 63) / 64), dim3(64), 0, st, vertmap, extents, H, W, C, k, seed,
-                     n_hyp, T, ws);
-  hipLaunchKernelGGL(k_p2d_pick, dim3(n_hyp), dim3(64), 0, st, vertmap, extents, H, W, C, k, seed, n_hyp, max_iter, T,
-                     ws, hyps_out, hyp_px);
+  const AttArgs A{vertmap, extents, nullptr, H, W, C, k, seed};
+  hipLaunchKernelGGL(k_attempts<false>, dim3((n_hyp * T + 63) / 64), dim3(64), 0, st, A, n_hyp, T, ws);
+  hipLaunchKernelGGL(k_pick<false>, dim3(n_hyp), dim3(64), 0, st, A, n_hyp, max_iter, T, ws, hyps_out, hyp_px);
   hipLaunchKernelGGL(k_p2d_collect, dim3(C), dim3(64), 0, st, n_hyp, ws);
   for (int r = 0; r < kRounds; r++) {
     const int gx = std::max(1, n_hyp >> r);  // survivors halve each round (one stays one)
@@ -807,6 +1604,119 @@ extern "C" int pcnn_pose2d(const int32_t* label, const float* vertmap, const flo
     hipLaunchKernelGGL(k_p2d_select, dim3(C), dim3(1024), 0, st, ws);
   }
   hipLaunchKernelGGL(k_p2d_finish, dim3(C), dim3(64), 0, st, C, n_hyp, ws, final_out, poses_out);
+  PCNN_CHECK_LAUNCH();
+  return PCNN_OK;
+}
+
+namespace {
+
+struct Layout3 {
+  Layout b;
+  size_t eye, valid, imask, pick, npick, total;
+  int mwords;
+};
+
+Layout3 layout3(int H, int W, int C, int n_hyp) {
+  Layout3 l;
+  l.b = layout(H, W, C, n_hyp);
+  size_t off = l.b.total;
+  auto take = [&](size_t bytes) {
+    off = pcnn::align_up(off, 256);
+    const size_t o = off;
+    off += bytes;
+    return o;
+  };
+  const long HW = (long)H * W;
+  l.mwords = (int)((HW + 63) / 64);
+  l.eye = take((size_t)HW * 3 * sizeof(float));
+  l.valid = take((size_t)valid_blocks((int)HW) * 4 * sizeof(uint64_t));
+  l.imask = take((size_t)n_hyp * l.mwords * sizeof(uint64_t));
+  l.pick = take((size_t)n_hyp * kMaxInl * sizeof(int32_t));
+  l.npick = take((size_t)n_hyp * sizeof(int32_t));
+  l.total = off + 256;
+  return l;
+}
+
+P2dWs carve2(char* base, const Layout& l) {
+  P2dWs ws;
+  ws.colcnt = (int32_t*)(base + l.colcnt);
+  ws.coloff = (int32_t*)(base + l.coloff);
+  ws.count = (int32_t*)(base + l.count);
+  ws.lists = (int32_t*)(base + l.lists);
+  ws.listoff = (int32_t*)(base + l.listoff);
+  ws.objs = (int32_t*)(base + l.objs);
+  ws.nobj = (int32_t*)(base + l.nobj);
+  ws.subcnt = (int32_t*)(base + l.subcnt);
+  ws.hyp = (double*)(base + l.hyp);
+  ws.att = (double*)(base + l.att);
+  ws.rl = (int32_t*)(base + l.rl);
+  ws.rc = (int32_t*)(base + l.rc);
+  ws.rm = (int32_t*)(base + l.rm);
+  ws.sub = (int32_t*)(base + l.sub);
+  return ws;
+}
+
+}  // namespace
+
+extern "C" size_t pcnn_pose3d_workspace_size(int H, int W, int C, int n_hyp) {
+  if (H <= 0 || W <= 0 || C <= 0 || n_hyp <= 0) return 256;
+  return layout3(H, W, C, n_hyp).total;
+}
+
+extern "C" int pcnn_pose3d(const int32_t* label, const uint16_t* depth, const float* vertmap, const float* extents,
+                           int H, int W, int C, float fx, float fy, float px, float py, float depth_factor,
+                           uint64_t seed, int n_hyp, int max_iter, int nm_evals, float* poses_out, float* hyps_out,
+                           int32_t* hyp_px, int32_t* inl_out, int32_t* final_out, float* energy_out, float* eye_out,
+                           void* workspace, size_t workspace_bytes, void* stream) {
+  PCNN_REQUIRE(label && depth && vertmap && extents && poses_out && hyps_out && hyp_px && inl_out && final_out &&
+               energy_out);
+  PCNN_REQUIRE(H > 0 && W > 0 && C > 1 && C <= 64 && n_hyp > 0 && n_hyp <= kMaxHyp && max_iter > 0 && nm_evals > 0);
+  PCNN_REQUIRE((long)H * W < (1l << 28));
+  const Layout3 l = layout3(H, W, C, n_hyp);
+  if (!workspace || workspace_bytes < l.total) return PCNN_ECAPACITY;
+  char* base = (char*)workspace;
+  P3dWs w3;
+  w3.b = carve2(base, l.b);
+  w3.eye = (float*)(base + l.eye);
+  w3.valid = (uint64_t*)(base + l.valid);
+  w3.imask = (uint64_t*)(base + l.imask);
+  w3.pick = (int32_t*)(base + l.pick);
+  w3.npick = (int32_t*)(base + l.npick);
+  w3.mwords = l.mwords;
+  const P2dWs& ws = w3.b;
+  hipStream_t st = (hipStream_t)stream;
+  if (hipMemsetAsync(poses_out, 0, (size_t)12 * C * sizeof(float), st) != hipSuccess) return PCNN_EHIP;
+  if (hipMemsetAsync(energy_out, 0, (size_t)C * sizeof(float), st) != hipSuccess) return PCNN_EHIP;
+  if (hipMemsetAsync(inl_out, 0xFF, (size_t)n_hyp * kRounds * sizeof(int32_t), st) != hipSuccess) return PCNN_EHIP;
+  if (hipMemsetAsync(final_out, 0xFF, (size_t)C * 3 * sizeof(int32_t), st) != hipSuccess) return PCNN_EHIP;
+  if (hipMemsetAsync(ws.rm, 0, (size_t)C * sizeof(int32_t), st) != hipSuccess) return PCNN_EHIP;
+  const Cam k{fx, fy, px, py};
+  const int HW = H * W;
+  hipLaunchKernelGGL(k_p3d_eye, dim3((HW + 255) / 256), dim3(256), 0, st, depth, H, W, fx, fy, px, py, depth_factor,
+                     w3.eye);
+  hipLaunchKernelGGL(k_p2d_colcount, dim3((W + 3) / 4), dim3(256), 0, st, label, H, W, C, ws.colcnt);
+  hipLaunchKernelGGL(k_p2d_scan, dim3(C), dim3(1024), 0, st, ws.colcnt, W, ws.coloff, ws.count);
+  hipLaunchKernelGGL(k_p2d_objs, dim3(1), dim3(64), 0, st, C, ws);
+  hipLaunchKernelGGL(k_p2d_scatter, dim3((W + 3) / 4), dim3(256), 0, st, label, H, W, C, ws);
+  hipLaunchKernelGGL(k_p3d_valid, dim3(valid_blocks(HW)), dim3(256), 0, st, C, w3);
+  hipLaunchKernelGGL(k_p3d_subset, dim3(C, kRounds), dim3(1024), 0, st, seed, w3);
+  const int T = max_iter < kAttempts ? max_iter : kAttempts;
+  const AttArgs A{vertmap, extents, w3.eye, H, W, C, k, seed};
+  hipLaunchKernelGGL(k_attempts<true>, dim3((n_hyp * T + 63) / 64), dim3(64), 0, st, A, n_hyp, T, ws);
+  hipLaunchKernelGGL(k_pick<true>, dim3(n_hyp), dim3(64), 0, st, A, n_hyp, max_iter, T, ws, hyps_out, hyp_px);
+  hipLaunchKernelGGL(k_p2d_collect, dim3(C), dim3(64), 0, st, n_hyp, ws);
+  for (int r = 0; r < kRounds; r++) {
+    const int gx = std::max(1, n_hyp >> r);  // survivors halve each round (one stays one)
+    hipLaunchKernelGGL(k_p3d_count, dim3(gx, C), dim3(256), 0, st, vertmap, extents, C, w3, r, inl_out);
+    hipLaunchKernelGGL(k_p2d_select, dim3(C), dim3(1024), 0, st, ws);
+    hipLaunchKernelGGL(k_p3d_update, dim3(std::max(1, n_hyp >> (r + 1)), C), dim3(64), 0, st, vertmap, extents, C,
+                       seed, w3, r);
+  }
+  hipLaunchKernelGGL(k_p3d_finish, dim3(C), dim3(64), 0, st, vertmap, extents, C, n_hyp, seed, nm_evals, w3, final_out,
+                     poses_out, energy_out);
+  if (eye_out &&
+      hipMemcpyAsync(eye_out, w3.eye, (size_t)HW * 3 * sizeof(float), hipMemcpyDeviceToDevice, st) != hipSuccess)
+    return PCNN_EHIP;
   PCNN_CHECK_LAUNCH();
   return PCNN_OK;
 }

@@ -10,7 +10,8 @@ import numpy as np
 from refine_scene import CAMERA, axis_angle_quat, quat_to_R, render_box
 
 
-def make_scene(seed=0, n_obj=3, C=6, H=480, W=640, coord_noise=0.0, extents=None):
+def make_scene(seed=0, n_obj=3, C=6, H=480, W=640, coord_noise=0.0, extents=None, depth_factor=10000.0,
+               hole_frac=0.0, depth_noise=0.0):
     rng = np.random.default_rng(seed)
     if extents is None:
         extents = np.zeros((C, 3), np.float32)
@@ -40,4 +41,13 @@ def make_scene(seed=0, n_obj=3, C=6, H=480, W=640, coord_noise=0.0, extents=None
             norm = norm + rng.normal(0, coord_noise, size=norm.shape)
         vertmap[front, 3 * c:3 * c + 3] = norm[front].astype(np.float32)
         poses[int(c)] = dict(R=quat_to_R(q), t=t, uv=(u, v))
-    return dict(label=label, vertmap=vertmap, extents=extents.astype(np.float32), poses=poses, camera=CAMERA, C=C)
+    # raw depth for estimatePose3D (getEye, synthesize.cpp:1393): the
+    # z-buffer in depth_factor units, optional noise (m) and holes (0)
+    z = np.where(np.isfinite(zbuf), zbuf, 1.5)
+    if depth_noise:
+        z = z + rng.normal(0, depth_noise, size=z.shape)
+    depth = np.clip(np.rint(z * depth_factor), 1, 65535).astype(np.uint16)
+    if hole_frac:
+        depth[rng.uniform(size=depth.shape) < hole_frac] = 0
+    return dict(label=label, vertmap=vertmap, extents=extents.astype(np.float32), poses=poses, camera=CAMERA, C=C,
+                depth=depth, depth_factor=float(depth_factor))
