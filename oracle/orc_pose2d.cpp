@@ -467,7 +467,8 @@ ORC_API int orc_pose2d(const int* label, const float* vertmap, const float* exte
 //     cross product of the first two when its singular value is below 1e-9 of
 //     the first (three-point covariances have rank two): R = V D U^T does
 //     not depend on the SVD's sign conventions.  The centroid and covariance
-//     sums run in the GPU wave's fold64 order (OpenCV: sequential).
+//     sums, and optEnergy3D's float sum, run in the GPU workgroup's fixed
+//     tree (tree1024; the reference's loops are sequential).
 //   * sin, cos, acos (Rodrigues) from + - * / sqrt only (dsincos, dacos), so
 //     the GPU reproduces them bit for bit; libm differs in the last ulp.
 //   * Hypothesis poses stay (R, t) between steps; the reference round-trips
@@ -476,9 +477,7 @@ ORC_API int orc_pose2d(const int* label, const float* vertmap, const float* exte
 //   * refineWithOpt's NLopt LN_NELDERMEAD is the bounded Nelder-Mead of
 //     posecnn_amd/synthesize/icp.py nelder_mead_steps (6 parameters: Rodrigues
 //     vector and translation, +-10 deg / +-0.1 / +-0.1 / +-0.5 m bounds, 100
-//     evaluations); optEnergy3D's float sum of double distances is taken as
-//     64 strided float partial sums folded by halving (i < off: p[i] +=
-//     p[i + off]), the order the GPU's wave uses.
+//     evaluations).
 namespace {
 
 struct TStream {  // Philox words of the stream (draw, h, tag, a)
@@ -562,33 +561,40 @@ double det3(const double* m) {
   return m[0] * (m[4] * m[8] - m[5] * m[7]) - m[1] * (m[3] * m[8] - m[5] * m[6]) + m[2] * (m[3] * m[7] - m[4] * m[6]);
 }
 
-// 64 strided partial sums folded by halving -- the order of a wave that
-// gives lane l the elements l, l + 64, ... and then adds p[i + off] into p[i]
-// for off = 32, 16, ..., 1 (posecnn_amd/csrc/pose2d.hip fold64)
-template <class F>
-double fold64(F x, int n) {
-  double p[64];
-  for (int l = 0; l < 64; l++) {
-    p[l] = 0.0;
-    for (int i = l; i < n; i += 64) p[l] = p[l] + x(i);
+// The fixed summation tree of the GPU's 1024-thread workgroups (n <= 1024):
+// leaf i = 0.0 + x_i (0.0 past n); each 64-leaf wave folds by halving
+// (p_i += p_{i + off}, off = 32 .. 1), then the 16 wave sums fold the same way
+// (off = 8 .. 1) -- posecnn_amd/csrc/pose2d.hip tree_sum
+template <class T, class F>
+T tree1024(F x, int n) {
+  T p[1024];
+  for (int i = 0; i < 1024; i++) p[i] = i < n ? (T)0 + x(i) : (T)0;
+  T w[16];
+  for (int v = 0; v < 16; v++) {
+    T* q = p + 64 * v;
+    for (int off = 32; off >= 1; off >>= 1)
+      for (int i = 0; i < off; i++) q[i] = q[i] + q[i + off];
+    w[v] = q[0];
   }
-  for (int off = 32; off >= 1; off >>= 1)
-    for (int i = 0; i < off; i++) p[i] = p[i] + p[i + off];
-  return p[0];
+  for (int off = 8; off >= 1; off >>= 1)
+    for (int i = 0; i < off; i++) w[i] = w[i] + w[i + off];
+  return w[0];
 }
+template <class F>
+double tsum(F x, int n) { return tree1024<double>(x, n); }
 
 // calcRigidBodyTransform (Hypothesis.cpp:186-241): b ~ R a + t.  The
-// centroid and covariance sums in fold64 order (OpenCV: sequential).
+// centroid and covariance sums in tree1024 order (OpenCV: sequential).
 Pose kabsch(const V3* a, const V3* b, int n) {
   const double inv = 1.0 / (double)n;
-  const V3 cA{fold64([&](int i) { return a[i].x; }, n) * inv, fold64([&](int i) { return a[i].y; }, n) * inv,
-              fold64([&](int i) { return a[i].z; }, n) * inv};
-  const V3 cB{fold64([&](int i) { return b[i].x; }, n) * inv, fold64([&](int i) { return b[i].y; }, n) * inv,
-              fold64([&](int i) { return b[i].z; }, n) * inv};
+  const V3 cA{tsum([&](int i) { return a[i].x; }, n) * inv, tsum([&](int i) { return a[i].y; }, n) * inv,
+              tsum([&](int i) { return a[i].z; }, n) * inv};
+  const V3 cB{tsum([&](int i) { return b[i].x; }, n) * inv, tsum([&](int i) { return b[i].y; }, n) * inv,
+              tsum([&](int i) { return b[i].z; }, n) * inv};
   double H[9];  // pointsA * pointsB^T
   for (int r = 0; r < 3; r++)
     for (int c = 0; c < 3; c++)
-      H[r * 3 + c] = fold64(
+      H[r * 3 + c] = tsum(
           [&](int i) {
             const double pa = r == 0 ? a[i].x - cA.x : r == 1 ? a[i].y - cA.y : a[i].z - cA.z;
             const double pb = c == 0 ? b[i].x - cB.x : c == 1 ? b[i].y - cB.y : b[i].z - cB.z;
@@ -723,28 +729,28 @@ Pose kabsch_corr(const std::vector<Corr>& v) {
 }
 
 // optEnergy3D (:1464-1507): mean distance of the transformed object
-// coordinates to the camera coordinates; the float sum in the GPU's order
+// coordinates to the camera coordinates; the float sum of the double
+// distances (each rounded to float) in tree1024 order (the reference: a
+// sequential float accumulator)
 double energy3d(const double* x, const std::vector<Corr>& v) {
   double Rd[9];
   rod_v2m(x, Rd);
   float Rf[9];
   for (int i = 0; i < 9; i++) Rf[i] = (float)Rd[i];  // jp::double2float
-  float part[64] = {0};
-  for (size_t i = 0; i < v.size(); i++) {
-    const F3 o = v[i].obj;
-    float tr[3];
-    for (int r = 0; r < 3; r++) {
-      const float m = Rf[r * 3 + 0] * o.x + Rf[r * 3 + 1] * o.y + Rf[r * 3 + 2] * o.z;
-      tr[r] = (float)((double)m + x[3 + r]);
-    }
-    const double dx = (double)tr[0] - (double)v[i].eye.x, dy = (double)tr[1] - (double)v[i].eye.y,
-                 dz = (double)tr[2] - (double)v[i].eye.z;
-    float& p = part[i % 64];
-    p = (float)((double)p + std::sqrt(dx * dx + dy * dy + dz * dz));
-  }
-  for (int off = 32; off >= 1; off >>= 1)
-    for (int i = 0; i < off; i++) part[i] = part[i] + part[i + off];
-  return (double)(part[0] / (float)v.size());
+  const float tot = tree1024<float>(
+      [&](int i) {
+        const F3 o = v[i].obj;
+        float tr[3];
+        for (int r = 0; r < 3; r++) {
+          const float m = Rf[r * 3 + 0] * o.x + Rf[r * 3 + 1] * o.y + Rf[r * 3 + 2] * o.z;
+          tr[r] = (float)((double)m + x[3 + r]);
+        }
+        const double dx = (double)tr[0] - (double)v[i].eye.x, dy = (double)tr[1] - (double)v[i].eye.y,
+                     dz = (double)tr[2] - (double)v[i].eye.z;
+        return (float)std::sqrt(dx * dx + dy * dy + dz * dz);
+      },
+      (int)v.size());
+  return (double)(tot / (float)v.size());
 }
 
 // the bounded Nelder-Mead of icp.py nelder_mead_steps (n parameters)

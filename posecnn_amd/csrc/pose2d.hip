@@ -593,18 +593,23 @@ __device__ void svd3(const double* A, double* U, double* S, double* V) {
     for (int r = 0; r < 3; r++) a = a + M[r * 3 + i] * M[r * 3 + i];
     sv[i] = sqrt(a);
   }
-  int o[3] = {0, 1, 2};  // descending, stable
-  for (int i = 1; i < 3; i++)
-    for (int j = i; j > 0 && sv[o[j]] > sv[o[j - 1]]; j--) {
-      const int tmp = o[j];
-      o[j] = o[j - 1];
-      o[j - 1] = tmp;
-    }
+  // descending, stable (the oracle's insertion sort), as selects: no
+  // dynamically indexed arrays, so everything stays in registers
+  auto pick3 = [](const double* a, int i) { return i == 0 ? a[0] : i == 1 ? a[1] : a[2]; };
+  int o0 = 0, o1 = 1, o2 = 2;
+  if (pick3(sv, o1) > pick3(sv, o0)) { const int tmp = o0; o0 = o1; o1 = tmp; }
+  if (pick3(sv, o2) > pick3(sv, o1)) {
+    { const int tmp = o1; o1 = o2; o2 = tmp; }
+    if (pick3(sv, o1) > pick3(sv, o0)) { const int tmp = o0; o0 = o1; o1 = tmp; }
+  }
+  const int o[3] = {o0, o1, o2};
+#pragma unroll
   for (int kk = 0; kk < 3; kk++) {
-    S[kk] = sv[o[kk]];
+    S[kk] = pick3(sv, o[kk]);
+#pragma unroll
     for (int r = 0; r < 3; r++) {
-      V[r * 3 + kk] = Vm[r * 3 + o[kk]];
-      U[r * 3 + kk] = S[kk] > 0 ? M[r * 3 + o[kk]] / S[kk] : 0.0;
+      V[r * 3 + kk] = pick3(Vm + r * 3, o[kk]);
+      U[r * 3 + kk] = S[kk] > 0 ? pick3(M + r * 3, o[kk]) / S[kk] : 0.0;
     }
   }
   if (!(S[2] > 1e-9 * S[0])) {
@@ -620,7 +625,7 @@ __device__ __forceinline__ double det3(const double* m) {
 
 // calcRigidBodyTransform (Hypothesis.cpp:217-241) from the centroids and the
 // covariance: R = V diag(1, 1, sign det(V U^T)) U^T, t = -R cA + cB
-__device__ Pose rigid_from_cov(const double* Hc, const double* cA, const double* cB) {
+__device__ __forceinline__ Pose rigid_from_cov(const double* Hc, const double* cA, const double* cB) {
   double U[9], S[3], V[9];
   svd3(Hc, U, S, V);
   double VU[9];
@@ -635,9 +640,19 @@ __device__ Pose rigid_from_cov(const double* Hc, const double* cA, const double*
   return P;
 }
 
-// the 64-lane fold (partials p_l over elements l, l + 64, ...; then p_i +=
-// p_{i + off}, off = 32 .. 1) of n <= 4 elements held by one lane: the same
-// additions, zeros included, as the wave version below
+// out of line for the 1024-thread k_p3d_update: only its thread 0 runs it,
+// and inlined it would set the whole workgroup's register budget
+__device__ __noinline__ Pose rigid_from_cov_ool(const double* Hc, const double* cA, const double* cB) {
+  return rigid_from_cov(Hc, cA, cB);
+}
+
+// The fixed summation tree of a 1024-thread workgroup (the oracle's
+// tree1024): leaf i = 0.0 + x_i (0 past n), each wave folds its 64 leaves by
+// halving (p_i += p_{i + off}, off = 32 .. 1), then the 16 wave sums fold the
+// same way (off = 8 .. 1).
+// fold_small<n>: that tree over n <= 4 leaves held by one lane, zeros
+// included (the additions of 0.0 matter only to the sign of a zero, kept
+// anyway)
 template <int n>
 __device__ __forceinline__ double fold_small(const double* x) {
   double p[64];
@@ -647,25 +662,34 @@ __device__ __forceinline__ double fold_small(const double* x) {
   for (int off = 32; off >= 1; off >>= 1)
 #pragma unroll
     for (int i = 0; i < off; i++) p[i] = p[i] + p[i + off];
-  return p[0];
+  double w = p[0];
+#pragma unroll
+  for (int off = 8; off >= 1; off >>= 1) w = w + 0.0;  // the other 15 wave sums are zero
+  return w;
 }
 
-// the wave's fold of per-lane partials; the sum is returned on every lane
-__device__ __forceinline__ double fold64(double v) {
+// the in-wave half of the tree: the wave's sum on lane 0 (other lanes: partial)
+template <class T>
+__device__ __forceinline__ T wave_fold(T v) {
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) {
-    const double w = __shfl_down(v, off, 64);
+    const T w = __shfl_down(v, off, 64);
     v = v + w;
   }
-  return __shfl(v, 0, 64);
+  return v;
 }
-__device__ __forceinline__ float fold64f(float v) {
+
+// the cross-wave half: ws[16][K] wave sums (LDS, visible) -> the tree's total
+template <class T, int K>
+__device__ __forceinline__ T cross_fold(const T (*ws)[K], int k) {
+  T w[16];
 #pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) {
-    const float w = __shfl_down(v, off, 64);
-    v = v + w;
-  }
-  return __shfl(v, 0, 64);
+  for (int i = 0; i < 16; i++) w[i] = ws[i][k];
+#pragma unroll
+  for (int off = 8; off >= 1; off >>= 1)
+#pragma unroll
+    for (int i = 0; i < off; i++) w[i] = w[i] + w[i + off];
+  return w[0];
 }
 
 __device__ __forceinline__ D3 xform(const Pose& P, D3 p) {  // Hypothesis::transform
@@ -960,18 +984,9 @@ __global__ void __launch_bounds__(256) k_p2d_count(const float* __restrict__ vm,
   }
 }
 
-// stable sort by inliers (descending, then list position), keep the better half
-__global__ void __launch_bounds__(1024) k_p2d_select(P2dWs ws) {
-  __shared__ int hl[kMaxHypBlock], hc[kMaxHypBlock], tmp[kMaxHypBlock];
-  const int oi = blockIdx.x;
-  if (oi >= *ws.nobj) return;
-  const int m = ws.rm[oi];
-  if (m <= 1) return;
-  for (int j = threadIdx.x; j < m; j += blockDim.x) {
-    hl[j] = ws.rl[oi * kMaxHypBlock + j];
-    hc[j] = ws.rc[oi * kMaxHypBlock + j];
-  }
-  __syncthreads();
+// stable sort by inliers (descending, then list position), keep the better
+// half; hl / hc (the m survivors and counts) are in LDS and visible
+__device__ void keep_better_half(const P2dWs& ws, int oi, int m, const int* hl, const int* hc, int* tmp) {
   for (int j = threadIdx.x; j < m; j += blockDim.x) {
     int rank = 0;
     for (int q = 0; q < m; q++) rank += hc[q] > hc[j] || (hc[q] == hc[j] && q < j);
@@ -984,6 +999,20 @@ __global__ void __launch_bounds__(1024) k_p2d_select(P2dWs ws) {
     ws.rc[oi * kMaxHypBlock + j] = hc[tmp[j]];
   }
   if (threadIdx.x == 0) ws.rm[oi] = keep;
+}
+
+__global__ void __launch_bounds__(1024) k_p2d_select(P2dWs ws) {
+  __shared__ int hl[kMaxHypBlock], hc[kMaxHypBlock], tmp[kMaxHypBlock];
+  const int oi = blockIdx.x;
+  if (oi >= *ws.nobj) return;
+  const int m = ws.rm[oi];
+  if (m <= 1) return;
+  for (int j = threadIdx.x; j < m; j += blockDim.x) {
+    hl[j] = ws.rl[oi * kMaxHypBlock + j];
+    hc[j] = ws.rc[oi * kMaxHypBlock + j];
+  }
+  __syncthreads();
+  keep_better_half(ws, oi, m, hl, hc, tmp);
 }
 
 __global__ void __launch_bounds__(64) k_p2d_finish(int C, int n_hyp, P2dWs ws, int32_t* __restrict__ final_out,
@@ -1027,13 +1056,13 @@ __global__ void __launch_bounds__(64) k_p2d_finish(int C, int n_hyp, P2dWs ws, i
 //       each: filterInliers3D (:1308-1322; pick k of round r on its own
 //       stream (draw, h, 'F3D', 1024 r + k)), the inlier ranks resolved to
 //       subset positions by a popcount prefix, then the rigid transform with
-//       the wave's fold64 sums and the 3x3 Jacobi SVD;
+//       the workgroup-tree sums and the 3x3 Jacobi SVD;
 //   k_p3d_finish: the survivor's output (:1936-1964): when it has more than
 //       minPixels = 10 inliers, filterInliers3D again (r = 8) and
 //       refineWithOpt (:1510-1567) -- the bounded Nelder-Mead over the
 //       Rodrigues vector and translation (+-10 deg, +-0.1, +-0.1, +-0.5 m,
-//       100 evaluations) of optEnergy3D (:1464-1507), one wave per object,
-//       the energy's float sum as 64 strided partials folded by halving.
+//       100 evaluations) of optEnergy3D (:1464-1507), one workgroup per
+//       object, the energy's float sum in the workgroup tree.
 
 struct P3dWs {
   P2dWs b;
@@ -1042,12 +1071,30 @@ struct P3dWs {
   uint64_t* imask;  // (n_hyp, mwords) inlier bits over the round's subset
   int32_t* pick;    // (n_hyp, kMaxInl) pixels of the last refit's correspondences
   int32_t* npick;   // (n_hyp)
+  int32_t* pcnt;    // (C, kMaxHypBlock, kCntZ) partial inlier counts of k_p3d_count
   int mwords;
 };
 
 constexpr int kMaxInl = 1000;     // maxPixels: filterInliers3D's cap (:1796)
 constexpr int kLdsWords = 5120;   // class-list bits kept in LDS by k_p3d_subset (327,680 positions)
+constexpr int kSkipMax = 65536;   // class lists up to this long also get the per-position skip bytes
 constexpr int kPrefWords = 2048;  // subset words with an LDS popcount prefix in k_p3d_update
+constexpr int kCntChunk = 512;    // subset entries per k_p3d_count workgroup pass
+constexpr int kCntZ = 16;         // k_p3d_count workgroups per hypothesis
+constexpr int kFinThreads = 1024;  // k_p3d_finish workgroup (one correspondence per thread)
+
+// the outputs' initial values (one launch instead of five fills)
+__global__ void __launch_bounds__(1024) k_p3d_init(int C, int n_hyp, float* __restrict__ poses_out,
+                                                   float* __restrict__ energy_out, int32_t* __restrict__ inl_out,
+                                                   int32_t* __restrict__ final_out, int32_t* __restrict__ rm) {
+  for (int i = threadIdx.x; i < 12 * C; i += 1024) poses_out[i] = 0.f;
+  for (int i = threadIdx.x; i < C; i += 1024) {
+    energy_out[i] = 0.f;
+    rm[i] = 0;
+  }
+  for (int i = threadIdx.x; i < 3 * C; i += 1024) final_out[i] = -1;
+  for (int i = threadIdx.x; i < kRounds * n_hyp; i += 1024) inl_out[i] = -1;
+}
 
 __global__ void __launch_bounds__(256) k_p3d_eye(const uint16_t* __restrict__ depth, int H, int W, float fx, float fy,
                                                  float px, float py, float factor, float* __restrict__ eye) {
@@ -1091,6 +1138,7 @@ __device__ __forceinline__ uint64_t class_word(const uint64_t* __restrict__ V, l
 
 __global__ void __launch_bounds__(1024) k_p3d_subset(uint64_t seed, P3dWs w3) {
   __shared__ uint64_t bits[kLdsWords];  // 40 KiB
+  __shared__ uint8_t skip[kSkipMax];     // 64 KiB
   __shared__ int wsum[16];
   __shared__ long qrel[1024];
   __shared__ int sh_int[4];
@@ -1150,6 +1198,37 @@ __global__ void __launch_bounds__(1024) k_p3d_subset(uint64_t seed, P3dWs w3) {
     subset_nohole(seed, c, r, N, q, S, cnt_out, wsum);
     return;
   }
+  // skip[x] = next_valid(x) - x (0: x valid; 255: 255 or more, resolved by a
+  // word search) when the class list fits kSkipMax bytes: one LDS byte per
+  // walk step decides both "hole?" and "how far"
+  const bool use_skip = N <= kSkipMax;  // block-uniform
+  if (use_skip) {
+    for (int x = t; x < N; x += 1024) {
+      const int k = x >> 6;
+      uint64_t w = word(k) >> (x & 63);
+      int d = 0;
+      if (!(w & 1ull)) {
+        if (w) {
+          d = __ffsll((unsigned long long)w) - 1;
+        } else {
+          d = 64 - (x & 63);
+          for (int kk = k + 1; d < 255; kk++, d += 64) {
+            if (kk >= nw) {
+              d = N - x;  // no valid position after x: the walk leaves the list
+              break;
+            }
+            const uint64_t v = word(kk);
+            if (v) {
+              d += __ffsll((unsigned long long)v) - 1;
+              break;
+            }
+          }
+        }
+      }
+      skip[x] = (uint8_t)(d < 255 ? d : 255);
+    }
+    __syncthreads();
+  }
   long carry = 0;  // q_{j0}: the hole-free position of draw j0
   long D = 0;      // holes skipped so far (wave 0)
   for (int j0 = 0;; j0 += 1024) {
@@ -1169,13 +1248,62 @@ __global__ void __launch_bounds__(1024) k_p3d_subset(uint64_t seed, P3dWs w3) {
     }
     qrel[t] = wb + incl - g;
     __syncthreads();
-    if (wave == 0) {
+    if (wave == 0 && use_skip) {  // the lean walk: 32-bit positions, one LDS byte per step
+      int done = 0, cnt = 0, Di = (int)D;  // D < N <= kSkipMax
+      for (int sc = 0; sc < 16 && !done; sc++) {
+        const int jl = sc * 64 + lane;
+        const long ql = carry + qrel[jl];
+        const int qj = ql < N ? (int)ql : N;  // every position at or past N means "past the list"
+        int s = 0, pos = 0, nvalid = 64;
+        for (;;) {  // wave-uniform; one hole hit resolved per step
+          const int x = qj + Di;
+          const int hv = x < N ? (int)skip[x] : 0;
+          const bool ev = lane >= s && (x >= N || hv != 0);
+          const uint64_t b = __ballot(ev);
+          const int first = b ? __ffsll((unsigned long long)b) - 1 : 64;
+          if (lane >= s && lane < first) pos = x;
+          if (first == 64) break;
+          const int xs = __builtin_amdgcn_readlane(x, first);
+          int hs = __builtin_amdgcn_readlane(hv, first);
+          if (xs < N && hs == 255) {  // a run of 255 or more holes: the word search
+            long nh = N;
+            for (long kb = (xs >> 6); kb < nw; kb += 64) {
+              const long k = kb + lane;
+              uint64_t v = k < nw ? bits[k] : 0ull;
+              if (k == (xs >> 6)) v &= ~0ull << (xs & 63);
+              const uint64_t hit = __ballot(v != 0ull);
+              if (hit) {
+                const int l = __ffsll((unsigned long long)hit) - 1;
+                const uint64_t vv = __shfl((unsigned long long)v, l, 64);
+                nh = 64 * (kb + l) + __ffsll((unsigned long long)vv) - 1;
+                break;
+              }
+            }
+            hs = (int)(nh - xs);
+          }
+          if (xs >= N || xs + hs >= N) {  // the walk leaves the list
+            done = 1;
+            cnt = j0 + sc * 64 + first;
+            nvalid = first;
+            break;
+          }
+          Di += hs;
+          s = first;
+        }
+        if (lane < nvalid) S[j0 + jl] = pos;
+      }
+      D = Di;
+      if (lane == 0) {
+        sh_int[1] = done;
+        sh_int[2] = cnt;
+      }
+    } else if (wave == 0) {  // class lists longer than kSkipMax: the bit walk
       int done = 0, cnt = 0;
       for (int sc = 0; sc < 16 && !done; sc++) {
         const int jl = sc * 64 + lane;
         const long qj = carry + qrel[jl];
         int s = 0;
-        for (;;) {  // wave-uniform
+        for (;;) {  // wave-uniform; one hole hit resolved per step
           const long x = qj + D;
           bool ev = false;
           if (lane >= s) ev = x >= N || !((word(x >> 6) >> (x & 63)) & 1ull);
@@ -1185,11 +1313,13 @@ __global__ void __launch_bounds__(1024) k_p3d_subset(uint64_t seed, P3dWs w3) {
           if (first == 64) break;
           const long xs = __shfl(x, first, 64);
           long nh = N;
-          if (xs < N) {  // the next valid position at or after xs (wave-wide word search)
-            for (long kb = xs >> 6; kb < nw; kb += 64) {
+          const uint64_t w0 = xs < N ? word(xs >> 6) >> (xs & 63) : 0ull;
+          if (w0) {  // the hole run ends in this word (the usual case)
+            nh = xs + __ffsll((unsigned long long)w0) - 1;
+          } else if (xs < N) {  // the next valid position past this word (wave-wide word search)
+            for (long kb = (xs >> 6) + 1; kb < nw; kb += 64) {
               const long k = kb + lane;
-              uint64_t v = k < nw ? word(k) : 0ull;
-              if (k == (xs >> 6)) v &= ~0ull << (xs & 63);
+              const uint64_t v = k < nw ? word(k) : 0ull;
               const uint64_t hit = __ballot(v != 0ull);
               if (hit) {
                 const int l = __ffsll((unsigned long long)hit) - 1;
@@ -1222,11 +1352,14 @@ __global__ void __launch_bounds__(1024) k_p3d_subset(uint64_t seed, P3dWs w3) {
   }
 }
 
+// grid (hypothesis slot, object, kCntZ): workgroup z takes the subset chunks
+// z, z + kCntZ, ... of kCntChunk entries and writes its partial count (the
+// chunks' inlier bits go to the hypothesis's mask)
 __global__ void __launch_bounds__(256) k_p3d_count(const float* __restrict__ vm, const float* __restrict__ ext, int C,
-                                                   P3dWs w3, int r, int32_t* __restrict__ inl_out) {
+                                                   P3dWs w3, int r) {
   __shared__ int part[4];
   const P2dWs& ws = w3.b;
-  const int j = blockIdx.x, oi = blockIdx.y, lane = pcnn::lane_id(), wave = threadIdx.x >> 6;
+  const int j = blockIdx.x, oi = blockIdx.y, z = blockIdx.z, lane = pcnn::lane_id(), wave = threadIdx.x >> 6;
   if (oi >= *ws.nobj || j >= ws.rm[oi]) return;  // block-uniform
   const int obj = ws.objs[oi];
   const int* L = ws.lists + ws.listoff[obj];
@@ -1239,27 +1372,48 @@ __global__ void __launch_bounds__(256) k_p3d_count(const float* __restrict__ vm,
   for (int i = 0; i < 3; i++) P.t[i] = hr[10 + i];
   uint64_t* M = w3.imask + (size_t)h * w3.mwords;
   int cnt = 0;
-  for (int i0 = 0; i0 < ns; i0 += 256) {  // countInliers3D (:1255-1287)
-    const int i = i0 + threadIdx.x;
-    bool in = false;
-    if (i < ns) {
-      const int p = L[S[i]];
-      const F3 e = eye_at(w3.eye, p);
-      const F3 o = mode3d(vm, ext, C, obj, p);
-      in = nrm(sub(D3{e.x, e.y, e.z}, xform(P, D3{o.x, o.y, o.z}))) < 0.01;
+  for (int c0 = z * kCntChunk; c0 < ns; c0 += kCntZ * kCntChunk) {  // countInliers3D (:1255-1287)
+    for (int i0 = c0; i0 < c0 + kCntChunk && i0 < ns; i0 += 256) {
+      const int i = i0 + threadIdx.x;
+      bool in = false;
+      if (i < ns) {
+        const int p = L[S[i]];
+        const F3 e = eye_at(w3.eye, p);
+        const F3 o = mode3d(vm, ext, C, obj, p);
+        in = nrm(sub(D3{e.x, e.y, e.z}, xform(P, D3{o.x, o.y, o.z}))) < 0.01;
+      }
+      const uint64_t b = __ballot(in);
+      if (lane == 0 && i0 + 64 * wave < ns) M[(i0 >> 6) + wave] = b;
+      cnt += in;
     }
-    const uint64_t b = __ballot(in);
-    if (lane == 0 && i0 + 64 * wave < ns) M[(i0 >> 6) + wave] = b;
-    cnt += in;
   }
   cnt = pcnn::wave_sum(cnt);
   if (lane == 0) part[wave] = cnt;
   __syncthreads();
-  if (threadIdx.x == 0) {
-    const int c = part[0] + part[1] + part[2] + part[3];
+  if (threadIdx.x == 0) w3.pcnt[((size_t)oi * kMaxHypBlock + j) * kCntZ + z] = part[0] + part[1] + part[2] + part[3];
+}
+
+// the round's counts (partials summed: integers) into rc / inl_out, then the
+// stable halving of k_p2d_select
+__global__ void __launch_bounds__(1024) k_p3d_select(P3dWs w3, int r, int32_t* __restrict__ inl_out) {
+  __shared__ int hl[kMaxHypBlock], hc[kMaxHypBlock], tmp[kMaxHypBlock];
+  const P2dWs& ws = w3.b;
+  const int oi = blockIdx.x;
+  if (oi >= *ws.nobj) return;
+  const int m = ws.rm[oi];
+  for (int j = threadIdx.x; j < m; j += blockDim.x) {
+    const int32_t* pc = w3.pcnt + ((size_t)oi * kMaxHypBlock + j) * kCntZ;
+    int c = 0;
+    for (int z = 0; z < kCntZ; z++) c += pc[z];
+    const int h = ws.rl[oi * kMaxHypBlock + j];
+    hl[j] = h;
+    hc[j] = c;
     ws.rc[oi * kMaxHypBlock + j] = c;
     inl_out[h * kRounds + r] = c;
   }
+  __syncthreads();
+  if (m <= 1) return;  // block-uniform
+  keep_better_half(ws, oi, m, hl, hc, tmp);
 }
 
 // the subset position of the rank-th set bit of M (pref: exclusive popcount
@@ -1281,49 +1435,33 @@ __device__ __forceinline__ int select_bit(const uint64_t* __restrict__ M, const 
       rank -= pc;
     }
   }
-  uint64_t v = M[k];
-  for (int i = 0; i < rank; i++) v &= v - 1;
-  return 64 * k + __ffsll((unsigned long long)v) - 1;
+  uint64_t v = M[k];  // the rank-th set bit of v by halving
+  int pos = 0;
+#pragma unroll
+  for (int w = 32; w >= 1; w >>= 1) {
+    const uint64_t low = (1ull << w) - 1;
+    const int c = __popcll(v & low);
+    if (rank >= c) {
+      rank -= c;
+      v >>= w;
+      pos += w;
+    } else {
+      v &= low;
+    }
+  }
+  return 64 * k + pos;
 }
 
-// the rigid transform of the correspondences corr[0, m) (pixels): object
-// coordinate -> camera coordinate, fold64 sums; every lane gets the pose
-__device__ Pose wave_rigid(const float* __restrict__ vm, const float* __restrict__ ext, int C, int obj,
-                           const float* __restrict__ eye, const int* corr, int m) {
-  const int lane = pcnn::lane_id();
-  double sa[3] = {0.0, 0.0, 0.0}, sb[3] = {0.0, 0.0, 0.0};
-  for (int k = lane; k < m; k += 64) {
-    const F3 o = mode3d(vm, ext, C, obj, corr[k]);
-    const F3 e = eye_at(eye, corr[k]);
-    sa[0] = sa[0] + (double)o.x; sa[1] = sa[1] + (double)o.y; sa[2] = sa[2] + (double)o.z;
-    sb[0] = sb[0] + (double)e.x; sb[1] = sb[1] + (double)e.y; sb[2] = sb[2] + (double)e.z;
-  }
-  const double inv = 1.0 / (double)m;
-  double cA[3], cB[3];
-  for (int i = 0; i < 3; i++) {
-    cA[i] = fold64(sa[i]) * inv;
-    cB[i] = fold64(sb[i]) * inv;
-  }
-  double sc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-  for (int k = lane; k < m; k += 64) {
-    const F3 o = mode3d(vm, ext, C, obj, corr[k]);
-    const F3 e = eye_at(eye, corr[k]);
-    const double pa[3] = {(double)o.x - cA[0], (double)o.y - cA[1], (double)o.z - cA[2]};
-    const double pb[3] = {(double)e.x - cB[0], (double)e.y - cB[1], (double)e.z - cB[2]};
-    for (int rr = 0; rr < 3; rr++)
-      for (int cc = 0; cc < 3; cc++) sc[rr * 3 + cc] = sc[rr * 3 + cc] + pa[rr] * pb[cc];
-  }
-  double Hc[9];
-  for (int i = 0; i < 9; i++) Hc[i] = fold64(sc[i]);
-  return rigid_from_cov(Hc, cA, cB);
-}
-
-__global__ void __launch_bounds__(64) k_p3d_update(const float* __restrict__ vm, const float* __restrict__ ext, int C,
-                                                   uint64_t seed, P3dWs w3, int r) {
+// one workgroup per survivor: the popcount prefix and the picks spread over
+// 1024 threads (each pick on its own stream, one correspondence per thread),
+// the centroid and covariance sums in the workgroup tree, the SVD on thread 0
+__global__ void __launch_bounds__(1024) k_p3d_update(const float* __restrict__ vm, const float* __restrict__ ext,
+                                                     int C, uint64_t seed, P3dWs w3, int r) {
   __shared__ int pref[kPrefWords];
-  __shared__ int corr[kMaxInl];
+  __shared__ int wsum[16];
+  __shared__ double wc[16][6], wv[16][9];
   const P2dWs& ws = w3.b;
-  const int j = blockIdx.x, oi = blockIdx.y, lane = pcnn::lane_id();
+  const int j = blockIdx.x, oi = blockIdx.y, t = threadIdx.x, lane = pcnn::lane_id(), wave = t >> 6;
   if (oi >= *ws.nobj || j >= ws.rm[oi]) return;  // block-uniform
   const int n = ws.rc[oi * kMaxHypBlock + j];
   if (n < 4) return;  // :1350-1351
@@ -1334,10 +1472,10 @@ __global__ void __launch_bounds__(64) k_p3d_update(const float* __restrict__ vm,
   const int ns = ws.subcnt[obj * kRounds + r];
   const int nw = (ns + 63) / 64;
   const uint64_t* M = w3.imask + (size_t)h * w3.mwords;
-  if (nw <= kPrefWords) {
+  if (nw <= kPrefWords) {  // block-uniform
     int carry = 0;
-    for (int base = 0; base < nw; base += 64) {
-      const int k = base + lane;
+    for (int base = 0; base < nw; base += 1024) {
+      const int k = base + t;
       const int pc = k < nw ? __popcll(M[k]) : 0;
       int incl = pc;
 #pragma unroll
@@ -1345,167 +1483,249 @@ __global__ void __launch_bounds__(64) k_p3d_update(const float* __restrict__ vm,
         const int y = __shfl_up(incl, d, 64);
         if (lane >= d) incl += y;
       }
-      if (k < nw) pref[k] = carry + incl - pc;
-      carry += __shfl(incl, 63, 64);
+      if (lane == 63) wsum[wave] = incl;
+      __syncthreads();
+      int wb = 0, tot = 0;
+      for (int w = 0; w < 16; w++) {
+        if (w < wave) wb += wsum[w];
+        tot += wsum[w];
+      }
+      if (k < nw) pref[k] = carry + wb + incl - pc;
+      __syncthreads();
+      carry += tot;
     }
   }
-  __syncthreads();
   const int m = n >= kMaxInl ? kMaxInl : n;  // filterInliers3D (:1308-1322)
-  for (int k = lane; k < m; k += 64) {
-    int rank = k;
+  const bool live = t < m;
+  double a[3] = {0.0, 0.0, 0.0}, b[3] = {0.0, 0.0, 0.0};
+  if (live) {
+    int rank = t;
     if (n >= kMaxInl) {
-      Stream rs(seed, (uint32_t)h, kTagF3D, (uint32_t)(1024 * r + k));
+      Stream rs(seed, (uint32_t)h, kTagF3D, (uint32_t)(1024 * r + t));
       rank = rs.uniform(n);
     }
     const int p = L[S[select_bit(M, pref, nw, rank)]];
-    corr[k] = p;
-    w3.pick[(size_t)h * kMaxInl + k] = p;
+    const F3 o = mode3d(vm, ext, C, obj, p);
+    const F3 e = eye_at(w3.eye, p);
+    a[0] = o.x; a[1] = o.y; a[2] = o.z;
+    b[0] = e.x; b[1] = e.y; b[2] = e.z;
+    w3.pick[(size_t)h * kMaxInl + t] = p;
   }
-  if (lane == 0) w3.npick[h] = m;
+  if (t == 0) w3.npick[h] = m;
+  // Hypothesis::refine (:1359): calcRigidBodyTransform's sums in the tree
+  for (int i = 0; i < 3; i++) {
+    const double sa = wave_fold(live ? 0.0 + a[i] : 0.0), sb = wave_fold(live ? 0.0 + b[i] : 0.0);
+    if (lane == 0) {
+      wc[wave][i] = sa;
+      wc[wave][3 + i] = sb;
+    }
+  }
   __syncthreads();
-  const Pose P = wave_rigid(vm, ext, C, obj, w3.eye, corr, m);  // Hypothesis::refine (:1359)
-  if (lane != 0) return;
+  const double inv = 1.0 / (double)m;
+  double cA[3], cB[3];
+  for (int i = 0; i < 3; i++) {
+    cA[i] = cross_fold<double, 6>(wc, i) * inv;
+    cB[i] = cross_fold<double, 6>(wc, 3 + i) * inv;
+  }
+  for (int rr = 0; rr < 3; rr++)
+    for (int cc = 0; cc < 3; cc++) {
+      const double v = wave_fold(live ? 0.0 + (a[rr] - cA[rr]) * (b[cc] - cB[cc]) : 0.0);
+      if (lane == 0) wv[wave][rr * 3 + cc] = v;
+    }
+  __syncthreads();
+  if (t != 0) return;
+  double Hc[9];
+  for (int i = 0; i < 9; i++) Hc[i] = cross_fold<double, 9>(wv, i);
+  const Pose P = rigid_from_cov_ool(Hc, cA, cB);
   double* hr = ws.hyp + (size_t)h * 16;
   for (int i = 0; i < 9; i++) hr[1 + i] = P.R[i];
   for (int i = 0; i < 3; i++) hr[10 + i] = P.t[i];
 }
 
-__global__ void __launch_bounds__(64) k_p3d_finish(const float* __restrict__ vm, const float* __restrict__ ext, int C,
-                                                   int n_hyp, uint64_t seed, int nm_evals, P3dWs w3,
-                                                   int32_t* __restrict__ final_out, float* __restrict__ poses_out,
-                                                   float* __restrict__ energy_out) {
-  __shared__ float co[kMaxInl][3], ce[kMaxInl][3];
+// one workgroup per object: the final filter, then refineWithOpt as the
+// bounded Nelder-Mead of k_nm (icp.hip): thread 0 keeps the simplex in LDS,
+// each thread holds one correspondence, and every evaluation sums the
+// distances in the workgroup tree (the oracle's order)
+__global__ void __launch_bounds__(kFinThreads) k_p3d_finish(const float* __restrict__ vm,
+                                                            const float* __restrict__ ext, int C, int n_hyp,
+                                                            uint64_t seed, int nm_evals, P3dWs w3,
+                                                            int32_t* __restrict__ final_out,
+                                                            float* __restrict__ poses_out,
+                                                            float* __restrict__ energy_out) {
+  constexpr int nd = 6;
+  __shared__ float wf[16][1];
+  __shared__ double pts[nd + 1][nd], vals[nd + 1], lb[nd], ub[nd], xq[nd], xr[nd], cen[nd];
+  __shared__ float Rf[9];
+  __shared__ int nh_s;
   const P2dWs& ws = w3.b;
-  const int oi = blockIdx.x, lane = pcnn::lane_id();  // one wave per object
-  if (oi >= *ws.nobj || ws.rm[oi] == 0) return;
+  const int oi = blockIdx.x, t = threadIdx.x, lane = pcnn::lane_id(), wave = t >> 6;
+  if (oi >= *ws.nobj || ws.rm[oi] == 0) return;  // block-uniform
   const int obj = ws.objs[oi];
   const int h = ws.rl[oi * kMaxHypBlock];
   const int n = ws.rc[oi * kMaxHypBlock];
-  int nh = 0;
-  for (int q = lane; q < n_hyp; q += 64) nh += ws.hyp[(size_t)q * 16] == (double)obj;
-  nh = pcnn::wave_sum(nh);
-  if (lane == 0) {
-    final_out[obj * 3] = h;
-    final_out[obj * 3 + 1] = n;
-    final_out[obj * 3 + 2] = nh;
+  if (t == 0) nh_s = 0;
+  __syncthreads();
+  {
+    int nh = 0;
+    for (int q = t; q < n_hyp; q += kFinThreads) nh += ws.hyp[(size_t)q * 16] == (double)obj;
+    nh = pcnn::wave_sum(nh);
+    if (lane == 0) atomicAdd(&nh_s, nh);  // integer: order-free
   }
   const double* hr = ws.hyp + (size_t)h * 16;
   Pose P;
   for (int i = 0; i < 9; i++) P.R[i] = hr[1 + i];
   for (int i = 0; i < 3; i++) P.t[i] = hr[10 + i];
   float en = 0.f;
-  if (n > 10) {  // minPixels (:1939)
+  if (n > 10) {  // minPixels (:1939); block-uniform
     const int mp = w3.npick[h];
     const int m = mp >= kMaxInl ? kMaxInl : mp;
-    for (int k = lane; k < m; k += 64) {
-      int idx = k;
+    float co[3] = {0.f, 0.f, 0.f}, ce[3] = {0.f, 0.f, 0.f};
+    const bool live = t < m;
+    if (live) {  // filterInliers3D again (:1942): correspondence t of this thread
+      int idx = t;
       if (mp >= kMaxInl) {
-        Stream rs(seed, (uint32_t)h, kTagF3D, (uint32_t)(1024 * kRounds + k));
+        Stream rs(seed, (uint32_t)h, kTagF3D, (uint32_t)(1024 * kRounds + t));
         idx = rs.uniform(mp);
       }
       const int p = w3.pick[(size_t)h * kMaxInl + idx];
       const F3 o = mode3d(vm, ext, C, obj, p);
       const F3 e = eye_at(w3.eye, p);
-      co[k][0] = o.x; co[k][1] = o.y; co[k][2] = o.z;
-      ce[k][0] = e.x; ce[k][1] = e.y; ce[k][2] = e.z;
+      co[0] = o.x; co[1] = o.y; co[2] = o.z;
+      ce[0] = e.x; ce[1] = e.y; ce[2] = e.z;
     }
-    __syncthreads();
-    auto energy = [&](const double* x) -> double {  // optEnergy3D (:1464-1507)
-      double Rd[9];
-      rod_v2m(x, Rd);
-      float Rf[9];
-      for (int i = 0; i < 9; i++) Rf[i] = (float)Rd[i];
-      float pt = 0.f;
-      for (int k = lane; k < m; k += 64) {
+    auto eval = [&]() -> double {  // optEnergy3D (:1464-1507) at xq (written by thread 0)
+      if (t == 0) {
+        double Rd[9];
+        rod_v2m(xq, Rd);
+        for (int i = 0; i < 9; i++) Rf[i] = (float)Rd[i];  // jp::double2float
+      }
+      __syncthreads();
+      float leaf = 0.f;
+      if (live) {
         float tr[3];
         for (int rr = 0; rr < 3; rr++) {
-          const float mm = Rf[rr * 3 + 0] * co[k][0] + Rf[rr * 3 + 1] * co[k][1] + Rf[rr * 3 + 2] * co[k][2];
-          tr[rr] = (float)((double)mm + x[3 + rr]);
+          const float mm = Rf[rr * 3 + 0] * co[0] + Rf[rr * 3 + 1] * co[1] + Rf[rr * 3 + 2] * co[2];
+          tr[rr] = (float)((double)mm + xq[3 + rr]);
         }
-        const double dx = (double)tr[0] - (double)ce[k][0], dy = (double)tr[1] - (double)ce[k][1],
-                     dz = (double)tr[2] - (double)ce[k][2];
-        pt = (float)((double)pt + sqrt(dx * dx + dy * dy + dz * dz));
+        const double dx = (double)tr[0] - (double)ce[0], dy = (double)tr[1] - (double)ce[1],
+                     dz = (double)tr[2] - (double)ce[2];
+        leaf = 0.f + (float)sqrt(dx * dx + dy * dy + dz * dz);
       }
-      return (double)(fold64f(pt) / (float)m);
+      const float sw = wave_fold(leaf);
+      if (lane == 0) wf[wave][0] = sw;
+      __syncthreads();
+      // every thread folds the 16 wave sums (the next evaluation's first
+      // barrier orders these reads before wf is rewritten)
+      return (double)(cross_fold<float, 1>(wf, 0) / (float)m);
     };
-    // refineWithOpt (:1510-1567): every lane runs the same search
-    constexpr int nd = 6;
-    double x0[nd], lb[nd], ub[nd];
-    rod_m2v(P.R, x0);
-    for (int i = 0; i < 3; i++) x0[3 + i] = P.t[i];
-    const double rot = 10 * 3.1415926 / 180;  // rotRange, PI of types.h:33
-    const double rng[nd] = {rot, rot, rot, 0.1, 0.1, 0.5};
-    for (int i = 0; i < nd; i++) {
-      lb[i] = x0[i] - rng[i];
-      ub[i] = x0[i] + rng[i];
-    }
-    double pts[nd + 1][nd], vals[nd + 1];
-    for (int i = 0; i <= nd; i++)
-      for (int e = 0; e < nd; e++) pts[i][e] = x0[e];
-    for (int i = 0; i < nd; i++) {
-      const double st = fmin(0.25 * (ub[i] - lb[i]), fmin(0.75 * (ub[i] - x0[i]), 0.75 * (x0[i] - lb[i])));
-      for (int e = 0; e < nd; e++) pts[i + 1][e] = e == i ? x0[e] + st : x0[e] + 0.0;
-    }
-    for (int i = 0; i <= nd; i++) vals[i] = energy(pts[i]);
-    int nev = nd + 1;
-    auto clampe = [&](int e, double v) { return fmin(fmax(v, lb[e]), ub[e]); };
-    double c[nd], xr[nd], xe[nd], xc[nd];
-    while (nev < nm_evals) {
-      for (int i = 1; i <= nd; i++)
-        for (int jj = i; jj > 0 && vals[jj] < vals[jj - 1]; jj--) {
-          const double tv = vals[jj];
-          vals[jj] = vals[jj - 1];
-          vals[jj - 1] = tv;
-          for (int e = 0; e < nd; e++) {
-            const double tp = pts[jj][e];
-            pts[jj][e] = pts[jj - 1][e];
-            pts[jj - 1][e] = tp;
-          }
-        }
-      for (int e = 0; e < nd; e++) {
-        double sm = pts[0][e];
-        for (int i = 1; i < nd; i++) sm = sm + pts[i][e];
-        c[e] = sm / (double)nd;
+    auto clampq = [&](int e, double v) { return fmin(fmax(v, lb[e]), ub[e]); };
+    if (t == 0) {  // refineWithOpt (:1510-1567)
+      double x0[nd];
+      rod_m2v(P.R, x0);
+      for (int i = 0; i < 3; i++) x0[3 + i] = P.t[i];
+      const double rot = 10 * 3.1415926 / 180;  // rotRange, PI of types.h:33
+      const double rng[nd] = {rot, rot, rot, 0.1, 0.1, 0.5};
+      for (int i = 0; i < nd; i++) {
+        lb[i] = x0[i] - rng[i];
+        ub[i] = x0[i] + rng[i];
+        pts[0][i] = x0[i];
       }
-      for (int e = 0; e < nd; e++) xr[e] = clampe(e, c[e] + (c[e] - pts[nd][e]));
-      const double fr = energy(xr);
+      for (int i = 0; i < nd; i++) {
+        const double st = fmin(0.25 * (ub[i] - lb[i]), fmin(0.75 * (ub[i] - x0[i]), 0.75 * (x0[i] - lb[i])));
+        for (int e = 0; e < nd; e++) pts[i + 1][e] = e == i ? x0[e] + st : x0[e] + 0.0;
+      }
+    }
+    for (int i = 0; i <= nd; i++) {
+      if (t == 0)
+        for (int e = 0; e < nd; e++) xq[e] = pts[i][e];
+      const double v = eval();
+      if (t == 0) vals[i] = v;
+    }
+    int nev = nd + 1;
+    while (nev < nm_evals) {  // nev is identical in every thread
+      if (t == 0) {
+        for (int i = 1; i <= nd; i++)
+          for (int jj = i; jj > 0 && vals[jj] < vals[jj - 1]; jj--) {
+            const double tv = vals[jj];
+            vals[jj] = vals[jj - 1];
+            vals[jj - 1] = tv;
+            for (int e = 0; e < nd; e++) {
+              const double tp = pts[jj][e];
+              pts[jj][e] = pts[jj - 1][e];
+              pts[jj - 1][e] = tp;
+            }
+          }
+        for (int e = 0; e < nd; e++) {
+          double sm = pts[0][e];
+          for (int i = 1; i < nd; i++) sm = sm + pts[i][e];
+          cen[e] = sm / (double)nd;
+        }
+        for (int e = 0; e < nd; e++) {
+          xr[e] = clampq(e, cen[e] + (cen[e] - pts[nd][e]));
+          xq[e] = xr[e];
+        }
+      }
+      const double fr = eval();
       nev++;
-      if (fr < vals[0] && nev < nm_evals) {
-        for (int e = 0; e < nd; e++) xe[e] = clampe(e, c[e] + 2.0 * (c[e] - pts[nd][e]));
-        const double fe = energy(xe);
+      const double v0 = vals[0], vn1 = vals[nd - 1], vn = vals[nd];
+      if (fr < v0 && nev < nm_evals) {
+        if (t == 0)
+          for (int e = 0; e < nd; e++) xq[e] = clampq(e, cen[e] + 2.0 * (cen[e] - pts[nd][e]));
+        const double fe = eval();
         nev++;
-        const bool ex = fe < fr;
-        for (int e = 0; e < nd; e++) pts[nd][e] = ex ? xe[e] : xr[e];
-        vals[nd] = ex ? fe : fr;
-      } else if (fr < vals[nd - 1]) {
-        for (int e = 0; e < nd; e++) pts[nd][e] = xr[e];
-        vals[nd] = fr;
+        if (t == 0) {
+          const bool ex = fe < fr;
+          for (int e = 0; e < nd; e++) pts[nd][e] = ex ? xq[e] : xr[e];
+          vals[nd] = ex ? fe : fr;
+        }
+      } else if (fr < vn1) {
+        if (t == 0) {
+          for (int e = 0; e < nd; e++) pts[nd][e] = xr[e];
+          vals[nd] = fr;
+        }
       } else if (nev < nm_evals) {
-        for (int e = 0; e < nd; e++)
-          xc[e] = fr >= vals[nd] ? clampe(e, c[e] + 0.5 * (pts[nd][e] - c[e])) : clampe(e, c[e] + 0.5 * (xr[e] - c[e]));
-        const double fc = energy(xc);
+        if (t == 0)
+          for (int e = 0; e < nd; e++)
+            xq[e] = fr >= vn ? clampq(e, cen[e] + 0.5 * (pts[nd][e] - cen[e])) : clampq(e, cen[e] + 0.5 * (xr[e] - cen[e]));
+        const double fc = eval();
         nev++;
-        if (fc < fmin(fr, vals[nd])) {
-          for (int e = 0; e < nd; e++) pts[nd][e] = xc[e];
-          vals[nd] = fc;
+        if (fc < fmin(fr, vn)) {
+          if (t == 0) {
+            for (int e = 0; e < nd; e++) pts[nd][e] = xq[e];
+            vals[nd] = fc;
+          }
         } else {
           const int sm = min(nd, nm_evals - nev);
-          for (int i = 1; i <= sm; i++) {
-            for (int e = 0; e < nd; e++) pts[i][e] = clampe(e, pts[0][e] + 0.5 * (pts[i][e] - pts[0][e]));
-            vals[i] = energy(pts[i]);
+          for (int i = 1; i <= sm; i++) {  // shrink toward the best
+            if (t == 0)
+              for (int e = 0; e < nd; e++) xq[e] = clampq(e, pts[0][e] + 0.5 * (pts[i][e] - pts[0][e]));
+            const double fv = eval();
+            if (t == 0) {
+              for (int e = 0; e < nd; e++) pts[i][e] = xq[e];
+              vals[i] = fv;
+            }
           }
           nev += sm > 0 ? sm : 0;
         }
       }
+      __syncthreads();
     }
-    int bi = 0;
-    for (int i = 1; i <= nd; i++)
-      if (vals[i] < vals[bi]) bi = i;
-    rod_v2m(pts[bi], P.R);
-    for (int i = 0; i < 3; i++) P.t[i] = pts[bi][3 + i];
-    en = (float)vals[bi];
+    if (t == 0) {
+      int bi = 0;
+      for (int i = 1; i <= nd; i++)
+        if (vals[i] < vals[bi]) bi = i;
+      double xb[nd];
+      for (int e = 0; e < nd; e++) xb[e] = pts[bi][e];
+      rod_v2m(xb, P.R);
+      for (int i = 0; i < 3; i++) P.t[i] = xb[3 + i];
+      en = (float)vals[bi];
+    }
   }
-  if (lane != 0) return;
+  __syncthreads();
+  if (t != 0) return;
+  final_out[obj * 3] = h;
+  final_out[obj * 3 + 1] = n;
+  final_out[obj * 3 + 2] = nh_s;
   energy_out[obj] = en;
   for (int y = 0; y < 3; y++)
     for (int x = 0; x < 4; x++) poses_out[obj + C * (y * 4 + x)] = x < 3 ? (float)P.R[y * 3 + x] : (float)P.t[y];
@@ -1612,7 +1832,7 @@ namespace {
 
 struct Layout3 {
   Layout b;
-  size_t eye, valid, imask, pick, npick, total;
+  size_t eye, valid, imask, pick, npick, pcnt, total;
   int mwords;
 };
 
@@ -1633,6 +1853,7 @@ Layout3 layout3(int H, int W, int C, int n_hyp) {
   l.imask = take((size_t)n_hyp * l.mwords * sizeof(uint64_t));
   l.pick = take((size_t)n_hyp * kMaxInl * sizeof(int32_t));
   l.npick = take((size_t)n_hyp * sizeof(int32_t));
+  l.pcnt = take((size_t)C * kMaxHypBlock * kCntZ * sizeof(int32_t));
   l.total = off + 256;
   return l;
 }
@@ -1682,14 +1903,12 @@ extern "C" int pcnn_pose3d(const int32_t* label, const uint16_t* depth, const fl
   w3.imask = (uint64_t*)(base + l.imask);
   w3.pick = (int32_t*)(base + l.pick);
   w3.npick = (int32_t*)(base + l.npick);
+  w3.pcnt = (int32_t*)(base + l.pcnt);
   w3.mwords = l.mwords;
   const P2dWs& ws = w3.b;
   hipStream_t st = (hipStream_t)stream;
-  if (hipMemsetAsync(poses_out, 0, (size_t)12 * C * sizeof(float), st) != hipSuccess) return PCNN_EHIP;
-  if (hipMemsetAsync(energy_out, 0, (size_t)C * sizeof(float), st) != hipSuccess) return PCNN_EHIP;
-  if (hipMemsetAsync(inl_out, 0xFF, (size_t)n_hyp * kRounds * sizeof(int32_t), st) != hipSuccess) return PCNN_EHIP;
-  if (hipMemsetAsync(final_out, 0xFF, (size_t)C * 3 * sizeof(int32_t), st) != hipSuccess) return PCNN_EHIP;
-  if (hipMemsetAsync(ws.rm, 0, (size_t)C * sizeof(int32_t), st) != hipSuccess) return PCNN_EHIP;
+  hipLaunchKernelGGL(k_p3d_init, dim3(1), dim3(1024), 0, st, C, n_hyp, poses_out, energy_out, inl_out, final_out,
+                     ws.rm);
   const Cam k{fx, fy, px, py};
   const int HW = H * W;
   hipLaunchKernelGGL(k_p3d_eye, dim3((HW + 255) / 256), dim3(256), 0, st, depth, H, W, fx, fy, px, py, depth_factor,
@@ -1707,12 +1926,12 @@ extern "C" int pcnn_pose3d(const int32_t* label, const uint16_t* depth, const fl
   hipLaunchKernelGGL(k_p2d_collect, dim3(C), dim3(64), 0, st, n_hyp, ws);
   for (int r = 0; r < kRounds; r++) {
     const int gx = std::max(1, n_hyp >> r);  // survivors halve each round (one stays one)
-    hipLaunchKernelGGL(k_p3d_count, dim3(gx, C), dim3(256), 0, st, vertmap, extents, C, w3, r, inl_out);
-    hipLaunchKernelGGL(k_p2d_select, dim3(C), dim3(1024), 0, st, ws);
-    hipLaunchKernelGGL(k_p3d_update, dim3(std::max(1, n_hyp >> (r + 1)), C), dim3(64), 0, st, vertmap, extents, C,
+    hipLaunchKernelGGL(k_p3d_count, dim3(gx, C, kCntZ), dim3(256), 0, st, vertmap, extents, C, w3, r);
+    hipLaunchKernelGGL(k_p3d_select, dim3(C), dim3(1024), 0, st, w3, r, inl_out);
+    hipLaunchKernelGGL(k_p3d_update, dim3(std::max(1, n_hyp >> (r + 1)), C), dim3(1024), 0, st, vertmap, extents, C,
                        seed, w3, r);
   }
-  hipLaunchKernelGGL(k_p3d_finish, dim3(C), dim3(64), 0, st, vertmap, extents, C, n_hyp, seed, nm_evals, w3, final_out,
+  hipLaunchKernelGGL(k_p3d_finish, dim3(C), dim3(kFinThreads), 0, st, vertmap, extents, C, n_hyp, seed, nm_evals, w3, final_out,
                      poses_out, energy_out);
   if (eye_out &&
       hipMemcpyAsync(eye_out, w3.eye, (size_t)HW * 3 * sizeof(float), hipMemcpyDeviceToDevice, st) != hipSuccess)

@@ -3,7 +3,7 @@ box scene (tests/refine_scene.py): live vertices, df::icp for N problems
 (solveICP's 8 hypotheses) x iterations, one JSON line with per-kernel HIP-event
 times, the step kernel's bandwidth against HBM, and the oracle's CPU ICP
 (oracle/orc_icp.cpp, one thread) timed on the same problems beside it.
-    python scripts/icp_bench.py [--n 8] [--iters 8] [--reps 20] [--no-cpu]"""
+    python tests/perf_icp.py [--n 8] [--iters 8] [--reps 20] [--no-cpu]"""
 import argparse
 import json
 import os

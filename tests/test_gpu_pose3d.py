@@ -135,3 +135,60 @@ def test_pose3d_device_inputs_and_errors(hip):
     with pytest.raises(ValueError):
         pose3d.estimate_poses_3d(sc["label"], sc["depth"][:5], sc["vertmap"], sc["extents"], p2, sc["C"],
                                  *sc["camera"], sc["depth_factor"])
+
+
+def _mat2quat(R):
+    """(w, x, y, z) of a rotation matrix (the role of test.py's mat2quat)."""
+    m = np.asarray(R, np.float64)
+    tr = np.trace(m)
+    if tr > 0:
+        s = 2.0 * np.sqrt(tr + 1.0)
+        q = [0.25 * s, (m[2, 1] - m[1, 2]) / s, (m[0, 2] - m[2, 0]) / s, (m[1, 0] - m[0, 1]) / s]
+    else:
+        i = int(np.argmax(np.diag(m)))
+        j, k = (i + 1) % 3, (i + 2) % 3
+        s = 2.0 * np.sqrt(1.0 + m[i, i] - m[j, j] - m[k, k])
+        q = [0.0] * 4
+        q[0] = (m[k, j] - m[j, k]) / s
+        q[1 + i] = 0.25 * s
+        q[1 + j] = (m[j, i] + m[i, j]) / s
+        q[1 + k] = (m[k, i] + m[i, k]) / s
+    q = np.asarray(q)
+    return q / np.linalg.norm(q) * (1 if q[0] >= 0 else -1)
+
+
+def test_pose3d_then_refine_poses(hip):
+    """test.py:1383-1416 under VERTEX_REG_3D + POSE_REFINE: estimate_poses_3d,
+    the found classes turned into (rois, poses) rows, then refine_poses
+    (solve_icp, the box ray-caster as the renderer): every object found, the
+    refined translation within 5 mm of the truth on a noisy frame."""
+    from posecnn_amd.synthesize import icp as R
+    from refine_scene import render_box
+    sc = make_scene(seed=12, n_obj=3, hole_frac=0.05, depth_noise=0.001, coord_noise=0.005)
+    C = sc["C"]
+    poses_tmp = np.zeros((3, 4, C), np.float32)
+    pose3d.estimate_poses_3d(sc["label"], sc["depth"], sc["vertmap"], sc["extents"], poses_tmp, C, *sc["camera"],
+                             sc["depth_factor"])
+    found = [j for j in range(C) if poses_tmp[2, 3, j] > 0]
+    assert sorted(found) == sorted(sc["poses"])
+    rois = np.zeros((len(found), 6), np.float32)
+    poses = np.zeros((len(found), 7), np.float32)
+    for i, j in enumerate(found):
+        rois[i, 1] = j
+        poses[i, :4] = _mat2quat(poses_tmp[:3, :3, j])
+        poses[i, 4:] = poses_tmp[:, 3, j]
+
+    def render(obj, pose):
+        m = render_box(np.asarray(pose, np.float64), sc["extents"][obj] / 2.0, obj)
+        dev = torch.device("cuda")
+        return (torch.from_numpy(m["vertmap"]).to(dev), torch.from_numpy(m["pred_v"]).to(dev),
+                torch.from_numpy(m["pred_n"]).to(dev))
+
+    params = list(sc["camera"]) + [0.25, 6.0, sc["depth_factor"]]
+    dev = torch.device("cuda")
+    depth = torch.from_numpy(sc["depth"].astype(np.int32)).to(dev).to(torch.uint16)
+    pnew, picp = R.solve_icp(torch.from_numpy(sc["label"]).to(dev), depth, params, rois, poses, render,
+                             max_error=0.02, nm_evals=20)
+    for i, j in enumerate(found):
+        assert np.linalg.norm(picp[i, 4:] - sc["poses"][j]["t"]) < 5e-3
+        assert abs(np.linalg.norm(picp[i, :4]) - 1) < 1e-4
