@@ -91,7 +91,7 @@ res["icp_score_us"] = {"scene_object": round(score_scene_us, 1), "dense_640x480"
 # solve_icp end to end (live vertices, re-centring, Nelder-Mead on optEnergy,
 # 8 hypotheses x ICP, SegICP score) for a RoIs of one frame, the renderer a
 # GPU ray-caster standing in for the reference's OpenGL pass
-from refine_scene import render_box_torch  # noqa: E402
+from refine_scene import GraphBoxRenderer, render_box_torch  # noqa: E402
 params = list(CAMERA) + [0.25, 6.0, 10000.0]
 half = sc["half"]
 render = lambda o, p: render_box_torch(np.asarray(p, np.float64), half, o)  # noqa: E731
@@ -108,22 +108,25 @@ def wall(fn, reps=3):
     return (time.perf_counter() - t0) / reps * 1e3
 
 
-for nroi in (1, 4):
-    rois = np.tile(np.array([[0, sc["cls"], 0, 0, 1, 1]], np.float32), (nroi, 1))
-    poses = np.tile(sc["init"].astype(np.float32)[None], (nroi, 1))
-    for nm in (0, 50):
-        e2e[f"rois{nroi}_nm{nm}_ms"] = round(wall(lambda: R.solve_icp(lab, depth, params, rois, poses, render,
-                                                                       max_error=0.02, nm_evals=nm)), 2)
-        if nm:  # the host-driven searches (one energy launch + host read per lock-step round), for comparison
-            e2e[f"rois{nroi}_nm{nm}_host_search_ms"] = round(wall(lambda: R.solve_icp(
-                lab, depth, params, rois, poses, render, max_error=0.02, nm_evals=nm, nm_device=False)), 2)
-        # the caller's renders alone (1 initial + 1 for the search + 8 hypotheses per RoI): the reference's
-        # OpenGL pass, here a torch ray-caster, outside the path
-        n_render = nroi * (1 + (1 if nm else 0) + 8)
-        e2e[f"rois{nroi}_nm{nm}_renders_ms"] = round(wall(lambda: [render(sc["cls"], sc["init"]) for _ in
-                                                                    range(n_render)]), 2)
-        e2e[f"rois{nroi}_nm{nm}_minus_renders_ms"] = round(e2e[f"rois{nroi}_nm{nm}_ms"] -
-                                                           e2e[f"rois{nroi}_nm{nm}_renders_ms"], 2)
+renderers = {"eager": render, "graph": GraphBoxRenderer(lambda o: half)}
+for rname, rnd in renderers.items():
+    pre = "" if rname == "eager" else "graph_"
+    for nroi in (1, 4):
+        rois = np.tile(np.array([[0, sc["cls"], 0, 0, 1, 1]], np.float32), (nroi, 1))
+        poses = np.tile(sc["init"].astype(np.float32)[None], (nroi, 1))
+        for nm in (0, 50):
+            key = f"{pre}rois{nroi}_nm{nm}"
+            e2e[f"{key}_ms"] = round(wall(lambda: R.solve_icp(lab, depth, params, rois, poses, rnd,
+                                                              max_error=0.02, nm_evals=nm)), 2)
+            if nm and rname == "eager":  # the host-driven searches (one energy launch + host read per round)
+                e2e[f"{key}_host_search_ms"] = round(wall(lambda: R.solve_icp(
+                    lab, depth, params, rois, poses, rnd, max_error=0.02, nm_evals=nm, nm_device=False)), 2)
+            # the caller's renders alone (1 initial + 1 for the search + 8 hypotheses per RoI): the
+            # reference's OpenGL pass, here a torch ray-caster (eager, or replayed from a HIP graph)
+            n_render = nroi * (1 + (1 if nm else 0) + 8)
+            e2e[f"{key}_renders_ms"] = round(wall(lambda: [rnd(sc["cls"], sc["init"]) for _ in
+                                                            range(n_render)]), 2)
+            e2e[f"{key}_minus_renders_ms"] = round(e2e[f"{key}_ms"] - e2e[f"{key}_renders_ms"], 2)
 # the Nelder-Mead searches alone (pcnn_nelder_mead_energy: one workgroup per RoI, 50 evaluations)
 pv0 = render(sc["cls"], sc["init"])[1]
 for nroi in (1, 4):
@@ -137,7 +140,8 @@ res["solve_icp_end_to_end"] = {**e2e, "records_per_roi": int(cnt[0].item()),
                                "note": "wall time per solve_icp call (host orchestration, renders, all launches and "
                                        "host reads); rois share one frame; *_renders_ms = the caller's renders alone, "
                                        "*_minus_renders_ms the rest; *_host_search_ms the searches driven from the "
-                                       "host (nm_device=False)"}
+                                       "host (nm_device=False); graph_* with the ray-caster replayed from a captured "
+                                       "HIP graph (GraphBoxRenderer)"}
 if not a.no_cpu:
     from oracle import oracle
     ref_lv = oracle.icp_live_vertices(sc["live"]["depth"], sc["live"]["label"], sc["cls"], 10000.0, CAMERA)
