@@ -372,8 +372,8 @@ __global__ void k_label_hist_prob(const float* __restrict__ prob, int32_t* __res
                                   int H, HoughWs ws);
 __global__ void k_label_place(const int32_t* __restrict__ label, const float* __restrict__ vertex, int vch,
                               const float* __restrict__ extents, const float* __restrict__ meta, int num_meta, int H,
-                              int W, int C, int skip, int label_thr, int index_size, int nms, HoughWs ws);
-__global__ void k_voter_setup(int H, int W, int C, float inlier, double so, double si, HoughWs ws);
+                              int W, int C, int skip, int label_thr, int index_size, int nms, float inlier,
+                              double so, double si, HoughWs ws);
 template <int kBand, int kVoteThreads>
 __global__ void k_hough_vote(int H, int W, int C, float inlier, HoughWs ws, int32_t* __restrict__ counts_out);
 __global__ void k_hough_peak(int B, int H, int W, int C, float inlier, const float* __restrict__ extents,

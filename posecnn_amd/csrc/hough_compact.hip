@@ -38,10 +38,17 @@ __global__ void __launch_bounds__(kCompactThreads) k_label_hist(const int32_t* _
   __syncthreads();
   const int32_t* lab = label + (size_t)b * HW;
   const int base = blk * kPixPerBlk;
-  for (int r = 0; r < kPixPerBlk / kCompactThreads; r++) {
-    int p = base + r * kCompactThreads + threadIdx.x;
-    int l = p < HW ? lab[p] : -1;
-    bool valid = p < HW && l > 0 && l < C;
+  constexpr int kRounds = kPixPerBlk / kCompactThreads;
+  int lr[kRounds];  // every round's label load in flight at once
+#pragma unroll
+  for (int r = 0; r < kRounds; r++) {
+    const int p = base + r * kCompactThreads + threadIdx.x;
+    lr[r] = p < HW ? lab[p] : -1;
+  }
+#pragma unroll
+  for (int r = 0; r < kRounds; r++) {
+    const int l = lr[r];
+    const bool valid = l > 0 && l < C;
     for_each_label_group(l, valid, [&](int l0, uint64_t m) {
       if (pcnn::lane_id() == __ffsll((long long)m) - 1) atomicAdd(&h[l0], __popcll(m));
     });
@@ -144,18 +151,23 @@ __device__ __forceinline__ int voter_cone(float4 q, float inlier, double so, dou
 // vote, cu.cc:775-776) and the voter-list offsets in LDS -- block 0 publishes
 // them for the later kernels -- then the ranked scatter of the sampled voters
 // (list positions 0, skip, 2 skip, ...: cu.cc:269) with each voter's record
-// (u, v, d = exp(z), T(d)).  (The per-voter cone setup stays a dense pass of
-// its own: inline here, one lane in ten of a wave runs the double-precision
-// setup, 25.9 -> 35.2 us at B = 1.)
+// (u, v, d = exp(z), T(d)), its cone row-bound slopes and code, its (slot,
+// row) count and the slot's largest box radius.  The block's sampled voters
+// are queued in LDS first and set up in one dense pass (round 5: the setup
+// used to run per round on the one lane in ten that samples -- or as a
+// kernel of its own, k_voter_setup, 7.8 us at B = 1).
 __global__ void __launch_bounds__(kCompactThreads) k_label_place(
     const int32_t* __restrict__ label, const float* __restrict__ vertex, int vch, const float* __restrict__ extents,
     const float* __restrict__ meta, int num_meta, int H, int W, int C, int skip, int label_thr, int index_size,
-    int nms, HoughWs ws) {
+    int nms, float inlier, double so, double si, HoughWs ws) {
   __shared__ int run[kMaxClasses];
   __shared__ int tot[kMaxClasses];
   __shared__ int vbl[kMaxClasses], vcl[kMaxClasses], slot_of[kMaxClasses], scls[kMaxClasses];
   __shared__ int pe[kCompactThreads], pa[kCompactThreads];
-  __shared__ int wcnt[kCompactThreads / 64][kMaxClasses];
+  __shared__ int wc[(kPixPerBlk / 64) * kMaxClasses];  // (round, wave, class) group counts, then their prefix
+  __shared__ int qp[kPixPerBlk], ql[kPixPerBlk], qi[kPixPerBlk];  // sampled-voter queue
+  __shared__ int smax[kMaxClasses];  // the block's largest box radius per slot
+  __shared__ int s_nq;
   __shared__ int s_nvote, s_count;
   const int b = blockIdx.y, blk = blockIdx.x, nblk = ws.nblk;
   const int HW = H * W;
@@ -165,8 +177,20 @@ __global__ void __launch_bounds__(kCompactThreads) k_label_place(
   if (t < G * C) {
     const int c = t % C, g = t / C;
     int e = 0, a = 0;
-    for (int k = g; k < nblk; k += G) {
-      const int v = ws.blk[((size_t)b * nblk + k) * C + c];
+    const int* hb = ws.blk + (size_t)b * nblk * C + c;
+    int k = g;
+    for (; k + 7 * G < nblk; k += 8 * G) {  // eight loads in flight
+      int v[8];
+#pragma unroll
+      for (int u = 0; u < 8; u++) v[u] = hb[(size_t)(k + u * G) * C];
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        a += v[u];
+        e += k + u * G < blk ? v[u] : 0;
+      }
+    }
+    for (; k < nblk; k += G) {
+      const int v = hb[(size_t)k * C];
       a += v;
       e += k < blk ? v : 0;
     }
@@ -222,81 +246,105 @@ __global__ void __launch_bounds__(kCompactThreads) k_label_place(
     }
   if (blk == 0)
     for (int sl = t; sl < s_count; sl += blockDim.x) ws.slot_cls[(size_t)b * C + sl] = scls[sl];
-  // 3. ranked scatter + voter setup
+  // 3. ranked scatter + voter setup.  The block's labels are loaded up front
+  // (kRounds loads in flight per thread), the ranks of every round come from
+  // one LDS prefix over (round, wave) group counts, and the sampled voters'
+  // vertex gathers are issued together before any of them is used: the
+  // rounds no longer wait on each other's global loads.
+  constexpr int kRounds = kPixPerBlk / kCompactThreads;
+  constexpr int kWaves = kCompactThreads / 64;
   const int32_t* lab = label + (size_t)b * HW;
   const float* mb = meta + (size_t)b * num_meta;
   const int base = blk * kPixPerBlk;
-  for (int r = 0; r < kPixPerBlk / kCompactThreads; r++) {
-    for (int i = pcnn::lane_id(); i < C; i += 64) wcnt[wave][i] = 0;
-    const int p = base + r * kCompactThreads + t;
-    const int l = p < HW ? lab[p] : -1;
-    const bool valid = p < HW && l > 0 && l < C;
-    int rank_w = 0;
-    for_each_label_group(l, valid, [&](int l0, uint64_t m) {
-      if (l == l0 && valid) rank_w = __popcll(m & pcnn::lanemask_lt());
-      if (pcnn::lane_id() == __ffsll((long long)m) - 1) wcnt[wave][l0] = __popcll(m);
-    });
-    __syncthreads();
-    if (valid && vcl[l] > 0) {
-      int rank = run[l] + rank_w;
-      for (int w = 0; w < wave; w++) rank += wcnt[w][l];
-      if (rank % skip == 0) {  // list positions 0, skip, 2 skip, ... (cu.cc:269)
-        const size_t vi = (size_t)b * ws.vcap + vbl[l] + rank / skip;
-        const size_t off = ((size_t)b * HW + p) * (size_t)vch + (vch == 3 ? 0 : 3 * l);
-        const float u = vertex[off], v = vertex[off + 1];
-        const float d = (float)exp((double)vertex[off + 2]);  // cu.cc:280
-        const float T = project_box(l, extents, mb, d, 0.6f);  // cu.cc:285
-        ws.vdat[vi] = make_float4(u, v, d, T);
-        ws.vpos[vi] = p;
-      }
-    }
-    __syncthreads();
-    for (int i = t; i < C; i += blockDim.x) {
-      int sum = 0;
-      for (int w = 0; w < kCompactThreads / 64; w++) sum += wcnt[w][i];
-      run[i] += sum;
-    }
-    __syncthreads();
+  int lr[kRounds];
+#pragma unroll
+  for (int rr = 0; rr < kRounds; rr++) {
+    const int p = base + rr * kCompactThreads + t;
+    lr[rr] = p < HW ? lab[p] : -1;
   }
-}
-
-// One lane per sampled voter: the cone row-bound slopes and code, the
-// (slot, row) voter counts that let a vote band find its voter range, and
-// each slot's largest box radius: a band [y0, y1) visits only voters with rows
-// in [y0 - kmax, y1 - 1 + kmax].
-__global__ void __launch_bounds__(256) k_voter_setup(int H, int W, int C, float inlier, double so, double si,
-                                                      HoughWs ws) {
-  __shared__ int sbase[kMaxClasses + 1];  // slot s covers voters [sbase[s], sbase[s + 1])
-  const int b = blockIdx.y;
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  const int nvote = ws.nvote[b];
-  for (int sl = threadIdx.x; sl < nvote; sl += blockDim.x) {
-    const int cls = ws.slot_cls[(size_t)b * C + sl];
-    sbase[sl] = ws.vbase[(size_t)b * C + cls];
-    if (sl == nvote - 1) sbase[nvote] = ws.vbase[(size_t)b * C + cls] + ws.vcount[(size_t)b * C + cls];
+  for (int i = t; i < kRounds * kWaves * C; i += blockDim.x) wc[i] = 0;
+  for (int i = t; i < C; i += blockDim.x) smax[i] = -1;
+  if (t == 0) s_nq = 0;
+  __syncthreads();
+  int rank_w[kRounds];
+#pragma unroll
+  for (int rr = 0; rr < kRounds; rr++) {
+    const int l = lr[rr];
+    const bool valid = l > 0 && l < C;
+    rank_w[rr] = 0;
+    for_each_label_group(l, valid, [&](int l0, uint64_t m) {
+      if (l == l0 && valid) rank_w[rr] = __popcll(m & pcnn::lanemask_lt());
+      if (pcnn::lane_id() == __ffsll((long long)m) - 1) wc[(rr * kWaves + wave) * C + l0] = __popcll(m);
+    });
   }
   __syncthreads();
-  const bool in = nvote > 0 && i < sbase[nvote];
-  int k = -1, slot = 0, y = 0;
-  if (in) {
-    const size_t vi = (size_t)b * ws.vcap + i;
-    float4 cone;
-    int code;
-    k = voter_cone(ws.vdat[vi], inlier, so, si, cone, code);
-    ws.vcone[vi] = cone;
-    ws.vcode[vi] = code;
-    while (slot + 1 < nvote && i >= sbase[slot + 1]) slot++;
-    y = ws.vpos[vi] / W;
+  // wc -> exclusive prefix over (round, wave) per class, starting at run[c]
+  for (int c = t; c < C; c += blockDim.x) {
+    int acc = run[c];
+    for (int i = 0; i < kRounds * kWaves; i++) {
+      const int v = wc[i * C + c];
+      wc[i * C + c] = acc;
+      acc += v;
+    }
   }
+  __syncthreads();
+  // the sampled voters of the block into an LDS queue (any order: each has
+  // its own record slot), then one dense pass of gathers, exp and
+  // project_box -- the double exp and the box projection run once per
+  // voter, not once per round for every wave holding one
+#pragma unroll
+  for (int rr = 0; rr < kRounds; rr++) {
+    const int l = lr[rr];
+    if (l > 0 && l < C && vcl[l] > 0) {
+      const int rank = wc[(rr * kWaves + wave) * C + l] + rank_w[rr];
+      if (rank % skip == 0) {  // list positions 0, skip, 2 skip, ... (cu.cc:269)
+        const int q = atomicAdd(&s_nq, 1);
+        qp[q] = base + rr * kCompactThreads + t;
+        ql[q] = l;
+        qi[q] = vbl[l] + rank / skip;
+      }
+    }
+  }
+  __syncthreads();
+  const int nq = s_nq;
   int32_t* rowcnt = ws.rowcnt + (size_t)b * C * H;
-  for_each_label_group(slot * H + y, in, [&](int key, uint64_t m) {
-    if (pcnn::lane_id() == __ffsll((long long)m) - 1) atomicAdd(&rowcnt[key], __popcll(m));
-  });
-  for_each_label_group(slot, in && k >= 0, [&](int s0, uint64_t m) {
-    int kk = (in && k >= 0 && slot == s0) ? k : -1;
-    kk = pcnn::wave_max(kk);
-    if (pcnn::lane_id() == __ffsll((long long)m) - 1) atomicMax(ws.kmax + (size_t)b * C + s0, kk);
-  });
+  for (int q0 = 0; q0 < nq; q0 += blockDim.x) {  // block-uniform trip count
+    const int q = q0 + t;
+    const bool in = q < nq;
+    int k = -1, slot = 0, y = 0;
+    if (in) {
+      const int p = qp[q], l = ql[q];
+      const size_t off = ((size_t)b * HW + p) * (size_t)vch + (vch == 3 ? 0 : 3 * l);
+      const float u = vertex[off], v = vertex[off + 1];
+      const float d = (float)exp((double)vertex[off + 2]);  // cu.cc:280
+      const float T = project_box(l, extents, mb, d, 0.6f);  // cu.cc:285
+      const size_t vi = (size_t)b * ws.vcap + qi[q];
+      const float4 rec = make_float4(u, v, d, T);
+      ws.vdat[vi] = rec;
+      ws.vpos[vi] = p;
+      // the voter's cone row-bound slopes and code (formerly k_voter_setup)
+      float4 cone;
+      int code;
+      k = voter_cone(rec, inlier, so, si, cone, code);
+      ws.vcone[vi] = cone;
+      ws.vcode[vi] = code;
+      slot = slot_of[l];
+      y = p / W;
+    }
+    // (slot, row) voter counts and the slot's largest box radius, aggregated
+    // per wave (queued voters of one row and class sit together)
+    for_each_label_group(slot * H + y, in, [&](int key, uint64_t m) {
+      if (pcnn::lane_id() == __ffsll((long long)m) - 1) atomicAdd(&rowcnt[key], __popcll(m));
+    });
+    for_each_label_group(slot, in && k >= 0, [&](int s0, uint64_t m) {
+      int kk = (in && k >= 0 && slot == s0) ? k : -1;
+      kk = pcnn::wave_max(kk);
+      if (pcnn::lane_id() == __ffsll((long long)m) - 1) atomicMax(&smax[s0], kk);
+    });
+  }
+  __syncthreads();
+  for (int sl = t; sl < s_nvote; sl += blockDim.x)
+    if (smax[sl] >= 0) atomicMax(ws.kmax + (size_t)b * C + sl, smax[sl]);
 }
 
 }  // namespace pcnn_hough
