@@ -31,7 +31,7 @@
 //       lane each), then one lane per hypothesis keeps its first accepted
 //       attempt (one wave per hypothesis: 64 further attempts at a time, the
 //       first accepted in attempt order, if none of the 32 was);
-//   k_p2d_collect / k_p2d_count / k_p2d_select / k_p2d_finish: the 8 rounds
+//   k_p2d_collect / k_p2d_count / k_select_sum / k_p2d_finish: the 8 rounds
 //       as launches: per round one workgroup per (surviving hypothesis,
 //       object) counts inliers over the round's subset (double projections),
 //       then one workgroup per object keeps the better half by a stable rank
@@ -52,6 +52,11 @@ constexpr int kMaxHypBlock = 1024;
 constexpr int kMaxHyp = 256;     // ransacIterations (:1601)
 constexpr int kAttempts = 32;  // sampling attempts per hypothesis evaluated in one launch
 constexpr int kAttRec = 17;    // attempt record: obj (-1 rejected), R (9), t (3), pixels (4)
+constexpr int kCntChunk = 512;  // subset entries per count workgroup pass
+constexpr int kCntZ = 16;       // count workgroups per hypothesis at most (partial counts, summed by k_select_sum)
+// round r's count workgroups per hypothesis: the early rounds have many
+// hypotheses and short subsets, the late ones few hypotheses and long subsets
+inline int count_z(int r) { return std::min(kCntZ, 2 << r); }
 
 struct U4 { uint32_t x, y, z, w; };
 
@@ -169,8 +174,12 @@ __device__ int quartic_roots(const double* c, double* out) {
     w = cmul(w, sd);
   }
   // up to 200 sweeps, stopping at the first sweep whose steps are all below
-  // 1e-13 of their root (the oracle stops at the same sweep: identical IEEE
-  // double operations on both sides)
+  // 1e-9 of their root (the oracle stops at the same sweep: identical IEEE
+  // double operations on both sides); the Newton polish below finishes the
+  // real roots.  Round 5: 1e-13 was never reached by 2/3 of the quartics
+  // (clustered roots oscillate at 1e-13..1e-10), so most ran all 200 sweeps;
+  // at 1e-9, 97 % stop within 20 with the same real roots on the test scenes
+  // (oracle outputs identical)
   for (int it = 0; it < 200; it++) {
     double mstep = 0;
     for (int k = 0; k < 4; k++) {
@@ -186,7 +195,7 @@ __device__ int quartic_roots(const double* c, double* out) {
       z[k] = csub(z[k], st);
       mstep = fmax(mstep, (fabs(st.re) + fabs(st.im)) / (1 + fabs(z[k].re) + fabs(z[k].im)));
     }
-    if (mstep < 1e-13) break;
+    if (mstep < 1e-9) break;
   }
   int n = 0;
   for (int k = 0; k < 4; k++) {
@@ -332,6 +341,7 @@ struct P2dWs {
   int32_t* rl;       // (C, kMaxHypBlock) surviving hypotheses per object, in rank order
   int32_t* rc;       // (C, kMaxHypBlock) their inlier counts of the last round
   int32_t* rm;       // (C) survivors per object
+  int32_t* pcnt;     // (C, kMaxHypBlock, kCntZ) partial inlier counts of a round's count kernel
 };
 
 // one wave per column (4 per workgroup): 64 rows at a time, class counts by
@@ -932,7 +942,7 @@ __global__ void __launch_bounds__(64) k_pick(AttArgs A, int n_hyp, int max_iter,
 // The preemptive rounds of :1693-1727 as launches over (surviving
 // hypothesis, object): per round one workgroup counts one hypothesis's
 // inliers over the round's subset (k_p2d_count), then one workgroup per
-// object keeps the better half (k_p2d_select); survivor lists live in the
+// object keeps the better half (k_select_sum); survivor lists live in the
 // workspace.  k_p2d_collect seeds them (each object's hypotheses in
 // ascending h, the stored order -- see the oracle), k_p2d_finish writes the
 // output of :1729-1764.
@@ -951,10 +961,14 @@ __global__ void __launch_bounds__(64) k_p2d_collect(int n_hyp, P2dWs ws) {  // o
   if (lane == 0) ws.rm[oi] = m;
 }
 
+// grid (hypothesis slot, object, kCntZ): workgroup z counts the subset chunks
+// z, z + kCntZ, ... of kCntChunk entries (round 5: one workgroup per
+// hypothesis walked the whole subset, 26 us per round) and writes its partial
+// count; k_select_sum adds the partials (integers)
 __global__ void __launch_bounds__(256) k_p2d_count(const float* __restrict__ vm, const float* __restrict__ ext, int W,
-                                                   int C, Cam k, P2dWs ws, int r, int32_t* __restrict__ inl_out) {
+                                                   int C, Cam k, P2dWs ws, int r) {
   __shared__ int part[4];
-  const int j = blockIdx.x, oi = blockIdx.y;
+  const int j = blockIdx.x, oi = blockIdx.y, z = blockIdx.z;
   if (oi >= *ws.nobj || j >= ws.rm[oi]) return;  // block-uniform
   const int obj = ws.objs[oi];
   const int* L = ws.lists + ws.listoff[obj];
@@ -966,22 +980,20 @@ __global__ void __launch_bounds__(256) k_p2d_count(const float* __restrict__ vm,
   for (int i = 0; i < 9; i++) P.R[i] = hr[1 + i];
   for (int i = 0; i < 3; i++) P.t[i] = hr[10 + i];
   int cnt = 0;
-  for (int i = threadIdx.x; i < ns; i += 256) {  // countInliers2D (:1171-1214)
-    const int idx = L[S[i]];
-    const double u0 = idx % W, v0 = idx / W;
-    const F3 o = mode3d(vm, ext, C, obj, idx);
-    double u, v;
-    project(P, D3{o.x, o.y, o.z}, k, u, v);
-    if (sqrt((u0 - u) * (u0 - u) + (v0 - v) * (v0 - v)) < 10.0f) cnt++;
+  for (int c0 = z * kCntChunk; c0 < ns; c0 += (int)gridDim.z * kCntChunk) {  // countInliers2D (:1171-1214)
+    for (int i = c0 + threadIdx.x; i < c0 + kCntChunk && i < ns; i += 256) {
+      const int idx = L[S[i]];
+      const double u0 = idx % W, v0 = idx / W;
+      const F3 o = mode3d(vm, ext, C, obj, idx);
+      double u, v;
+      project(P, D3{o.x, o.y, o.z}, k, u, v);
+      if (sqrt((u0 - u) * (u0 - u) + (v0 - v) * (v0 - v)) < 10.0f) cnt++;
+    }
   }
   cnt = pcnn::wave_sum(cnt);
   if (pcnn::lane_id() == 0) part[threadIdx.x >> 6] = cnt;
   __syncthreads();
-  if (threadIdx.x == 0) {
-    const int c = part[0] + part[1] + part[2] + part[3];
-    ws.rc[oi * kMaxHypBlock + j] = c;
-    inl_out[h * kRounds + r] = c;
-  }
+  if (threadIdx.x == 0) ws.pcnt[((size_t)oi * kMaxHypBlock + j) * kCntZ + z] = part[0] + part[1] + part[2] + part[3];
 }
 
 // stable sort by inliers (descending, then list position), keep the better
@@ -1001,17 +1013,25 @@ __device__ void keep_better_half(const P2dWs& ws, int oi, int m, const int* hl, 
   if (threadIdx.x == 0) ws.rm[oi] = keep;
 }
 
-__global__ void __launch_bounds__(1024) k_p2d_select(P2dWs ws) {
+// the round's counts (partials summed: integers) into rc / inl_out, then the
+// stable halving (both estimators)
+__global__ void __launch_bounds__(1024) k_select_sum(P2dWs ws, int r, int Z, int32_t* __restrict__ inl_out) {
   __shared__ int hl[kMaxHypBlock], hc[kMaxHypBlock], tmp[kMaxHypBlock];
   const int oi = blockIdx.x;
   if (oi >= *ws.nobj) return;
   const int m = ws.rm[oi];
-  if (m <= 1) return;
   for (int j = threadIdx.x; j < m; j += blockDim.x) {
-    hl[j] = ws.rl[oi * kMaxHypBlock + j];
-    hc[j] = ws.rc[oi * kMaxHypBlock + j];
+    const int32_t* pc = ws.pcnt + ((size_t)oi * kMaxHypBlock + j) * kCntZ;
+    int c = 0;
+    for (int z = 0; z < Z; z++) c += pc[z];
+    const int h = ws.rl[oi * kMaxHypBlock + j];
+    hl[j] = h;
+    hc[j] = c;
+    ws.rc[oi * kMaxHypBlock + j] = c;
+    inl_out[h * kRounds + r] = c;
   }
   __syncthreads();
+  if (m <= 1) return;  // block-uniform
   keep_better_half(ws, oi, m, hl, hc, tmp);
 }
 
@@ -1051,7 +1071,8 @@ __global__ void __launch_bounds__(64) k_p2d_finish(int C, int n_hyp, P2dWs ws, i
 //   k_attempts<true> / k_pick<true>: the sampling loop (:1814-1889);
 //   k_p3d_count: countInliers3D over the round's subset (1 cm in double),
 //       inlier bits per hypothesis;
-//   k_p2d_select: the stable halving (as estimatePose2D);
+//   k_select_sum: the partial counts summed, the stable halving (as
+//       estimatePose2D);
 //   k_p3d_update: updateHyp3D (:1347-1364) for every survivor, one wave
 //       each: filterInliers3D (:1308-1322; pick k of round r on its own
 //       stream (draw, h, 'F3D', 1024 r + k)), the inlier ranks resolved to
@@ -1071,7 +1092,6 @@ struct P3dWs {
   uint64_t* imask;  // (n_hyp, mwords) inlier bits over the round's subset
   int32_t* pick;    // (n_hyp, kMaxInl) pixels of the last refit's correspondences
   int32_t* npick;   // (n_hyp)
-  int32_t* pcnt;    // (C, kMaxHypBlock, kCntZ) partial inlier counts of k_p3d_count
   int mwords;
 };
 
@@ -1079,8 +1099,6 @@ constexpr int kMaxInl = 1000;     // maxPixels: filterInliers3D's cap (:1796)
 constexpr int kLdsWords = 5120;   // class-list bits kept in LDS by k_p3d_subset (327,680 positions)
 constexpr int kSkipMax = 65536;   // class lists up to this long also get the per-position skip bytes
 constexpr int kPrefWords = 2048;  // subset words with an LDS popcount prefix in k_p3d_update
-constexpr int kCntChunk = 512;    // subset entries per k_p3d_count workgroup pass
-constexpr int kCntZ = 16;         // k_p3d_count workgroups per hypothesis
 constexpr int kFinThreads = 1024;  // k_p3d_finish workgroup (one correspondence per thread)
 
 // the outputs' initial values (one launch instead of five fills)
@@ -1372,7 +1390,7 @@ __global__ void __launch_bounds__(256) k_p3d_count(const float* __restrict__ vm,
   for (int i = 0; i < 3; i++) P.t[i] = hr[10 + i];
   uint64_t* M = w3.imask + (size_t)h * w3.mwords;
   int cnt = 0;
-  for (int c0 = z * kCntChunk; c0 < ns; c0 += kCntZ * kCntChunk) {  // countInliers3D (:1255-1287)
+  for (int c0 = z * kCntChunk; c0 < ns; c0 += (int)gridDim.z * kCntChunk) {  // countInliers3D (:1255-1287)
     for (int i0 = c0; i0 < c0 + kCntChunk && i0 < ns; i0 += 256) {
       const int i = i0 + threadIdx.x;
       bool in = false;
@@ -1390,30 +1408,7 @@ __global__ void __launch_bounds__(256) k_p3d_count(const float* __restrict__ vm,
   cnt = pcnn::wave_sum(cnt);
   if (lane == 0) part[wave] = cnt;
   __syncthreads();
-  if (threadIdx.x == 0) w3.pcnt[((size_t)oi * kMaxHypBlock + j) * kCntZ + z] = part[0] + part[1] + part[2] + part[3];
-}
-
-// the round's counts (partials summed: integers) into rc / inl_out, then the
-// stable halving of k_p2d_select
-__global__ void __launch_bounds__(1024) k_p3d_select(P3dWs w3, int r, int32_t* __restrict__ inl_out) {
-  __shared__ int hl[kMaxHypBlock], hc[kMaxHypBlock], tmp[kMaxHypBlock];
-  const P2dWs& ws = w3.b;
-  const int oi = blockIdx.x;
-  if (oi >= *ws.nobj) return;
-  const int m = ws.rm[oi];
-  for (int j = threadIdx.x; j < m; j += blockDim.x) {
-    const int32_t* pc = w3.pcnt + ((size_t)oi * kMaxHypBlock + j) * kCntZ;
-    int c = 0;
-    for (int z = 0; z < kCntZ; z++) c += pc[z];
-    const int h = ws.rl[oi * kMaxHypBlock + j];
-    hl[j] = h;
-    hc[j] = c;
-    ws.rc[oi * kMaxHypBlock + j] = c;
-    inl_out[h * kRounds + r] = c;
-  }
-  __syncthreads();
-  if (m <= 1) return;  // block-uniform
-  keep_better_half(ws, oi, m, hl, hc, tmp);
+  if (threadIdx.x == 0) ws.pcnt[((size_t)oi * kMaxHypBlock + j) * kCntZ + z] = part[0] + part[1] + part[2] + part[3];
 }
 
 // the subset position of the rank-th set bit of M (pref: exclusive popcount
@@ -1732,7 +1727,7 @@ __global__ void __launch_bounds__(kFinThreads) k_p3d_finish(const float* __restr
 }
 
 struct Layout {
-  size_t colcnt, coloff, count, lists, listoff, objs, nobj, subcnt, hyp, att, rl, rc, rm, sub, total;
+  size_t colcnt, coloff, count, lists, listoff, objs, nobj, subcnt, hyp, att, rl, rc, rm, pcnt, sub, total;
 };
 
 Layout layout(int H, int W, int C, int n_hyp) {
@@ -1758,6 +1753,7 @@ Layout layout(int H, int W, int C, int n_hyp) {
   l.rl = take((size_t)C * kMaxHypBlock * sizeof(int32_t));
   l.rc = take((size_t)C * kMaxHypBlock * sizeof(int32_t));
   l.rm = take((size_t)C * sizeof(int32_t));
+  l.pcnt = take((size_t)C * kMaxHypBlock * kCntZ * sizeof(int32_t));
   // subsets: a round visits at most every pixel of the class once
   l.sub = take((size_t)kRounds * H * W * sizeof(int32_t));
   l.total = off + 256;
@@ -1798,6 +1794,7 @@ extern "C" int pcnn_pose2d(const int32_t* label, const float* vertmap, const flo
   ws.rl = (int32_t*)(base + l.rl);
   ws.rc = (int32_t*)(base + l.rc);
   ws.rm = (int32_t*)(base + l.rm);
+  ws.pcnt = (int32_t*)(base + l.pcnt);
   ws.sub = (int32_t*)(base + l.sub);
   hipStream_t st = (hipStream_t)stream;
   if (hipMemsetAsync(poses_out, 0, (size_t)12 * C * sizeof(float), st) != hipSuccess) return PCNN_EHIP;
@@ -1820,8 +1817,8 @@ extern "C" int pcnn_pose2d(const int32_t* label, const float* vertmap, const flo
   hipLaunchKernelGGL(k_p2d_collect, dim3(C), dim3(64), 0, st, n_hyp, ws);
   for (int r = 0; r < kRounds; r++) {
     const int gx = std::max(1, n_hyp >> r);  // survivors halve each round (one stays one)
-    hipLaunchKernelGGL(k_p2d_count, dim3(gx, C), dim3(256), 0, st, vertmap, extents, W, C, k, ws, r, inl_out);
-    hipLaunchKernelGGL(k_p2d_select, dim3(C), dim3(1024), 0, st, ws);
+    hipLaunchKernelGGL(k_p2d_count, dim3(gx, C, count_z(r)), dim3(256), 0, st, vertmap, extents, W, C, k, ws, r);
+    hipLaunchKernelGGL(k_select_sum, dim3(C), dim3(1024), 0, st, ws, r, count_z(r), inl_out);
   }
   hipLaunchKernelGGL(k_p2d_finish, dim3(C), dim3(64), 0, st, C, n_hyp, ws, final_out, poses_out);
   PCNN_CHECK_LAUNCH();
@@ -1832,7 +1829,7 @@ namespace {
 
 struct Layout3 {
   Layout b;
-  size_t eye, valid, imask, pick, npick, pcnt, total;
+  size_t eye, valid, imask, pick, npick, total;
   int mwords;
 };
 
@@ -1853,7 +1850,6 @@ Layout3 layout3(int H, int W, int C, int n_hyp) {
   l.imask = take((size_t)n_hyp * l.mwords * sizeof(uint64_t));
   l.pick = take((size_t)n_hyp * kMaxInl * sizeof(int32_t));
   l.npick = take((size_t)n_hyp * sizeof(int32_t));
-  l.pcnt = take((size_t)C * kMaxHypBlock * kCntZ * sizeof(int32_t));
   l.total = off + 256;
   return l;
 }
@@ -1873,6 +1869,7 @@ P2dWs carve2(char* base, const Layout& l) {
   ws.rl = (int32_t*)(base + l.rl);
   ws.rc = (int32_t*)(base + l.rc);
   ws.rm = (int32_t*)(base + l.rm);
+  ws.pcnt = (int32_t*)(base + l.pcnt);
   ws.sub = (int32_t*)(base + l.sub);
   return ws;
 }
@@ -1903,7 +1900,6 @@ extern "C" int pcnn_pose3d(const int32_t* label, const uint16_t* depth, const fl
   w3.imask = (uint64_t*)(base + l.imask);
   w3.pick = (int32_t*)(base + l.pick);
   w3.npick = (int32_t*)(base + l.npick);
-  w3.pcnt = (int32_t*)(base + l.pcnt);
   w3.mwords = l.mwords;
   const P2dWs& ws = w3.b;
   hipStream_t st = (hipStream_t)stream;
@@ -1926,8 +1922,8 @@ extern "C" int pcnn_pose3d(const int32_t* label, const uint16_t* depth, const fl
   hipLaunchKernelGGL(k_p2d_collect, dim3(C), dim3(64), 0, st, n_hyp, ws);
   for (int r = 0; r < kRounds; r++) {
     const int gx = std::max(1, n_hyp >> r);  // survivors halve each round (one stays one)
-    hipLaunchKernelGGL(k_p3d_count, dim3(gx, C, kCntZ), dim3(256), 0, st, vertmap, extents, C, w3, r);
-    hipLaunchKernelGGL(k_p3d_select, dim3(C), dim3(1024), 0, st, w3, r, inl_out);
+    hipLaunchKernelGGL(k_p3d_count, dim3(gx, C, count_z(r)), dim3(256), 0, st, vertmap, extents, C, w3, r);
+    hipLaunchKernelGGL(k_select_sum, dim3(C), dim3(1024), 0, st, ws, r, count_z(r), inl_out);
     hipLaunchKernelGGL(k_p3d_update, dim3(std::max(1, n_hyp >> (r + 1)), C), dim3(1024), 0, st, vertmap, extents, C,
                        seed, w3, r);
   }

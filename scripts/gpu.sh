@@ -14,6 +14,7 @@
 #   microab NAME V1,... alternating scripts/NAME.py $MICRO_ARGS runs of the tree vs scratch/V.so (two rounds)
 #   sqmicro NAME ARGS V1,...  the two SQ counter passes over scripts/NAME.py ARGS, tree and each scratch/V.so
 #   bppmc               back-projection bench + FETCH / WRITE passes -> bp_bench_pmc.json (scripts/bp_pmc.py)
+#   pose                estimatePose2D / 3D and solve_icp benches (tests/perf_*.py) + rocprofv3 kernel stats
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 O=$R/gpurun_out
 mkdir -p $O
@@ -29,7 +30,7 @@ while [ $# -gt 0 ]; do
   case $task in
     test)
       args=(tests)
-      if [ $# -gt 0 ] && [[ $1 != test && $1 != smoke && $1 != bench && $1 != prof && $1 != pmc && $1 != sq && $1 != ab && $1 != micro && $1 != microab && $1 != sqmicro && $1 != bppmc ]]; then
+      if [ $# -gt 0 ] && [[ $1 != test && $1 != smoke && $1 != bench && $1 != prof && $1 != pmc && $1 != sq && $1 != ab && $1 != micro && $1 != microab && $1 != sqmicro && $1 != bppmc && $1 != pose ]]; then
         args=($1); shift
       fi
       timeout -k 10 900 python -u -m pytest "${args[@]}" -m gpu -x -v --timeout 120 --timeout-method thread \
@@ -99,6 +100,14 @@ while [ $# -gt 0 ]; do
         done
       done
       python scripts/bp_pmc.py $O $O/bp_bench.json > $O/bp_bench_pmc.json || exit 1 ;;
+    pose)
+      timeout -k 10 300 python tests/perf_pose.py --mode 2d > $O/pose2d_bench.json 2> $O/pose2d_bench.err || exit 1
+      timeout -k 10 300 python tests/perf_pose.py --mode 3d > $O/pose3d_bench.json 2> $O/pose3d_bench.err || exit 1
+      timeout -k 10 500 python tests/perf_icp.py > $O/icp_bench.json 2> $O/icp_bench.err || exit 1
+      for m in 2d 3d; do
+        (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_p$m -o run -- \
+           python3 $R/tests/perf_pose.py --mode $m --no-cpu --iters 5 > $O/prof_p$m.log 2>&1) || exit 1
+      done ;;
     micro)
       n=$1; shift
       timeout -k 10 300 python scripts/$n.py > $O/$n.log 2>&1 || exit 1 ;;

@@ -27,7 +27,7 @@ def gemm_roles(per, fam):
     for i, (_, val) in enumerate(seq):
         out[STEP_ORDER[i % len(STEP_ORDER)]].append(val)
     return out
-HOUGH = ("k_label_hist", "k_label_place", "k_voter_setup", "k_hough_vote", "k_hough_peak",
+HOUGH = ("k_label_hist", "k_label_place", "k_hough_vote", "k_hough_peak",
          "k_hough_emit", "k_hough_nms_cand", "k_hough_cand_data", "k_hough_nms_select")
 
 
