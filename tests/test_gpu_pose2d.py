@@ -95,3 +95,17 @@ def test_pose2d_hypothesis_limit(hip):
     with pytest.raises(ValueError):
         pose2d.estimate_poses_2d(sc["label"], sc["vertmap"], sc["extents"], np.zeros((3, 4, sc["C"]), np.float32),
                                  sc["C"], *sc["camera"], n_hyp=257)
+
+
+@pytest.mark.parametrize("H,W,C,n_hyp", [(240, 321, 16, 7), (480, 640, 22, 1), (240, 300, 4, 64)])
+def test_pose2d_shapes(hip, H, W, C, n_hyp):
+    """Odd and small frames, C = 16 / 4, one hypothesis: hypotheses, rounds,
+    survivors and poses against the oracle."""
+    sc = make_scene(seed=13, n_obj=min(3, C - 1), C=C, H=H, W=W, coord_noise=0.003)
+    poses, d = _run(sc, n_hyp=n_hyp)
+    r = oracle.pose2d(sc["label"], sc["vertmap"], sc["extents"], *sc["camera"], n_hyp=n_hyp)
+    np.testing.assert_array_equal(d["hyps"][:, 0], r["hyps"][:, 0])
+    np.testing.assert_array_equal(d["hyp_px"], r["hyp_px"])
+    np.testing.assert_array_equal(d["inliers"], r["inliers"])
+    np.testing.assert_array_equal(d["final"], r["final"])
+    np.testing.assert_allclose(poses, r["poses"], atol=1e-5)

@@ -192,3 +192,14 @@ def test_pose3d_then_refine_poses(hip):
     for i, j in enumerate(found):
         assert np.linalg.norm(picp[i, 4:] - sc["poses"][j]["t"]) < 5e-3
         assert abs(np.linalg.norm(picp[i, :4]) - 1) < 1e-4
+
+
+@pytest.mark.parametrize("H,W,C,n_hyp,factor", [(240, 321, 16, 7, 1000.0), (480, 640, 22, 1, 10000.0),
+                                                 (240, 300, 4, 64, 5000.0)])
+def test_pose3d_shapes(hip, H, W, C, n_hyp, factor):
+    """Odd and small frames, LINEMOD's C = 16 with its depth factor 1000,
+    one hypothesis, and a 4-class frame: every output against the oracle."""
+    sc = make_scene(seed=13, n_obj=min(3, C - 1), C=C, H=H, W=W, hole_frac=0.05, depth_noise=0.001,
+                    coord_noise=0.003, depth_factor=factor)
+    poses, d = _run(sc, n_hyp=n_hyp)
+    _check(sc, poses, d, _oracle(sc, n_hyp=n_hyp))
