@@ -14,6 +14,7 @@ pose_energy(live, label, obj, pred_vertices, poses, ...)   -> (K,)
 Poses are (qw, qx, qy, qz, tx, ty, tz) float32 rows; camera = (fx, fy, px, py).
 The rendered maps (the reference's OpenGL pass) are inputs.
 """
+import numpy as np
 import torch
 
 from .. import _lib
@@ -342,6 +343,17 @@ def nelder_mead_batch(fbatch, starts, lb, ub, max_eval):
     return res
 
 
+def _render_many(render, objs, poses):
+    """(vertmap, pred_vertices, pred_normals) stacked over K (object, pose)
+    pairs: one call of render.render_many(objs, poses) when the renderer
+    offers a batched pass, else K calls of render(obj, pose)."""
+    many = getattr(render, "render_many", None)
+    if many is not None:
+        return many(list(objs), np.stack([np.asarray(p, np.float32) for p in poses]))
+    maps = [render(o, p) for o, p in zip(objs, poses)]
+    return tuple(torch.stack([m[i] for m in maps]) for i in range(3))
+
+
 def solve_icp(labelmap, depth, parameters, rois, poses, render, max_error=0.01, nm_evals=50, icp_iterations=8,
               min_pixels=400, nm_device=True, stream=None):
     """Synthesizer::solveICP (synthesize.cpp:2052-2395) on the GPU ops above,
@@ -352,7 +364,9 @@ def solve_icp(labelmap, depth, parameters, rois, poses, render, max_error=0.01, 
     znear, zfar, factor) (icp_python's meta, synthesize.cpp:2031-2049), rois
     (R, >= 2) with the class at column 1, poses (R,7).  render(obj_id, pose7)
     -> (vertmap (H,W,3), pred_vertices (H,W,4), pred_normals (H,W,4)) device
-    tensors stands in for the reference's OpenGL pass.  Returns (poses_new,
+    tensors stands in for the reference's OpenGL pass (a renderer with a
+    render_many(objs, poses (K,7)) method is called once per stage with every
+    pose of the stage instead: three calls per solve).  Returns (poses_new,
     poses_icp) (R,7) as the reference fills `outputs` / `outputs_icp`: rows of
     skipped RoIs stay zero.  The steps, each one launch for all RoIs: live
     vertices of every RoI's object; the >= min_pixels test (one host read);
@@ -393,17 +407,16 @@ def solve_icp(labelmap, depth, parameters, rois, poses, render, max_error=0.01, 
     for i in rows:
         p = poses_h[i].astype(np.float64)
         T.append(np.concatenate([p[:4] / np.linalg.norm(p[:4]), p[4:7]]).astype(np.float32))
-    maps = [render(o, Ti) for o, Ti in zip(objs, T)]
-    vm = torch.stack([m[0] for m in maps])
-    out, Tc = icp_center(live, lab, objt, vm, torch.stack([m[1] for m in maps]), torch.stack([m[2] for m in maps]),
-                         max_error, pose_in=torch.from_numpy(np.stack(T)).to(dev), stream=stream)
+    vm, pv_c, pn_c = _render_many(render, objs, T)
+    out, Tc = icp_center(live, lab, objt, vm, pv_c, pn_c, max_error, pose_in=torch.from_numpy(np.stack(T)).to(dev),
+                         stream=stream)
     c_h, Tc_h = out[:, 3].cpu().numpy(), Tc.cpu().numpy()
     for k in range(n):
         if c_h[k] > 0:
             T[k] = Tc_h[k]
     nm = [k for k in range(n) if c_h[k] > 0] if nm_evals > 0 else []
     if nm:  # refinePose(..., 0): optEnergy over a correction of each re-rendered pose (:2221-2250)
-        pv0 = torch.stack([render(objs[k], T[k])[1] for k in nm])
+        pv0 = _render_many(render, [objs[k] for k in nm], [T[k] for k in nm])[1]
         x0 = np.array([1, 0, 0, 0, 0, 0, 0], np.float64)
         r = np.array([0.1, 0.1, 0.1, 0.1, 0.01, 0.01, 0.1])  # poseWithOpt's bounds (:2535-2558)
         rec, cnt = energy_records(live, lab, [objs[k] for k in nm], nm, pv0, (znear, zfar), stream)
@@ -429,9 +442,7 @@ def solve_icp(labelmap, depth, parameters, rois, poses, render, max_error=0.01, 
     # eight depth hypotheses per RoI (:2255-2280), all refined by one ICP launch
     hyps = np.repeat(np.stack(T)[:, None], len(dz), 1)                    # (n, 8, 7)
     hyps[:, 1:, 6] = np.stack(T)[:, 6:7] + np.array(dz[1:])[None]
-    hmaps = [render(objs[k], hyps[k, h]) for k in range(n) for h in range(len(dz))]
-    pvs = torch.stack([m[1] for m in hmaps])
-    pns = torch.stack([m[2] for m in hmaps])
+    _, pvs, pns = _render_many(render, [objs[k] for k in range(n) for _ in dz], list(hyps.reshape(-1, 7)))
     li = torch.arange(n, dtype=torch.int32, device=dev).repeat_interleave(len(dz))
     _, refined = icp(live, pvs, pns, cam, (znear, zfar), max_error, icp_iterations, live_index=li,
                      pose_in=torch.from_numpy(hyps.reshape(-1, 7)).to(dev), stream=stream)

@@ -122,10 +122,16 @@ for rname, rnd in renderers.items():
                 e2e[f"{key}_host_search_ms"] = round(wall(lambda: R.solve_icp(
                     lab, depth, params, rois, poses, rnd, max_error=0.02, nm_evals=nm, nm_device=False)), 2)
             # the caller's renders alone (1 initial + 1 for the search + 8 hypotheses per RoI): the
-            # reference's OpenGL pass, here a torch ray-caster (eager, or replayed from a HIP graph)
-            n_render = nroi * (1 + (1 if nm else 0) + 8)
-            e2e[f"{key}_renders_ms"] = round(wall(lambda: [rnd(sc["cls"], sc["init"]) for _ in
-                                                            range(n_render)]), 2)
+            # reference's OpenGL pass, here a torch ray-caster (eager per pose, or replayed from a HIP
+            # graph once per stage through render_many)
+            if rname == "eager":
+                n_render = nroi * (1 + (1 if nm else 0) + 8)
+                e2e[f"{key}_renders_ms"] = round(wall(lambda: [rnd(sc["cls"], sc["init"]) for _ in
+                                                                range(n_render)]), 2)
+            else:
+                stages = [nroi] + ([nroi] if nm else []) + [8 * nroi]
+                e2e[f"{key}_renders_ms"] = round(wall(lambda: [rnd.render_many([sc["cls"]] * k, [sc["init"]] * k)
+                                                                for k in stages]), 2)
             e2e[f"{key}_minus_renders_ms"] = round(e2e[f"{key}_ms"] - e2e[f"{key}_renders_ms"], 2)
 # the Nelder-Mead searches alone (pcnn_nelder_mead_energy: one workgroup per RoI, 50 evaluations)
 pv0 = render(sc["cls"], sc["init"])[1]
@@ -140,8 +146,8 @@ res["solve_icp_end_to_end"] = {**e2e, "records_per_roi": int(cnt[0].item()),
                                "note": "wall time per solve_icp call (host orchestration, renders, all launches and "
                                        "host reads); rois share one frame; *_renders_ms = the caller's renders alone, "
                                        "*_minus_renders_ms the rest; *_host_search_ms the searches driven from the "
-                                       "host (nm_device=False); graph_* with the ray-caster replayed from a captured "
-                                       "HIP graph (GraphBoxRenderer)"}
+                                       "host (nm_device=False); graph_* with the ray-caster replayed from captured "
+                                       "HIP graphs, one batched render per stage (GraphBoxRenderer.render_many)"}
 if not a.no_cpu:
     from oracle import oracle
     ref_lv = oracle.icp_live_vertices(sc["live"]["depth"], sc["live"]["label"], sc["cls"], 10000.0, CAMERA)

@@ -92,58 +92,82 @@ def render_box_torch(pose, half, cls, H=480, W=640, camera=CAMERA, device="cuda"
     """render_box on the GPU (torch), returning the (vertmap, pred_vertices,
     pred_normals) device maps solve_icp's renderer hands back."""
     import torch
-    rt = torch.tensor(np.concatenate([quat_to_R(pose[:4]).reshape(-1), np.asarray(pose[4:7], np.float64)]),
-                      dtype=torch.float64, device=device)
-    h = torch.tensor(np.asarray(half, np.float64), device=device)
-    return _render_box_rt(rt, h, cls, H, W, camera, device)
+    rt = torch.tensor(_rt_of(pose)[None], dtype=torch.float64, device=device)
+    h = torch.tensor(np.asarray(half, np.float64)[None], device=device)
+    c = torch.tensor([float(cls)], dtype=torch.float64, device=device)
+    return tuple(m[0] for m in _render_boxes(rt, h, c, H, W, camera, device))
+
+
+def _rt_of(pose):
+    p = np.asarray(pose, np.float64)
+    return np.concatenate([quat_to_R(p[:4]).reshape(-1), p[4:7]])
 
 
 class GraphBoxRenderer:
-    """render_box_torch replayed from a captured HIP graph per (class, box):
-    the pose enters through a static device tensor [R | t], so a call is one
-    small H2D copy, one graph launch and clones of the three maps (solve_icp
-    keeps several renders alive at once).  The test harness's stand-in for the
-    reference's OpenGL pass, without the ~30 eager launches per render."""
+    """The torch box ray-caster replayed from captured HIP graphs: the poses,
+    boxes and classes enter through static device tensors, so a call is one
+    small H2D copy, one graph launch and clones of the maps (solve_icp keeps
+    several renders alive at once).  __call__ renders one pose; render_many
+    renders K (object, pose) pairs in one pass (one graph per K), which
+    solve_icp uses once per stage.  The test harness's stand-in for the
+    reference's OpenGL pass."""
 
     def __init__(self, half_of, H=480, W=640, camera=CAMERA, device="cuda"):
-        import torch
         self.half_of, self.H, self.W, self.camera, self.device = half_of, H, W, camera, device
-        self.rt = torch.zeros(12, dtype=torch.float64, device=device)
         self.graphs = {}
 
-    def __call__(self, obj, pose):
+    def _graph(self, K):
         import torch
-        rt = np.concatenate([quat_to_R(np.asarray(pose, np.float64)[:4]).reshape(-1),
-                             np.asarray(pose, np.float64)[4:7]])
-        self.rt.copy_(torch.from_numpy(rt))
-        if obj not in self.graphs:
-            h = torch.tensor(np.asarray(self.half_of(obj), np.float64), device=self.device)
+        if K not in self.graphs:
+            rt = torch.zeros((K, 12), dtype=torch.float64, device=self.device)
+            rt[:, 0] = rt[:, 4] = rt[:, 8] = 1.0
+            rt[:, 11] = 1.0
+            h = torch.full((K, 3), 0.05, dtype=torch.float64, device=self.device)
+            c = torch.ones(K, dtype=torch.float64, device=self.device)
             s = torch.cuda.Stream()
             s.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(s):  # warm-up outside the capture
-                _render_box_rt(self.rt, h, obj, self.H, self.W, self.camera, self.device)
+                _render_boxes(rt, h, c, self.H, self.W, self.camera, self.device)
             torch.cuda.current_stream().wait_stream(s)
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
-                out = _render_box_rt(self.rt, h, obj, self.H, self.W, self.camera, self.device)
-            self.graphs[obj] = (g, out, h)
-        g, out, _ = self.graphs[obj]
+                out = _render_boxes(rt, h, c, self.H, self.W, self.camera, self.device)
+            self.graphs[K] = (g, out, rt, h, c)
+        return self.graphs[K]
+
+    def render_many(self, objs, poses):
+        import torch
+        K = len(objs)
+        g, out, rt, h, c = self._graph(K)
+        rt.copy_(torch.from_numpy(np.stack([_rt_of(p) for p in poses])))
+        h.copy_(torch.from_numpy(np.stack([np.asarray(self.half_of(o), np.float64) for o in objs])))
+        c.copy_(torch.tensor([float(o) for o in objs], dtype=torch.float64))
         g.replay()
         return tuple(o.clone() for o in out)
 
+    def __call__(self, obj, pose):
+        return tuple(m[0] for m in self.render_many([obj], [pose]))
 
-def _render_box_rt(rt, h, cls, H, W, camera, device):
+
+def _render_boxes(rt, h, cls, H, W, camera, device):
+    """K boxes at once: rt (K, 12) [R | t], h (K, 3) half extents, cls (K)
+    -> vertmap (K,H,W,3), pred_vertices (K,H,W,4), pred_normals (K,H,W,4);
+    elementwise arithmetic only, so a pose renders the same in any batch."""
     import torch
     fx, fy, px, py = camera
-    R = rt[:9].reshape(3, 3)
-    tt = rt[9:12]
+    K = rt.shape[0]
+    R = rt[:, :9].reshape(K, 3, 3)
+    tt = rt[:, 9:12]
     ys, xs = torch.meshgrid(torch.arange(H, dtype=torch.float64, device=device),
                             torch.arange(W, dtype=torch.float64, device=device), indexing="ij")
-    d = torch.stack([(xs - px) / fx, (ys - py) / fy, torch.ones_like(xs)], -1)
-    o = R.T @ (-tt)
-    dd = d @ R
-    t1 = (-h - o) / dd
-    t2 = (h - o) / dd
+    d = torch.stack([(xs - px) / fx, (ys - py) / fy, torch.ones_like(xs)], -1)[None]      # (1,H,W,3)
+    o = -(R[:, 0, :] * tt[:, 0:1] + R[:, 1, :] * tt[:, 1:2] + R[:, 2, :] * tt[:, 2:3])  # R^T (-t), (K,3)
+    Rb = R[:, None, None]                                                                 # (K,1,1,3,3)
+    dd = d[..., 0:1] * Rb[..., 0, :] + d[..., 1:2] * Rb[..., 1, :] + d[..., 2:3] * Rb[..., 2, :]  # d @ R
+    hb = h[:, None, None, :]
+    ob = o[:, None, None, :]
+    t1 = (-hb - ob) / dd
+    t2 = (hb - ob) / dd
     tn = torch.minimum(t1, t2)
     tf = torch.maximum(t1, t2)
     tmin = tn.max(-1).values
@@ -151,15 +175,15 @@ def _render_box_rt(rt, h, cls, H, W, camera, device):
     hit = (tmax >= tmin) & (tmin > 0)
     axis = tn.argmax(-1)
     sgn = -torch.sign(torch.gather(dd, -1, axis[..., None])[..., 0])
-    nobj = torch.zeros_like(d).scatter_(-1, axis[..., None], sgn[..., None])
+    nobj = torch.zeros_like(dd).scatter_(-1, axis[..., None], sgn[..., None])
     P = d * tmin[..., None]
-    N = nobj @ R.T
-    canon = o + dd * tmin[..., None]
-    pv = torch.zeros((H, W, 4), dtype=torch.float32, device=device)
-    pn = torch.zeros((H, W, 4), dtype=torch.float32, device=device)
+    N = nobj[..., 0:1] * Rb[..., :, 0] + nobj[..., 1:2] * Rb[..., :, 1] + nobj[..., 2:3] * Rb[..., :, 2]  # nobj @ R^T
+    canon = ob + dd * tmin[..., None]
+    pv = torch.zeros((K, H, W, 4), dtype=torch.float32, device=device)
+    pn = torch.zeros((K, H, W, 4), dtype=torch.float32, device=device)
     pv[..., :3] = torch.where(hit[..., None], P, torch.zeros_like(P)).float()
     pv[..., 3] = hit.float()
     pn[..., :3] = torch.where(hit[..., None], N, torch.zeros_like(N)).float()
     vm = torch.where(hit[..., None], canon, torch.full_like(canon, float("nan"))).float()
-    vm[..., 0] = torch.where(hit, vm[..., 0] + cls, vm[..., 0])
+    vm[..., 0] = torch.where(hit, vm[..., 0] + cls[:, None, None].float(), vm[..., 0])
     return vm, pv, pn

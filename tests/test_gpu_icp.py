@@ -312,3 +312,31 @@ def test_solve_icp_device_search_matches_host_driver(hip):
     np.testing.assert_array_equal(a[0], b[0])
     np.testing.assert_array_equal(a[1], b[1])
     assert np.linalg.norm(a[1][0, 4:] - sc["true"][4:]) < 5e-3
+
+
+def test_solve_icp_batched_renderer_matches(hip):
+    """A renderer with render_many is called once per stage (three calls per
+    solve) instead of once per pose; the maps are the same, so poses_new and
+    poses_icp are identical to the per-pose calls (2 RoIs, Nelder-Mead on)."""
+    from posecnn_amd.synthesize import icp as R
+    from refine_scene import GraphBoxRenderer
+    sc = scene(5, perturb_deg=2.0, perturb_t=0.01)
+    rnd = GraphBoxRenderer(lambda o: sc["half"])
+    calls = {"many": 0}
+
+    class Counting:
+        def render_many(self, objs, poses):
+            calls["many"] += 1
+            return rnd.render_many(objs, poses)
+
+    params = list(CAMERA) + [0.25, 6.0, 10000.0]
+    rois = np.array([[0, sc["cls"], 0, 0, 1, 1], [0, sc["cls"], 0, 0, 1, 1]], np.float32)
+    poses = np.stack([sc["init"], sc["init"]]).astype(np.float32)
+    depth = t(sc["live"]["depth"].astype(np.int32)).to(torch.uint16)
+    lab = t(sc["live"]["label"])
+    a = R.solve_icp(lab, depth, params, rois, poses, lambda o, p: rnd(o, p), max_error=0.02, nm_evals=20)
+    b = R.solve_icp(lab, depth, params, rois, poses, Counting(), max_error=0.02, nm_evals=20)
+    assert calls["many"] == 3
+    np.testing.assert_array_equal(a[0], b[0])
+    np.testing.assert_array_equal(a[1], b[1])
+    assert np.linalg.norm(b[1][0, 4:] - sc["true"][4:]) < 5e-3
