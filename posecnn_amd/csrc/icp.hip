@@ -1224,8 +1224,7 @@ __device__ float energy_rec(const float* __restrict__ r, int n, const float (&P)
   const float qn = sqrtf(P[0] * P[0] + P[1] * P[1] + P[2] * P[2] + P[3] * P[3]);
   const Quat q = {P[0] / qn, P[1] / qn, P[2] / qn, P[3] / qn};
   float s = 0.f, c = 0.f;
-  for (int i = threadIdx.x; i < n; i += kNmThreads) {
-    const float* x = r + (size_t)i * 6;
+  auto term = [&](const float* x) {
     float p0, p1, p2;
     rotate(q, x[0], x[1], x[2], p0, p1, p2);
     p0 = p0 + P[4];
@@ -1236,7 +1235,21 @@ __device__ float energy_rec(const float* __restrict__ r, int n, const float (&P)
       s += sqrtf(dx * dx + dy * dy + dz * dz);
       c += 1.f;
     }
+  };
+  int i = threadIdx.x;
+  // four records per pass, their 24 loads issued together (the loop was
+  // bound by one record's load latency at a time); the sum keeps the
+  // thread's record order, so the value is unchanged
+  for (; i + 3 * kNmThreads < n; i += 4 * kNmThreads) {
+    float v[4][6];
+#pragma unroll
+    for (int u = 0; u < 4; u++)
+#pragma unroll
+      for (int e = 0; e < 6; e++) v[u][e] = r[(size_t)(i + u * kNmThreads) * 6 + e];
+#pragma unroll
+    for (int u = 0; u < 4; u++) term(v[u]);
   }
+  for (; i < n; i += kNmThreads) term(r + (size_t)i * 6);
   s = pcnn::wave_sum(s);
   c = pcnn::wave_sum(c);
   const int wave = threadIdx.x >> 6;
