@@ -203,3 +203,20 @@ def test_pose3d_shapes(hip, H, W, C, n_hyp, factor):
                     coord_noise=0.003, depth_factor=factor)
     poses, d = _run(sc, n_hyp=n_hyp)
     _check(sc, poses, d, _oracle(sc, n_hyp=n_hyp))
+
+
+@pytest.mark.parametrize("H,W,e,seed", [(480, 640, 0.30, 21), (720, 960, 0.55, 22)])
+def test_pose3d_long_class_lists(hip, H, W, e, seed):
+    """One object filling most of the frame with 10 % holes: its class list
+    (243 k / 449 k positions) is past the skip bytes' 64 k (the bit walk from
+    LDS) and, in the second frame, past the 327 k positions of the LDS bit
+    copy (the walk reads the bits from HBM)."""
+    C = 4
+    ext = np.zeros((C, 3), np.float32)
+    ext[1:] = e
+    sc = make_scene(seed=seed, n_obj=1, C=C, H=H, W=W, extents=ext, hole_frac=0.1, depth_noise=0.001,
+                    coord_noise=0.003)
+    c = list(sc["poses"])[0]
+    assert (sc["label"] == c).sum() > (65536 if H == 480 else 327680)
+    poses, d = _run(sc, n_hyp=32)
+    _check(sc, poses, d, _oracle(sc, n_hyp=32))
