@@ -370,6 +370,15 @@ __device__ __forceinline__ int wave_argmax_rows(const float* __restrict__ img, i
 __global__ void k_label_hist(const int32_t* __restrict__ label, int HW, int C, int H, HoughWs ws);
 __global__ void k_label_hist_prob(const float* __restrict__ prob, int32_t* __restrict__ label_out, int HW, int C,
                                   int H, HoughWs ws);
+// k_label_place's sampled voters per block: a class's pixels in a block hold
+// consecutive list ranks, so it samples at most cnt / skip + 1 of them
+__host__ __device__ inline int place_queue_cap(int C, int skip) {
+  const int q = kPixPerBlk / skip + C + 1;
+  return q < kPixPerBlk ? q : kPixPerBlk;
+}
+__host__ __device__ inline size_t place_lds_bytes(int C, int skip) {
+  return ((size_t)(kPixPerBlk / 64) * C + 3 * (size_t)place_queue_cap(C, skip)) * sizeof(int);
+}
 __global__ void k_label_place(const int32_t* __restrict__ label, const float* __restrict__ vertex, int vch,
                               const float* __restrict__ extents, const float* __restrict__ meta, int num_meta, int H,
                               int W, int C, int skip, int label_thr, int index_size, int nms, float inlier,

@@ -164,8 +164,15 @@ __global__ void __launch_bounds__(kCompactThreads) k_label_place(
   __shared__ int tot[kMaxClasses];
   __shared__ int vbl[kMaxClasses], vcl[kMaxClasses], slot_of[kMaxClasses], scls[kMaxClasses];
   __shared__ int pe[kCompactThreads], pa[kCompactThreads];
-  __shared__ int wc[(kPixPerBlk / 64) * kMaxClasses];  // (round, wave, class) group counts, then their prefix
-  __shared__ int qp[kPixPerBlk], ql[kPixPerBlk], qi[kPixPerBlk];  // sampled-voter queue
+  // dynamic LDS (sized by place_lds_bytes): the (round, wave, class) group
+  // counts, then their prefix; the sampled-voter queue (position, class,
+  // record slot) of at most place_queue_cap entries
+  extern __shared__ int dyn_lds[];
+  int* wc = dyn_lds;
+  const int qcap = place_queue_cap(C, skip);
+  int* qp = wc + (kPixPerBlk / 64) * C;
+  int* ql = qp + qcap;
+  int* qi = ql + qcap;
   __shared__ int smax[kMaxClasses];  // the block's largest box radius per slot
   __shared__ int s_nq;
   __shared__ int s_nvote, s_count;

@@ -112,7 +112,8 @@ static int hough_voting_impl(const int32_t* label, const float* prob, int32_t* l
   {
     const double c = (double)inlier_thr, co = c - kConeEps, ci = c + kConeEps;
     const double so = std::sqrt(std::max(0.0, 1.0 - co * co)), si = std::sqrt(std::max(0.0, 1.0 - ci * ci));
-    hipLaunchKernelGGL(k_label_place, dim3(ws.nblk, B), dim3(kCompactThreads), 0, st, label, vertex, vch, extents,
+    hipLaunchKernelGGL(k_label_place, dim3(ws.nblk, B), dim3(kCompactThreads), place_lds_bytes(C, skip_pixels), st,
+                       label, vertex, vch, extents,
                        meta, num_meta, H, W, C, skip_pixels, label_thr, index_size, nms ? 1 : 0, inlier_thr, so, si,
                        ws);
   }
