@@ -502,6 +502,17 @@ int pcnn_nelder_mead_energy(const float* records, const int32_t* counts, int str
                             const double* lb, const double* ub, int max_eval, float znear, float zfar, double* x_out,
                             double* f_out, int32_t* nev_out, void* stream);
 
+/* pcnn_nelder_mead_energy with 8 cooperating workgroups per problem (the
+ * evaluation's records spread over 8 CUs, one arrive-and-wait per evaluation
+ * through the workspace), launched cooperatively; the same bits.  N <= 128;
+ * the workspace holds the wave sums and one counter per problem (zeroed by the
+ * call).  nev_out = -1 marks a cross-workgroup wait that gave up. */
+size_t pcnn_nelder_mead_energy_workspace_size(int N);
+int pcnn_nelder_mead_energy_coop(const float* records, const int32_t* counts, int stride, int N, const double* x0,
+                                 const double* lb, const double* ub, int max_eval, float znear, float zfar,
+                                 double* x_out, double* f_out, int32_t* nev_out, void* workspace,
+                                 size_t workspace_bytes, void* stream);
+
 /* pcnn_icp_score: the SegICP hypothesis score of solveICP (synthesize.cpp:2288-2330):
  *   over the object's pixels with depth > 0 and a finite vertmap, each model
  *   point (vertmap, class offset dropped) moved by hypothesis j takes its

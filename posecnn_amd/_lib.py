@@ -124,6 +124,10 @@ _SIGS = {
                                 c_void_p]),
     "pcnn_nelder_mead_energy": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int,
                                         c_float, c_float, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "pcnn_nelder_mead_energy_workspace_size": (c_size_t, [c_int]),
+    "pcnn_nelder_mead_energy_coop": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int,
+                                             c_float, c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t,
+                                             c_void_p]),
     "pcnn_pose_energy_batch": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_float,
                                        c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t,
                                        c_void_p]),

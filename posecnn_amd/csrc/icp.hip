@@ -1219,11 +1219,13 @@ __global__ void __launch_bounds__(kBlk) k_rec_scatter(const float* __restrict__ 
 // optEnergy (:2476-2526) of pose P (float, quaternion normalised as
 // k_pose_energy does) over n records; every thread of a 1024-thread
 // workgroup calls it and gets the value
-__device__ float energy_rec(const float* __restrict__ r, int n, const float (&P)[7], float znear, float zfar,
-                            float* sh) {
-  const float qn = sqrtf(P[0] * P[0] + P[1] * P[1] + P[2] * P[2] + P[3] * P[3]);
-  const Quat q = {P[0] / qn, P[1] / qn, P[2] / qn, P[3] / qn};
-  float s = 0.f, c = 0.f;
+// the record sums of virtual thread vt (of kNmThreads): records vt, vt +
+// kNmThreads, ... in order, four records' loads issued per pass (the loop
+// was bound by one record's load latency at a time; the order is unchanged)
+__device__ __forceinline__ void rec_sums(const float* __restrict__ r, int n, const Quat& q, const float (&P)[7],
+                                         float znear, float zfar, int vt, float& s, float& c) {
+  s = 0.f;
+  c = 0.f;
   auto term = [&](const float* x) {
     float p0, p1, p2;
     rotate(q, x[0], x[1], x[2], p0, p1, p2);
@@ -1236,10 +1238,7 @@ __device__ float energy_rec(const float* __restrict__ r, int n, const float (&P)
       c += 1.f;
     }
   };
-  int i = threadIdx.x;
-  // four records per pass, their 24 loads issued together (the loop was
-  // bound by one record's load latency at a time); the sum keeps the
-  // thread's record order, so the value is unchanged
+  int i = vt;
   for (; i + 3 * kNmThreads < n; i += 4 * kNmThreads) {
     float v[4][6];
 #pragma unroll
@@ -1250,6 +1249,21 @@ __device__ float energy_rec(const float* __restrict__ r, int n, const float (&P)
     for (int u = 0; u < 4; u++) term(v[u]);
   }
   for (; i < n; i += kNmThreads) term(r + (size_t)i * 6);
+}
+
+__device__ __forceinline__ Quat rec_quat(const float (&P)[7]) {
+  const float qn = sqrtf(P[0] * P[0] + P[1] * P[1] + P[2] * P[2] + P[3] * P[3]);
+  return {P[0] / qn, P[1] / qn, P[2] / qn, P[3] / qn};
+}
+
+// optEnergy (:2476-2526) of pose P (float, quaternion normalised as
+// k_pose_energy does) over n records; every thread of a 1024-thread
+// workgroup calls it and gets the value
+__device__ float energy_rec(const float* __restrict__ r, int n, const float (&P)[7], float znear, float zfar,
+                            float* sh) {
+  const Quat q = rec_quat(P);
+  float s, c;
+  rec_sums(r, n, q, P, znear, zfar, threadIdx.x, s, c);
   s = pcnn::wave_sum(s);
   c = pcnn::wave_sum(c);
   const int wave = threadIdx.x >> 6;
@@ -1288,24 +1302,80 @@ __global__ void __launch_bounds__(kNmThreads) k_energy_rec(const float* __restri
 // inside), shrink toward the best; trial points clamped to the bounds; at
 // most max_eval evaluations.  One workgroup per problem: thread 0 keeps the
 // simplex in LDS, every thread evaluates.
-__global__ void __launch_bounds__(kNmThreads) k_nm(const float* __restrict__ rec, const int32_t* __restrict__ count,
-                                                   int stride, const double* __restrict__ x0_all,
-                                                   const double* __restrict__ lb_all,
-                                                   const double* __restrict__ ub_all, int max_eval, float znear,
-                                                   float zfar, double* __restrict__ x_out, double* __restrict__ f_out,
-                                                   int32_t* __restrict__ nev_out) {
+// Arrive-and-wait of the G workgroups of one problem on its counter (thread 0
+// of each): release the workgroup's partial sums, wait until every workgroup
+// of the problem has arrived for this evaluation.  Bounded: a wait that never
+// completes (not expected: the launch is cooperative) gives up and reports.
+__device__ __forceinline__ bool coop_arrive_wait(uint32_t* bar, uint32_t target) {
+  __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  uint32_t cur = __hip_atomic_load(bar, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+  for (int it = 0; cur < target && it < (1 << 24); it++) {
+    __builtin_amdgcn_s_sleep(2);
+    cur = __hip_atomic_load(bar, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  return cur >= target;
+}
+
+// G workgroups per problem (G = 1: one 1024-thread workgroup; G > 1: the
+// 1024 "virtual threads" of optEnergy's reduction split over G workgroups of
+// kNmThreads / G, each running the same search).  Every evaluation's record
+// sums are those of energy_rec -- virtual thread v sums records v, v + 1024,
+// ... in order, each 64 of them fold by the same butterfly, the 16 wave sums
+// add in order -- so the value is identical for every G; with G > 1 the wave
+// sums cross workgroups through `part` (double-buffered by evaluation
+// parity) and one arrive-and-wait per evaluation on the problem's counter.
+template <int G>
+__global__ void __launch_bounds__(kNmThreads / G) k_nm(const float* __restrict__ rec,
+                                                       const int32_t* __restrict__ count, int stride,
+                                                       const double* __restrict__ x0_all,
+                                                       const double* __restrict__ lb_all,
+                                                       const double* __restrict__ ub_all, int max_eval, float znear,
+                                                       float zfar, double* __restrict__ x_out,
+                                                       double* __restrict__ f_out, int32_t* __restrict__ nev_out,
+                                                       float* __restrict__ part, uint32_t* __restrict__ bar) {
   constexpr int n = kNmDim;
+  constexpr int kT = kNmThreads / G;
   __shared__ double pts[n + 1][n], vals[n + 1], lb[n], ub[n], xq[n], xr[n], cen[n];
   __shared__ double fres;
   __shared__ float sh[2 * kNmThreads / 64];
-  const int p = blockIdx.x, t = threadIdx.x;
+  __shared__ int s_fail;
+  const int p = blockIdx.x / G, g = blockIdx.x % G, t = threadIdx.x;
   const float* r = rec + (size_t)p * stride * 6;
   const int nr = count[p];
+  int ne = 0;  // evaluations so far (the same in every thread of every workgroup of the problem)
+  if (t == 0) s_fail = 0;
   auto eval = [&]() -> double {  // every thread; the point is xq (LDS)
     __syncthreads();
     float P[7];
     for (int e = 0; e < n; e++) P[e] = (float)xq[e];  // the host path evaluates float32 points
-    const float v = energy_rec(r, nr, P, znear, zfar, sh);
+    float v;
+    if constexpr (G == 1) {
+      v = energy_rec(r, nr, P, znear, zfar, sh);
+    } else {
+      const int vt = g * kT + t;
+      const Quat q = rec_quat(P);
+      float s_, c_;
+      rec_sums(r, nr, q, P, znear, zfar, vt, s_, c_);
+      s_ = pcnn::wave_sum(s_);
+      c_ = pcnn::wave_sum(c_);
+      float* pp = part + ((size_t)p * 2 + (ne & 1)) * (2 * kNmThreads / 64);
+      if (pcnn::lane_id() == 0) {
+        pp[2 * (vt >> 6)] = s_;
+        pp[2 * (vt >> 6) + 1] = c_;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      __syncthreads();
+      if (t == 0 && !coop_arrive_wait(bar + p, (uint32_t)(ne + 1) * G)) s_fail = 1;
+      __syncthreads();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      float S = 0.f, Cn = 0.f;
+      for (int w = 0; w < kNmThreads / 64; w++) {
+        S += pp[2 * w];
+        Cn += pp[2 * w + 1];
+      }
+      v = Cn > 0.f ? S / Cn : 0.f;  // distance /= c (:2520-2521)
+    }
+    ne++;
     return (double)v;
   };
   auto clampq = [&](int e, double v) { return fmin(fmax(v, lb[e]), ub[e]); };  // np.minimum(np.maximum(p, lb), ub)
@@ -1398,13 +1468,13 @@ __global__ void __launch_bounds__(kNmThreads) k_nm(const float* __restrict__ rec
     }
     __syncthreads();
   }
-  if (t == 0) {
+  if (t == 0 && g == 0) {
     int b = 0;
     for (int i = 1; i <= n; i++)
       if (vals[i] < vals[b]) b = i;  // np.argmin: the first minimum
     for (int e = 0; e < n; e++) x_out[(size_t)p * n + e] = pts[b][e];
     f_out[p] = vals[b];
-    nev_out[p] = nev;
+    nev_out[p] = s_fail ? -1 : nev;  // -1: a cross-workgroup wait gave up (results invalid)
   }
   (void)fres;
 }
@@ -1450,8 +1520,44 @@ extern "C" int pcnn_nelder_mead_energy(const float* records, const int32_t* coun
                                        void* stream) {
   PCNN_REQUIRE(records && counts && x0 && lb && ub && x_out && f_out && nev_out && N > 0 && stride > 0);
   PCNN_REQUIRE(max_eval >= 0 && max_eval <= (1 << 20));
-  hipLaunchKernelGGL(k_nm, dim3(N), dim3(kNmThreads), 0, (hipStream_t)stream, records, counts, stride, x0, lb, ub,
-                     max_eval, znear, zfar, x_out, f_out, nev_out);
+  hipLaunchKernelGGL(k_nm<1>, dim3(N), dim3(kNmThreads), 0, (hipStream_t)stream, records, counts, stride, x0, lb,
+                     ub, max_eval, znear, zfar, x_out, f_out, nev_out, nullptr, nullptr);
+  PCNN_CHECK_LAUNCH();
+  return PCNN_OK;
+}
+
+// The same searches with kNmCoop workgroups per problem (the evaluation's
+// records spread over kNmCoop CUs), launched cooperatively so that the
+// workgroups of a problem are resident together; bit-identical results.
+constexpr int kNmCoop = 8;
+
+extern "C" size_t pcnn_nelder_mead_energy_workspace_size(int N) {
+  if (N <= 0) return 256;
+  return pcnn::align_up((size_t)N * 2 * (2 * kNmThreads / 64) * sizeof(float), 256) + (size_t)N * sizeof(uint32_t) +
+         256;
+}
+
+extern "C" int pcnn_nelder_mead_energy_coop(const float* records, const int32_t* counts, int stride, int N,
+                                            const double* x0, const double* lb, const double* ub, int max_eval,
+                                            float znear, float zfar, double* x_out, double* f_out, int32_t* nev_out,
+                                            void* workspace, size_t workspace_bytes, void* stream) {
+  PCNN_REQUIRE(records && counts && x0 && lb && ub && x_out && f_out && nev_out && N > 0 && stride > 0);
+  PCNN_REQUIRE(max_eval >= 0 && max_eval <= (1 << 20) && N <= 128);
+  if (!workspace || workspace_bytes < pcnn_nelder_mead_energy_workspace_size(N)) return PCNN_ECAPACITY;
+  float* part = (float*)workspace;
+  uint32_t* bar =
+      (uint32_t*)((char*)workspace + pcnn::align_up((size_t)N * 2 * (2 * kNmThreads / 64) * sizeof(float), 256));
+  hipStream_t st = (hipStream_t)stream;
+  if (hipMemsetAsync(bar, 0, (size_t)N * sizeof(uint32_t), st) != hipSuccess) return PCNN_EHIP;
+  void* args[] = {(void*)&records, (void*)&counts, (void*)&stride, (void*)&x0, (void*)&lb, (void*)&ub,
+                  (void*)&max_eval, (void*)&znear, (void*)&zfar, (void*)&x_out, (void*)&f_out, (void*)&nev_out,
+                  (void*)&part, (void*)&bar};
+  if (hipLaunchCooperativeKernel((const void*)k_nm<kNmCoop>, dim3(N * kNmCoop), dim3(kNmThreads / kNmCoop), args, 0,
+                                 st) != hipSuccess) {
+    (void)hipGetLastError();  // cooperative launch unavailable: the one-workgroup search (same bits)
+    hipLaunchKernelGGL(k_nm<1>, dim3(N), dim3(kNmThreads), 0, st, records, counts, stride, x0, lb, ub, max_eval,
+                       znear, zfar, x_out, f_out, nev_out, nullptr, nullptr);
+  }
   PCNN_CHECK_LAUNCH();
   return PCNN_OK;
 }

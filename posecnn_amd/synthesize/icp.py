@@ -200,8 +200,8 @@ def pose_energy_records(records, counts, poses, pose_prob, depth_range=(0.25, 6.
 
 def nelder_mead_device(records, counts, x0, lb, ub, max_eval, depth_range=(0.25, 6.0), stream=None):
     """The bounded Nelder-Mead of nelder_mead_steps on optEnergy, for N
-    problems at once on the device (one workgroup each, no host read until
-    the end): x0 / lb / ub (N,7) float64.  Returns (x (N,7), f (N,), nev (N,))
+    problems at once on the device (eight cooperating workgroups each, no
+    host read until the end): x0 / lb / ub (N,7) float64.  Returns (x (N,7), f (N,), nev (N,))
     as device tensors; the same bits as nelder_mead over pose_energy_records."""
     _lib.require_gpu(records, counts)
     dev = records.device
@@ -213,10 +213,18 @@ def nelder_mead_device(records, counts, x0, lb, ub, max_eval, depth_range=(0.25,
     x = torch.empty((N, 7), **d64)
     f = torch.empty((N,), **d64)
     nev = torch.empty((N,), dtype=torch.int32, device=dev)
-    rc = _lib.load().pcnn_nelder_mead_energy(_lib.ptr(records), _lib.ptr(counts), records.shape[1], N, _lib.ptr(x0_),
-                                             _lib.ptr(lb_), _lib.ptr(ub_), int(max_eval), float(depth_range[0]),
-                                             float(depth_range[1]), _lib.ptr(x), _lib.ptr(f), _lib.ptr(nev),
-                                             _lib.stream_ptr(stream))
+    L = _lib.load()
+    if N <= 128:  # kNmCoop workgroups per problem, launched cooperatively (same bits as one workgroup)
+        ws = _lib.workspace(L.pcnn_nelder_mead_energy_workspace_size(N), dev, "nelder_mead", stream)
+        rc = L.pcnn_nelder_mead_energy_coop(_lib.ptr(records), _lib.ptr(counts), records.shape[1], N, _lib.ptr(x0_),
+                                            _lib.ptr(lb_), _lib.ptr(ub_), int(max_eval), float(depth_range[0]),
+                                            float(depth_range[1]), _lib.ptr(x), _lib.ptr(f), _lib.ptr(nev),
+                                            _lib.ptr(ws), ws.numel(), _lib.stream_ptr(stream))
+    else:
+        rc = L.pcnn_nelder_mead_energy(_lib.ptr(records), _lib.ptr(counts), records.shape[1], N, _lib.ptr(x0_),
+                                       _lib.ptr(lb_), _lib.ptr(ub_), int(max_eval), float(depth_range[0]),
+                                       float(depth_range[1]), _lib.ptr(x), _lib.ptr(f), _lib.ptr(nev),
+                                       _lib.stream_ptr(stream))
     _lib.check(rc, "nelder_mead_device")
     return x, f, nev
 

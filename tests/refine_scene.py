@@ -112,18 +112,20 @@ class GraphBoxRenderer:
     solve_icp uses once per stage.  The test harness's stand-in for the
     reference's OpenGL pass."""
 
-    def __init__(self, half_of, H=480, W=640, camera=CAMERA, device="cuda"):
+    def __init__(self, half_of, H=480, W=640, camera=CAMERA, device="cuda", dtype=None):
+        import torch
         self.half_of, self.H, self.W, self.camera, self.device = half_of, H, W, camera, device
+        self.dtype = dtype or torch.float32  # the ray-box arithmetic (the maps are float32 either way)
         self.graphs = {}
 
     def _graph(self, K):
         import torch
         if K not in self.graphs:
-            rt = torch.zeros((K, 12), dtype=torch.float64, device=self.device)
+            rt = torch.zeros((K, 12), dtype=self.dtype, device=self.device)
             rt[:, 0] = rt[:, 4] = rt[:, 8] = 1.0
             rt[:, 11] = 1.0
-            h = torch.full((K, 3), 0.05, dtype=torch.float64, device=self.device)
-            c = torch.ones(K, dtype=torch.float64, device=self.device)
+            h = torch.full((K, 3), 0.05, dtype=self.dtype, device=self.device)
+            c = torch.ones(K, dtype=self.dtype, device=self.device)
             s = torch.cuda.Stream()
             s.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(s):  # warm-up outside the capture
@@ -139,9 +141,9 @@ class GraphBoxRenderer:
         import torch
         K = len(objs)
         g, out, rt, h, c = self._graph(K)
-        rt.copy_(torch.from_numpy(np.stack([_rt_of(p) for p in poses])))
-        h.copy_(torch.from_numpy(np.stack([np.asarray(self.half_of(o), np.float64) for o in objs])))
-        c.copy_(torch.tensor([float(o) for o in objs], dtype=torch.float64))
+        rt.copy_(torch.from_numpy(np.stack([_rt_of(p) for p in poses])).to(self.dtype))
+        h.copy_(torch.from_numpy(np.stack([np.asarray(self.half_of(o), np.float64) for o in objs])).to(self.dtype))
+        c.copy_(torch.tensor([float(o) for o in objs], dtype=self.dtype))
         g.replay()
         return tuple(o.clone() for o in out)
 
@@ -158,8 +160,8 @@ def _render_boxes(rt, h, cls, H, W, camera, device):
     K = rt.shape[0]
     R = rt[:, :9].reshape(K, 3, 3)
     tt = rt[:, 9:12]
-    ys, xs = torch.meshgrid(torch.arange(H, dtype=torch.float64, device=device),
-                            torch.arange(W, dtype=torch.float64, device=device), indexing="ij")
+    ys, xs = torch.meshgrid(torch.arange(H, dtype=rt.dtype, device=device),
+                            torch.arange(W, dtype=rt.dtype, device=device), indexing="ij")
     d = torch.stack([(xs - px) / fx, (ys - py) / fy, torch.ones_like(xs)], -1)[None]      # (1,H,W,3)
     o = -(R[:, 0, :] * tt[:, 0:1] + R[:, 1, :] * tt[:, 1:2] + R[:, 2, :] * tt[:, 2:3])  # R^T (-t), (K,3)
     Rb = R[:, None, None]                                                                 # (K,1,1,3,3)
