@@ -197,7 +197,7 @@ struct EmitShared {
 
 __device__ __forceinline__ void emit_max(EmitShared& sh, int r0, int cap, int batch_index, int cls, float score,
                                          float bb_distance, float bb_height, float bb_width, int x, int y,
-                                         int is_train, int C, const float* __restrict__ extents,
+                                         int is_train, int C, const float* __restrict__ ext_cls,
                                          const float* __restrict__ mb, const float* __restrict__ gt, int num_gt,
                                          float* __restrict__ top_box, float* __restrict__ top_pose,
                                          float* __restrict__ top_target, float* __restrict__ top_weight,
@@ -224,7 +224,7 @@ __device__ __forceinline__ void emit_max(EmitShared& sh, int r0, int cap, int ba
       const int gt_batch = (int)gt[i * 13 + 0];
       const int gt_id = (int)gt[i * 13 + 1];
       if (cls == gt_id && batch_index == gt_batch) {
-        const float ov = box_overlap(cls, extents, mb, gt + (size_t)i * 13, sh.box);
+        const float ov = box_overlap(0, ext_cls, mb, gt + (size_t)i * 13, sh.box);  // ext_cls: this class's row
         if ((double)ov > 0.2) atomicMin(&sh.gsel, i);
       }
     }

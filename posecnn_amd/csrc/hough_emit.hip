@@ -53,7 +53,8 @@ __global__ void __launch_bounds__(kEmitThreads) k_hough_emit(int B, int H, int W
     const int slot = nms ? (int)pk[6] : k;
     const int cls = ws.slot_cls[(size_t)b * C + slot];
     emit_max(esh, s_off + k * rpm, cap, batch_base + b, cls, pk[0], pk[1], pk[2], pk[3], (int)pk[4], (int)pk[5],
-             is_train, C, extents, mb, gt, num_gt, top_box, top_pose, top_target, top_weight, top_domain, ws.diag);
+             is_train, C, extents + (size_t)cls * 3, mb, gt, num_gt, top_box, top_pose, top_target, top_weight,
+             top_domain, ws.diag);
     __syncthreads();
   }
   if (b == 0) emit_count(s_total, cap, C, top_box, top_pose, top_target, top_weight, top_domain, num_rois);

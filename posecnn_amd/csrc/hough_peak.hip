@@ -161,8 +161,15 @@ __device__ PeakOut exact_cell(int cx, int cy, int cls, float count_f, const floa
 //    serial chain.  The bb pass then uses the cached cone flags and |dx|,
 //    |dy| (no second read of the voters).
 // diag[3] counts the maxima that took that fallback.
+// The per-thread voter arrays are unrolled register arrays; the kernel picks
+// the smallest instantiation that holds the cell (kPsumPer voters per thread
+// is the largest), because the code executed once per cell is what costs:
+// at 24 per thread the kernel was 62 KB of straight-line code, and a
+// workgroup that runs through it once mostly waits on instruction fetch.
 constexpr int kPsumPer = 24;      // voters per thread held in registers (nv <= kPsumPer * kPeakThreads)
+constexpr int kPsumSmall = 8;     // the small instantiation
 constexpr int kPsumEvents = 256;  // crossing events per cell
+constexpr int kPsumBatch = 8;     // phase A voters loaded per batch
 
 struct PsumTr {  // running-sum transducer: increment for S even / odd; has = the run starts at an event
   int i0, i1, has;
@@ -193,6 +200,9 @@ __device__ __forceinline__ PsumTr psum_term(float q) {
   }
   return t;
 }
+// ilogb of a positive finite double (v_frexp_exp); 0 -> a sentinel that is
+// neither an exponent nor the -100000 of 'no partial sum yet'
+__device__ __forceinline__ int dlogb(double x) { return x > 0.0 ? __builtin_amdgcn_frexp_exp(x) - 1 : -200000; }
 __device__ __forceinline__ int f32_binade(float s) {  // E of a positive normal float, -1000 otherwise
   const unsigned b = __float_as_uint(s);
   const int e = (int)((b >> 23) & 0xFF);
@@ -212,44 +222,69 @@ struct PsumShared {
 
 // Returns true with o filled, or false (block-uniform) when the caller must
 // take exact_cell's serial path.
+template <int kPer>
 __device__ bool exact_cell_par(int cx, int cy, int cls, float count_f, const float4* __restrict__ vd,
                                const int32_t* __restrict__ vp, int nv, int W, float inlier,
-                               const float* __restrict__ extents, const float* __restrict__ meta, PsumShared& sh,
+                               PsumShared& sh, float pre, float gpre, int ngpre, float* s_pre, float* s_gt,
                                PeakOut& o) {
   const int nt = blockDim.x, t = threadIdx.x, lane = pcnn::lane_id(), wave = t >> 6, nw = nt >> 6;
+  constexpr int kBatch = kPer < kPsumBatch ? kPer : kPsumBatch;
+  const float rcpW = 1.f / (float)W;
   const int m = (nv + nt - 1) / nt;
-  if (m > kPsumPer) return false;  // block-uniform
+  if (m > kPer) return false;  // block-uniform
   const int j0 = t * m;
-  // phase A: the thread's voters -> voting flags, d, and the cone voters' |dx|, |dy|
-  float dd[kPsumPer];
-  unsigned pk[kPsumPer];
+  // phase A: the thread's voters -> voting flags, d, and the cone voters' |dx|, |dy|;
+  // a batch's loads are all issued before its first use (one memory latency
+  // per kBatch voters, not one per voter)
+  float dd[kPer];
+  unsigned pk[kPer];
   unsigned vbits = 0;
   bool bad = false;
 #pragma unroll
-  for (int i = 0; i < kPsumPer; i++) {
+  for (int i = 0; i < kPer; i++) {
     dd[i] = 0.f;
     pk[i] = 0xFFFFFFFFu;
-    const int j = j0 + i;
-    if (i < m && j < nv) {
-      const float4 q = vd[j];
-      const int p = vp[j];
-      const int x = p % W, y = p / W;
-      if (cone_pred(cx, cy, x, y, q.x, q.y, inlier)) {
-        const int adx = abs(x - cx), ady = abs(y - cy);
-        pk[i] = (unsigned)adx | ((unsigned)ady << 16);
-        if ((float)adx < q.w && (float)ady < q.w) {  // cu.cc:285-288
-          vbits |= 1u << i;
-          dd[i] = q.z;
-          bad |= !(q.z >= 0.f) || !isfinite(q.z);
+  }
+#pragma unroll
+  for (int i0 = 0; i0 < kPer; i0 += kBatch) {
+    if (i0 >= m) break;  // block-uniform
+    float4 q[kBatch];
+    int p[kBatch];
+#pragma unroll
+    for (int k = 0; k < kBatch; k++) {
+      const int j = j0 + i0 + k;
+      const bool live = i0 + k < m && j < nv;
+      q[k] = live ? vd[j] : make_float4(0.f, 0.f, 0.f, 0.f);
+      p[k] = live ? vp[j] : -1;
+    }
+#pragma unroll
+    for (int k = 0; k < kBatch; k++) {
+      const int i = i0 + k;
+      if (p[k] >= 0) {
+        int y = __float2int_rz((float)p[k] * rcpW), x = p[k] - y * W;  // y = p / W up to a small error, fixed up
+        while (x < 0) { y--; x += W; }
+        while (x >= W) { y++; x -= W; }
+        if (cone_pred(cx, cy, x, y, q[k].x, q[k].y, inlier)) {
+          const int adx = abs(x - cx), ady = abs(y - cy);
+          pk[i] = (unsigned)adx | ((unsigned)ady << 16);
+          if ((float)adx < q[k].w && (float)ady < q[k].w) {  // cu.cc:285-288
+            vbits |= 1u << i;
+            dd[i] = q[k].z;
+            bad |= !(q[k].z >= 0.f) || !isfinite(q[k].z);
+          }
         }
       }
     }
   }
+  // the bb pass's class extents / camera row and the emit's GT rows, loaded
+  // by the caller before the voters (their latency is behind phase A's)
+  if (t < 9) s_pre[t] = pre;
+  if (t < ngpre) s_gt[t] = gpre;
   // scan 1: voting counts and exact-ish prefix sums (double) -> binade predictions
   int c = __popc(vbits);
   double D = 0.0;
 #pragma unroll
-  for (int i = 0; i < kPsumPer; i++) D += (double)dd[i];
+  for (int i = 0; i < kPer; i++) D += (double)dd[i];
   int ci = c;
   double Di = D;
 #pragma unroll
@@ -263,19 +298,24 @@ __device__ bool exact_cell_par(int cx, int cy, int cls, float count_f, const flo
   __syncthreads();
   int cbase = ci - c;
   double Pbase = Di - D;
-  for (int w = 0; w < wave; w++) { cbase += sh.wcnt[w]; Pbase += sh.wsum[w]; }
+#pragma unroll
+  for (int w = 0; w < kPeakThreads / 64; w++) {  // independent LDS reads, summed in wave order
+    const int cw = sh.wcnt[w];
+    const double sw = sh.wsum[w];
+    if (w < wave) { cbase += cw; Pbase += sw; }
+  }
   if (t == nt - 1) sh.total_cnt = cbase + c;
   // phase B: events and the thread's tail transducer (terms after its last event)
   PsumTr tail = psum_id();
   int nev = 0;
   {
     double P = Pbase;
-    int Eprev = cbase > 0 ? ilogb(Pbase) : -100000;
+    int Eprev = cbase > 0 ? dlogb(Pbase) : -100000;
 #pragma unroll
-    for (int i = 0; i < kPsumPer; i++) {
+    for (int i = 0; i < kPer; i++) {
       if (vbits & (1u << i)) {
         P += (double)dd[i];
-        const int E = P > 0.0 ? ilogb(P) : -100000;
+        const int E = P > 0.0 ? dlogb(P) : -100000;
         if (E != Eprev) {  // first term or a predicted crossing: an event
           nev++;
           tail = PsumTr{0, 0, 1};
@@ -305,7 +345,12 @@ __device__ bool exact_cell_par(int cx, int cy, int cls, float count_f, const flo
   __syncthreads();
   PsumTr X = psum_id();
   int ebase = 0;
-  for (int w = 0; w < wave; w++) { X = psum_cat(X, sh.wtr[w]); ebase += sh.wev[w]; }
+#pragma unroll
+  for (int w = 0; w < kPeakThreads / 64; w++) {
+    const PsumTr tw = sh.wtr[w];
+    const int ew = sh.wev[w];
+    if (w < wave) { X = psum_cat(X, tw); ebase += ew; }
+  }
   {  // exclusive within the wave
     PsumTr y;
     y.i0 = __shfl_up(ti.i0, 1, 64);
@@ -322,13 +367,13 @@ __device__ bool exact_cell_par(int cx, int cy, int cls, float count_f, const flo
   {
     PsumTr tr = X;
     double P = Pbase;
-    int Eprev = cbase > 0 ? ilogb(Pbase) : -100000;
+    int Eprev = cbase > 0 ? dlogb(Pbase) : -100000;
     int e = ebase;
 #pragma unroll
-    for (int i = 0; i < kPsumPer; i++) {
+    for (int i = 0; i < kPer; i++) {
       if (vbits & (1u << i)) {
         P += (double)dd[i];
-        const int E = P > 0.0 ? ilogb(P) : -100000;
+        const int E = P > 0.0 ? dlogb(P) : -100000;
         if (E != Eprev) {
           if (e < kPsumEvents) {
             sh.ev_d[e] = dd[i];
@@ -354,37 +399,50 @@ __device__ bool exact_cell_par(int cx, int cy, int cls, float count_f, const flo
   o.bbw2 = 0.f;
   if (!(count_f > 0.f)) return true;  // hough_data stays memset-zero (cu.cc:296, :698-708)
   if (total == 0 || sh.fail || sh.total_ev > kPsumEvents) return false;
-  // the walk: one lane adds the events with the real fp32 add from the exact running sum
-  if (t == 0) {
+  // the walk: the events' fp32 adds in order from the exact running sum.  Wave
+  // 0 holds 64 events per pass in its lanes and runs the chain wave-uniformly
+  // (operands by readlane, the carried S / E in registers); lane k keeps the
+  // k-th event's S for phase D.
+  if (wave == 0) {
     float s = 0.f;
-    int fail = 0;
+    int fail = 0, Sp = 0, Ep = 0;
     const int ne = sh.total_ev;
-    for (int e = 0; e < ne && !fail; e++) {
-      if (e > 0) {
-        const int E = sh.ev_E[e - 1];
-        int S = sh.ev_S[e - 1];
-        S += (S & 1) ? sh.ev_i1[e] : sh.ev_i0[e];
-        fail |= !(S >= (1 << 23) && S < (1 << 24));
-        s = ldexpf((float)S, E - 23);
+    for (int e0 = 0; e0 < ne; e0 += 64) {
+      const int el = e0 + lane;
+      const bool lv = el < ne;
+      const float ld = lv ? sh.ev_d[el] : 0.f;
+      const int lE = lv ? sh.ev_E[el] : 0, l0 = lv ? sh.ev_i0[el] : 0, l1 = lv ? sh.ev_i1[el] : 0;
+      int myS = 0;
+      const int n = min(64, ne - e0);
+      for (int k = 0; k < n; k++) {
+        if (e0 + k > 0) {
+          const int inc0 = __builtin_amdgcn_readlane(l0, k), inc1 = __builtin_amdgcn_readlane(l1, k);
+          int S = Sp + ((Sp & 1) ? inc1 : inc0);
+          fail |= !(S >= (1 << 23) && S < (1 << 24));
+          s = ldexpf((float)S, Ep - 23);
+        }
+        s = s + __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ld), k));  // cu.cc:291, in order
+        const int E = __builtin_amdgcn_readlane(lE, k);
+        fail |= f32_binade(s) != E;
+        Sp = (int)ldexpf(s, 23 - E);
+        Ep = E;
+        if (lane == k) myS = Sp;
       }
-      s = s + sh.ev_d[e];  // cu.cc:291, in the reference's order
-      const int E = sh.ev_E[e];
-      fail |= f32_binade(s) != E;
-      sh.ev_S[e] = (int)ldexpf(s, 23 - E);
+      if (lv) sh.ev_S[el] = myS;
     }
-    if (!fail && ne > 0) {
-      const int E = sh.ev_E[ne - 1];
-      int S = sh.ev_S[ne - 1];
+    if (ne > 0) {
       const PsumTr ft = sh.final_tr;
-      S += (S & 1) ? ft.i1 : ft.i0;
+      const int S = Sp + ((Sp & 1) ? ft.i1 : ft.i0);
       fail |= !(S >= (1 << 23) && S < (1 << 24));
-      s = ldexpf((float)S, E - 23);
+      s = ldexpf((float)S, Ep - 23);
     }
     fail |= ne == 0;
-    sh.fail = fail;
-    sh.dist = s / count_f;  // cu.cc:298
-    sh.bbw = -1;
-    sh.bbh = -1;
+    if (lane == 0) {
+      sh.fail = fail;
+      sh.dist = s / count_f;  // cu.cc:298
+      sh.bbw = -1;
+      sh.bbh = -1;
+    }
   }
   __syncthreads();
   if (sh.fail) return false;
@@ -394,7 +452,7 @@ __device__ bool exact_cell_par(int cx, int cy, int cls, float count_f, const flo
     if (c > 0) {
       int S = 0, E = 0;
       double P = Pbase;
-      int Eprev = cbase > 0 ? ilogb(Pbase) : -100000;
+      int Eprev = cbase > 0 ? dlogb(Pbase) : -100000;
       if (cbase > 0 && ebase > 0) {  // the run continues from the last event before this thread
         S = sh.ev_S[ebase - 1];
         E = sh.ev_E[ebase - 1];
@@ -405,10 +463,10 @@ __device__ bool exact_cell_par(int cx, int cy, int cls, float count_f, const flo
       }
       int e = ebase;
 #pragma unroll
-      for (int i = 0; i < kPsumPer; i++) {
+      for (int i = 0; i < kPer; i++) {
         if (vbits & (1u << i)) {
           P += (double)dd[i];
-          const int Ep = P > 0.0 ? ilogb(P) : -100000;
+          const int Ep = P > 0.0 ? dlogb(P) : -100000;
           if (Ep != Eprev) {
             S = sh.ev_S[e];
             E = sh.ev_E[e];
@@ -424,14 +482,13 @@ __device__ bool exact_cell_par(int cx, int cy, int cls, float count_f, const flo
     }
     if (!ok) sh.fail = 1;
   }
-  __syncthreads();
-  if (sh.fail) return false;
-  // bb extent with T(distance) over the cached cone voters (cu.cc:300-330)
+  // bb extent with T(distance) over the cached cone voters (cu.cc:300-330),
+  // in the same phase as the check (discarded if the check failed)
   const float distance = sh.dist;
-  const float Tm = project_box(cls, extents, meta, distance, 0.6f);  // cu.cc:317
+  const float Tm = project_box(0, s_pre, s_pre + 3, distance, 0.6f);  // cu.cc:317 (s_pre: the class's row)
   int bw = -1, bh = -1;
 #pragma unroll
-  for (int i = 0; i < kPsumPer; i++) {
+  for (int i = 0; i < kPer; i++) {
     if (pk[i] != 0xFFFFFFFFu) {
       const int adx = (int)(pk[i] & 0xFFFFu), ady = (int)(pk[i] >> 16);
       if ((float)adx < Tm && (float)ady < Tm) {
@@ -445,6 +502,7 @@ __device__ bool exact_cell_par(int cx, int cy, int cls, float count_f, const flo
   if (lane == 0 && bw >= 0) atomicMax(&sh.bbw, bw);
   if (lane == 0 && bh >= 0) atomicMax(&sh.bbh, bh);
   __syncthreads();
+  if (sh.fail) return false;
   o.distance = distance;
   o.bbw2 = 2 * (float)sh.bbw;
   o.bbh2 = 2 * (float)sh.bbh;
@@ -473,6 +531,8 @@ __global__ void __launch_bounds__(kPeakThreads) k_hough_peak(int B, int H, int W
   __shared__ int s_off[2];
   __shared__ EmitShared esh;
   __shared__ PsumShared psh;
+  __shared__ float s_pre[9];             // extents[cls][0..2], meta[0..5] of the image
+  __shared__ float s_gt[kPeakThreads];  // the GT rows (train mode, num_gt * 13 <= kPeakThreads)
   const int b = blockIdx.y, slot = blockIdx.x;
   const int rpm = is_train ? 9 : 1;
   if (slot == 0 && b == 0) {  // batch row count: sum over images of nvote * rpm
@@ -502,11 +562,24 @@ __global__ void __launch_bounds__(kPeakThreads) k_hough_peak(int B, int H, int W
   const float* mb = meta + (size_t)b * num_meta;
   const float4* vd = ws.vdat + (size_t)b * ws.vcap + vb;
   const int32_t* vpp = ws.vpos + (size_t)b * ws.vcap + vb;
+  // what the bb pass and the emit read, loaded now and parked in LDS once the
+  // voters have arrived (exact_cell_par, or below on the serial path)
+  const int t = threadIdx.x;
+  const float pre = t < 3 ? extents[cls * 3 + t] : (t < 9 ? mb[t - 3] : 0.f);
+  const int ngpre = is_train && num_gt * 13 <= kPeakThreads ? num_gt * 13 : 0;
+  const float gpre = t < ngpre ? gt[t] : 0.f;
   PeakOut o;
-  if (!(psum && exact_cell_par(cx, cy, cls, (float)cnt, vd, vpp, nv, W, inlier, extents, mb, psh, o))) {
+  const int mper = (nv + kPeakThreads - 1) / kPeakThreads;
+  if (!(psum && (mper <= kPsumSmall
+                     ? exact_cell_par<kPsumSmall>(cx, cy, cls, (float)cnt, vd, vpp, nv, W, inlier, psh, pre, gpre,
+                                                  ngpre, s_pre, s_gt, o)
+                     : exact_cell_par<kPsumPer>(cx, cy, cls, (float)cnt, vd, vpp, nv, W, inlier, psh, pre, gpre,
+                                                ngpre, s_pre, s_gt, o)))) {
     o = exact_cell(cx, cy, cls, (float)cnt, vd, vpp, nv, W, inlier, extents, mb, sh_d, sh_red);
     if (psum && threadIdx.x == 0) atomicAdd(&ws.diag[3], 1);  // took the serial chain
   }
+  if (t < 9) s_pre[t] = pre;
+  if (t < ngpre) s_gt[t] = gpre;
   if (threadIdx.x == 0) {
     float* pk = ws.peak + ((size_t)b * ws.pks + slot) * 8;
     pk[0] = o.count;
@@ -518,8 +591,17 @@ __global__ void __launch_bounds__(kPeakThreads) k_hough_peak(int B, int H, int W
     if (o.mismatch) atomicAdd(&ws.diag[0], 1);
   }
   __syncthreads();  // s_off[0] complete
-  emit_max(esh, s_off[0] + slot * rpm, cap, batch_base + b, cls, o.count, o.distance, o.bbh2, o.bbw2, cx, cy,
-           is_train, C, extents, mb, gt, num_gt, top_box, top_pose, top_target, top_weight, top_domain, ws.diag);
+  // two call sites, so that each inlined copy sees one address space for the
+  // GT rows: LDS reads (ds_read) do not wait for this wave's earlier global
+  // stores the way generic (flat) reads of a mixed pointer would
+  if (ngpre)
+    emit_max(esh, s_off[0] + slot * rpm, cap, batch_base + b, cls, o.count, o.distance, o.bbh2, o.bbw2, cx, cy,
+             is_train, C, s_pre, s_pre + 3, s_gt, num_gt, top_box, top_pose, top_target, top_weight, top_domain,
+             ws.diag);
+  else
+    emit_max(esh, s_off[0] + slot * rpm, cap, batch_base + b, cls, o.count, o.distance, o.bbh2, o.bbw2, cx, cy,
+             is_train, C, s_pre, s_pre + 3, gt, num_gt, top_box, top_pose, top_target, top_weight, top_domain,
+             ws.diag);
 }
 
 // multi-instance (NMS) path
@@ -551,6 +633,7 @@ __global__ void __launch_bounds__(kPeakThreads) k_hough_cand_data(int H, int W, 
   __shared__ __attribute__((aligned(16))) float sh_d[kPeakChunk + 4];
   __shared__ float sh_red[2 * (kPeakThreads / 64)];
   __shared__ PsumShared psh;
+  __shared__ float s_pre[9];
   const int b = blockIdx.y;
   const int ncand = min(ws.ncand[b], kCandCap);
   const int HW = H * W;
@@ -564,8 +647,15 @@ __global__ void __launch_bounds__(kPeakThreads) k_hough_cand_data(int H, int W, 
     const float4* vd = ws.vdat + (size_t)b * ws.vcap + vb;
     const int32_t* vpp = ws.vpos + (size_t)b * ws.vcap + vb;
     const float* mb = meta + (size_t)b * num_meta;
+    const int t = threadIdx.x;
+    const float pre = t < 3 ? extents[cls * 3 + t] : (t < 9 ? mb[t - 3] : 0.f);
     PeakOut o;
-    if (!(psum && exact_cell_par(cell % W, cell / W, cls, cnt, vd, vpp, nv, W, inlier, extents, mb, psh, o))) {
+    const int mper = (nv + kPeakThreads - 1) / kPeakThreads;
+    if (!(psum && (mper <= kPsumSmall
+                       ? exact_cell_par<kPsumSmall>(cell % W, cell / W, cls, cnt, vd, vpp, nv, W, inlier, psh, pre,
+                                                    0.f, 0, s_pre, nullptr, o)
+                       : exact_cell_par<kPsumPer>(cell % W, cell / W, cls, cnt, vd, vpp, nv, W, inlier, psh, pre,
+                                                  0.f, 0, s_pre, nullptr, o)))) {
       o = exact_cell(cell % W, cell / W, cls, cnt, vd, vpp, nv, W, inlier, extents, mb, sh_d, sh_red);
       if (psum && threadIdx.x == 0) atomicAdd(&ws.diag[3], 1);
     }
