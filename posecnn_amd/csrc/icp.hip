@@ -783,58 +783,72 @@ __global__ void __launch_bounds__(kBlk) k_grid_count(const float4* __restrict__ 
   bucket_of[i] = b;
 }
 
-// exclusive scan of the bucket counts (one workgroup): start[b], start[NB] = total; cursor = start
-__global__ void __launch_bounds__(1024) k_grid_scan(const int32_t* __restrict__ bcount, int32_t* __restrict__ start,
-                                                    int32_t* __restrict__ cursor) {
-  __shared__ int part[1024];
-  constexpr int per = kGridBuckets / 1024;  // 128 consecutive buckets per thread, as 32 int4 loads in flight
-  const int t = threadIdx.x;
-  int4 v[per / 4];
-#pragma unroll
-  for (int k = 0; k < per / 4; k++) v[k] = ((const int4*)(bcount + t * per))[k];
-  int s = 0;
-#pragma unroll
-  for (int k = 0; k < per / 4; k++) s += v[k].x + v[k].y + v[k].z + v[k].w;
-  part[t] = s;
-  __syncthreads();
-  for (int off = 1; off < 1024; off <<= 1) {  // Hillis-Steele inclusive scan
-    const int v = t >= off ? part[t - off] : 0;
-    __syncthreads();
-    part[t] += v;
-    __syncthreads();
-  }
-  int run = part[t] - s;
-#pragma unroll
-  for (int k = 0; k < per / 4; k++) {
-    int4 o;
-    o.x = run;
-    o.y = o.x + v[k].x;
-    o.z = o.y + v[k].y;
-    o.w = o.z + v[k].z;
-    run = o.w + v[k].w;
-    ((int4*)(start + t * per))[k] = o;
-    ((int4*)(cursor + t * per))[k] = o;
-  }
-  if (t == 1023) start[kGridBuckets] = run;
+// exclusive scan of the bucket counts: start[b], start[NB] = total; cursor =
+// start.  Two passes over kGridScanBlocks workgroups of 1024 buckets each (a
+// single workgroup writing the 1 MB of starts and cursors took 110 us): the
+// per-workgroup totals, then each workgroup adds the totals before it to a
+// local scan of its own buckets.
+constexpr int kGridScanBlocks = kGridBuckets / 1024;
+__global__ void __launch_bounds__(256) k_grid_bsum(const int32_t* __restrict__ bcount, int32_t* __restrict__ bsum) {
+  __shared__ int sh[4];
+  const int4 v = ((const int4*)(bcount + (size_t)blockIdx.x * 1024))[threadIdx.x];
+  const int s = block_sum_int<256>(v.x + v.y + v.z + v.w, sh);
+  if (threadIdx.x == 0) bsum[blockIdx.x] = s;
 }
 
+__global__ void __launch_bounds__(256) k_grid_bscan(const int32_t* __restrict__ bcount,
+                                                    const int32_t* __restrict__ bsum, int32_t* __restrict__ start,
+                                                    int32_t* __restrict__ cursor) {
+  __shared__ int sh[4], wsum[4];
+  const int t = threadIdx.x, lane = pcnn::lane_id(), wave = t >> 6;
+  int pre = 0;  // totals of the workgroups before this one
+  for (int i = t; i < (int)blockIdx.x; i += 256) pre += bsum[i];
+  pre = block_sum_int<256>(pre, sh);
+  const int4 v = ((const int4*)(bcount + (size_t)blockIdx.x * 1024))[t];
+  const int mine = v.x + v.y + v.z + v.w;
+  int inc = mine;  // inclusive wave scan of the 4-bucket sums
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int u = __shfl_up(inc, d, 64);
+    if (lane >= d) inc += u;
+  }
+  if (lane == 63) wsum[wave] = inc;
+  __syncthreads();
+  int run = pre + inc - mine;
+#pragma unroll
+  for (int w = 0; w < 4; w++) run += w < wave ? wsum[w] : 0;
+  int4 o;
+  o.x = run;
+  o.y = o.x + v.x;
+  o.z = o.y + v.y;
+  o.w = o.z + v.z;
+  ((int4*)(start + (size_t)blockIdx.x * 1024))[t] = o;
+  ((int4*)(cursor + (size_t)blockIdx.x * 1024))[t] = o;
+  if (blockIdx.x == gridDim.x - 1 && t == 255) start[kGridBuckets] = o.w + v.w;
+}
+
+// the depth points in bucket order, each with its index (w: the int bits), so
+// that the search reads a candidate with one load
 __global__ void __launch_bounds__(kBlk) k_grid_fill(const int32_t* __restrict__ cnt, int nseg,
+                                                    const float4* __restrict__ dpts,
                                                     const int32_t* __restrict__ bucket_of, int32_t* __restrict__ cursor,
-                                                    int32_t* __restrict__ idx) {
+                                                    float4* __restrict__ spts) {
   __shared__ int ish[kBlk / 64];
   const int M = score_m(cnt, nseg, ish);
   const int i = blockIdx.x * kBlk + threadIdx.x;
   if ((int)blockIdx.x * kBlk >= M || i >= M) return;
   const int b = bucket_of[i];
-  if (b >= 0) idx[atomicAdd(cursor + b, 1)] = i;
+  if (b >= 0) {
+    const float4 p = dpts[i];
+    spts[atomicAdd(cursor + b, 1)] = make_float4(p.x, p.y, p.z, __int_as_float(i));
+  }
 }
 
 // grid (query blocks, hypotheses): nearest depth point of each transformed
 // model point, flagged when within the radius
-__global__ void __launch_bounds__(kBlk) k_score_nn(const float4* __restrict__ model, const float4* __restrict__ dpts,
-                                                   const int32_t* __restrict__ cnt, int nseg,
-                                                   const float* __restrict__ hyps, float r2, double inv_s,
-                                                   const int32_t* __restrict__ start, const int32_t* __restrict__ idx,
+__global__ void __launch_bounds__(kBlk) k_score_nn(const float4* __restrict__ model, const int32_t* __restrict__ cnt,
+                                                   int nseg, const float* __restrict__ hyps, float r2, double inv_s,
+                                                   const int32_t* __restrict__ start, const float4* __restrict__ spts,
                                                    uint8_t* __restrict__ flags, int cap) {
   __shared__ int ish[kBlk / 64];
   const int M = score_m(cnt, nseg, ish);
@@ -856,22 +870,31 @@ __global__ void __launch_bounds__(kBlk) k_score_nn(const float4* __restrict__ mo
   int bi = -1;
   // rings of cells by Chebyshev distance d = 0, 1, 2 around q's cell (cells
   // of edge s = 0.5005 r: every point within r is at most 2 cells away).  A
-  // point in ring d >= 1 is farther than (d - 1) s from q, so ring d is
-  // skipped once that bound (with a 1e-6 margin for the fp32 distances)
-  // exceeds the best squared distance so far: no point there can equal or
-  // beat it.
+  // cell is skipped when the squared distance from q to its box, less a 1e-5
+  // relative margin (far above the fp32 distance's rounding), exceeds the best
+  // squared distance so far: no point in it can equal or beat that.  Ring 2 is
+  // skipped whole once (d - 1) s does.
   const double s_cell = 1.0 / inv_s;
+  const double gx0 = (double)x - (double)cx * s_cell, gy0 = (double)y - (double)cy * s_cell,
+               gz0 = (double)z - (double)cz * s_cell;  // q's offset inside its cell
+  auto gap = [&](int o, double g) {  // distance from q to the cell o steps away along one axis
+    return o > 0 ? (double)o * s_cell - g : (o < 0 ? g - (double)(o + 1) * s_cell : 0.0);
+  };
   for (int d = 0; d <= 2; d++) {
     if (d >= 2 && (double)(d - 1) * s_cell * (d - 1) * s_cell * (1.0 - 1e-6) > (double)best) break;
     for (int dz = -d; dz <= d; dz++)
       for (int dy = -d; dy <= d; dy++)
         for (int dx = -d; dx <= d; dx++) {
           if (max(abs(dx), max(abs(dy), abs(dz))) != d) continue;
+          if (d > 0) {
+            const double ax = fmax(gap(dx, gx0), 0.0), ay = fmax(gap(dy, gy0), 0.0), az = fmax(gap(dz, gz0), 0.0);
+            if ((ax * ax + ay * ay + az * az) * (1.0 - 1e-5) > (double)best) continue;
+          }
           const int b = grid_bucket(cx + dx, cy + dy, cz + dz);
           const int e = start[b + 1];
           for (int k = start[b]; k < e; k++) {
-            const int i = idx[k];
-            const float4 p = dpts[i];
+            const float4 p = spts[k];
+            const int i = __float_as_int(p.w);
             const float ex = x - p.x, ey = y - p.y, ez = z - p.z;
             const float d2 = ex * ex + ey * ey + ez * ez;
             if (d2 < best || (bi >= 0 && d2 == best && i < bi)) {  // the first minimum in index order
@@ -1078,8 +1101,9 @@ extern "C" size_t pcnn_icp_score_workspace_size(int J, int H, int W) {
   cv.take<int32_t>((size_t)kGridBuckets);      // bucket counts
   cv.take<int32_t>((size_t)kGridBuckets + 1);  // bucket starts
   cv.take<int32_t>((size_t)kGridBuckets);      // fill cursors
+  cv.take<int32_t>((size_t)kGridScanBlocks);   // bucket-scan workgroup totals
   cv.take<int32_t>((size_t)HW);                // bucket of each depth point
-  cv.take<int32_t>((size_t)HW);                // point indices by bucket
+  cv.take<float4>((size_t)HW);                 // depth points (+ index) by bucket
   return cv.off + 256;
 }
 
@@ -1097,8 +1121,9 @@ extern "C" int pcnn_icp_score(const float* live, const int32_t* label, int obj, 
   int32_t* bcount = cv.take<int32_t>((size_t)kGridBuckets);
   int32_t* bstart = cv.take<int32_t>((size_t)kGridBuckets + 1);
   int32_t* cursor = cv.take<int32_t>((size_t)kGridBuckets);
+  int32_t* bsum = cv.take<int32_t>((size_t)kGridScanBlocks);
   int32_t* bucket_of = cv.take<int32_t>((size_t)HW);
-  int32_t* idx = cv.take<int32_t>((size_t)HW);
+  float4* spts = cv.take<float4>((size_t)HW);
   if (workspace_bytes < cv.off) return PCNN_ECAPACITY;
   PCNN_REQUIRE(radius > 0.f && radius < 1e6f);
   hipStream_t st = (hipStream_t)stream;
@@ -1110,10 +1135,11 @@ extern "C" int pcnn_icp_score(const float* live, const int32_t* label, int obj, 
   hipLaunchKernelGGL(k_score_scatter, dim3(nseg), dim3(kBlk), 0, st, live, label, obj, vertmap, HW, nseg, cnt, model,
                      dpts);
   hipLaunchKernelGGL(k_grid_count, dim3(qblocks), dim3(kBlk), 0, st, dpts, cnt, nseg, inv_s, bcount, bucket_of);
-  hipLaunchKernelGGL(k_grid_scan, dim3(1), dim3(1024), 0, st, bcount, bstart, cursor);
-  hipLaunchKernelGGL(k_grid_fill, dim3(qblocks), dim3(kBlk), 0, st, cnt, nseg, bucket_of, cursor, idx);
-  hipLaunchKernelGGL(k_score_nn, dim3(qblocks, J), dim3(kBlk), 0, st, model, dpts, cnt, nseg, hyps, radius * radius,
-                     inv_s, bstart, idx, flags, HW);
+  hipLaunchKernelGGL(k_grid_bsum, dim3(kGridScanBlocks), dim3(256), 0, st, bcount, bsum);
+  hipLaunchKernelGGL(k_grid_bscan, dim3(kGridScanBlocks), dim3(256), 0, st, bcount, bsum, bstart, cursor);
+  hipLaunchKernelGGL(k_grid_fill, dim3(qblocks), dim3(kBlk), 0, st, cnt, nseg, dpts, bucket_of, cursor, spts);
+  hipLaunchKernelGGL(k_score_nn, dim3(qblocks, J), dim3(kBlk), 0, st, model, cnt, nseg, hyps, radius * radius, inv_s,
+                     bstart, spts, flags, HW);
   hipLaunchKernelGGL(k_score_count_flags, dim3(J), dim3(1024), 0, st, flags, cnt, nseg, HW, score);
   hipLaunchKernelGGL(k_score_choose, dim3(1), dim3(64), 0, st, score, cnt, nseg, J, choose);
   PCNN_CHECK_LAUNCH();

@@ -418,7 +418,8 @@ def solve_icp(labelmap, depth, parameters, rois, poses, render, max_error=0.01, 
     vm, pv_c, pn_c = _render_many(render, objs, T)
     out, Tc = icp_center(live, lab, objt, vm, pv_c, pn_c, max_error, pose_in=torch.from_numpy(np.stack(T)).to(dev),
                          stream=stream)
-    c_h, Tc_h = out[:, 3].cpu().numpy(), Tc.cpu().numpy()
+    cT = torch.cat([out[:, 3:4].float(), Tc.float()], 1).cpu().numpy()  # one host read
+    c_h, Tc_h = cT[:, 0], cT[:, 1:].astype(np.float32)
     for k in range(n):
         if c_h[k] > 0:
             T[k] = Tc_h[k]
@@ -456,8 +457,8 @@ def solve_icp(labelmap, depth, parameters, rois, poses, render, max_error=0.01, 
                      pose_in=torch.from_numpy(hyps.reshape(-1, 7)).to(dev), stream=stream)
     refined = refined.view(n, len(dz), 7)
     chosen = [icp_score(live[k], lab, objs[k], vm[k], refined[k], 0.01, stream)[1] for k in range(n)]
-    ch = torch.cat(chosen).cpu().numpy()
-    ref_h = refined.cpu().numpy()
+    chr_ = torch.cat([torch.cat(chosen).float()[:, None], refined.reshape(n, -1).float()], 1).cpu().numpy()
+    ch, ref_h = chr_[:, 0].astype(np.int64), chr_[:, 1:].reshape(n, len(dz), 7).astype(np.float32)  # one host read
     for k, i in enumerate(rows):
         poses_new[i] = T[k]
         poses_icp[i] = ref_h[k, int(ch[k])]
