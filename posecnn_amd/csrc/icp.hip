@@ -768,9 +768,10 @@ __device__ __forceinline__ int score_m(const int32_t* __restrict__ cnt, int nseg
 // no query can be within r of them)
 __global__ void __launch_bounds__(kBlk) k_grid_count(const float4* __restrict__ dpts, const int32_t* __restrict__ cnt,
                                                      int nseg, double inv_s, int32_t* __restrict__ bcount,
-                                                     int32_t* __restrict__ bucket_of) {
+                                                     int32_t* __restrict__ bucket_of, int32_t* __restrict__ Mdev) {
   __shared__ int ish[kBlk / 64];
   const int M = score_m(cnt, nseg, ish);
+  if (blockIdx.x == 0 && threadIdx.x == 0) *Mdev = M;  // the point count, for the launches after this one
   const int i = blockIdx.x * kBlk + threadIdx.x;
   if ((int)blockIdx.x * kBlk >= M || i >= M) return;
   const float4 d = dpts[i];
@@ -829,12 +830,11 @@ __global__ void __launch_bounds__(256) k_grid_bscan(const int32_t* __restrict__ 
 
 // the depth points in bucket order, each with its index (w: the int bits), so
 // that the search reads a candidate with one load
-__global__ void __launch_bounds__(kBlk) k_grid_fill(const int32_t* __restrict__ cnt, int nseg,
+__global__ void __launch_bounds__(kBlk) k_grid_fill(const int32_t* __restrict__ Mdev,
                                                     const float4* __restrict__ dpts,
                                                     const int32_t* __restrict__ bucket_of, int32_t* __restrict__ cursor,
                                                     float4* __restrict__ spts) {
-  __shared__ int ish[kBlk / 64];
-  const int M = score_m(cnt, nseg, ish);
+  const int M = *Mdev;
   const int i = blockIdx.x * kBlk + threadIdx.x;
   if ((int)blockIdx.x * kBlk >= M || i >= M) return;
   const int b = bucket_of[i];
@@ -845,16 +845,27 @@ __global__ void __launch_bounds__(kBlk) k_grid_fill(const int32_t* __restrict__ 
 }
 
 // grid (query blocks, hypotheses): nearest depth point of each transformed
-// model point, flagged when within the radius
-__global__ void __launch_bounds__(kBlk) k_score_nn(const float4* __restrict__ model, const int32_t* __restrict__ cnt,
-                                                   int nseg, const float* __restrict__ hyps, float r2, double inv_s,
+// model point, flagged when within the radius.  kNnLanes adjacent lanes share
+// one query and split its cells (cell c of a ring to lane c % kNnLanes): a
+// query is a chain of dependent bucket and point loads, and one lane per
+// query left ~1 wave per SIMD to hide them.  The lanes' results merge as the
+// lexicographic minimum of (squared distance, index) -- the sequential scan's
+// first minimum -- and after each ring they share the smallest distance so
+// far as the pruning bound.
+#ifndef PCNN_NN_LANES
+#define PCNN_NN_LANES 4
+#endif
+constexpr int kNnLanes = PCNN_NN_LANES;
+__global__ void __launch_bounds__(kBlk) k_score_nn(const float4* __restrict__ model, const int32_t* __restrict__ Mdev,
+                                                   const float* __restrict__ hyps, float r2, double inv_s,
                                                    const int32_t* __restrict__ start, const float4* __restrict__ spts,
                                                    uint8_t* __restrict__ flags, int cap) {
-  __shared__ int ish[kBlk / 64];
-  const int M = score_m(cnt, nseg, ish);
+  constexpr int kQ = kBlk / kNnLanes;  // queries per workgroup
+  const int M = *Mdev;
   const int h = blockIdx.y;
-  const int q = blockIdx.x * kBlk + threadIdx.x;
-  if ((int)blockIdx.x * kBlk >= M || q >= M) return;
+  const int sub = threadIdx.x % kNnLanes;
+  const int q = blockIdx.x * kQ + threadIdx.x / kNnLanes;
+  if ((int)blockIdx.x * kQ >= M || q >= M) return;  // a query's lanes leave together
   const float* P = hyps + (size_t)h * 7;
   const float qn = sqrtf(P[0] * P[0] + P[1] * P[1] + P[2] * P[2] + P[3] * P[3]);
   const Quat qq = {P[0] / qn, P[1] / qn, P[2] / qn, P[3] / qn};
@@ -866,13 +877,14 @@ __global__ void __launch_bounds__(kBlk) k_score_nn(const float4* __restrict__ mo
   z = z + P[6];
   int cx, cy, cz;
   if (!grid_cell(x, y, z, inv_s, cx, cy, cz)) return;
-  float best = r2;  // strict: only squared distances < r2 qualify
+  float best = r2;  // this lane's: strict, only squared distances < r2 qualify
   int bi = -1;
+  float bound = r2;  // the query's smallest distance so far (all lanes), for pruning
   // rings of cells by Chebyshev distance d = 0, 1, 2 around q's cell (cells
   // of edge s = 0.5005 r: every point within r is at most 2 cells away).  A
   // cell is skipped when the squared distance from q to its box, less a 1e-5
-  // relative margin (far above the fp32 distance's rounding), exceeds the best
-  // squared distance so far: no point in it can equal or beat that.  Ring 2 is
+  // relative margin (far above the fp32 distance's rounding), exceeds the
+  // bound: no point in it can equal or beat the query's best.  Ring 2 is
   // skipped whole once (d - 1) s does.
   const double s_cell = 1.0 / inv_s;
   const double gx0 = (double)x - (double)cx * s_cell, gy0 = (double)y - (double)cy * s_cell,
@@ -881,14 +893,16 @@ __global__ void __launch_bounds__(kBlk) k_score_nn(const float4* __restrict__ mo
     return o > 0 ? (double)o * s_cell - g : (o < 0 ? g - (double)(o + 1) * s_cell : 0.0);
   };
   for (int d = 0; d <= 2; d++) {
-    if (d >= 2 && (double)(d - 1) * s_cell * (d - 1) * s_cell * (1.0 - 1e-6) > (double)best) break;
+    if (d >= 2 && (double)(d - 1) * s_cell * (d - 1) * s_cell * (1.0 - 1e-6) > (double)bound) break;
+    int c = 0;
     for (int dz = -d; dz <= d; dz++)
       for (int dy = -d; dy <= d; dy++)
         for (int dx = -d; dx <= d; dx++) {
           if (max(abs(dx), max(abs(dy), abs(dz))) != d) continue;
+          if (c++ % kNnLanes != sub) continue;
           if (d > 0) {
             const double ax = fmax(gap(dx, gx0), 0.0), ay = fmax(gap(dy, gy0), 0.0), az = fmax(gap(dz, gz0), 0.0);
-            if ((ax * ax + ay * ay + az * az) * (1.0 - 1e-5) > (double)best) continue;
+            if ((ax * ax + ay * ay + az * az) * (1.0 - 1e-5) > (double)bound) continue;
           }
           const int b = grid_bucket(cx + dx, cy + dy, cz + dz);
           const int e = start[b + 1];
@@ -903,8 +917,20 @@ __global__ void __launch_bounds__(kBlk) k_score_nn(const float4* __restrict__ mo
             }
           }
         }
+    bound = fminf(bound, best);
+#pragma unroll
+    for (int o = 1; o < kNnLanes; o <<= 1) bound = fminf(bound, __shfl_xor(bound, o, kNnLanes));
   }
-  if (bi >= 0) flags[(size_t)h * cap + bi] = 1;
+#pragma unroll
+  for (int o = 1; o < kNnLanes; o <<= 1) {  // lexicographic minimum of (distance, index) over the query's lanes
+    const float ob = __shfl_xor(best, o, kNnLanes);
+    const int oi = __shfl_xor(bi, o, kNnLanes);
+    if (oi >= 0 && (bi < 0 || ob < best || (ob == best && oi < bi))) {
+      best = ob;
+      bi = oi;
+    }
+  }
+  if (sub == 0 && bi >= 0) flags[(size_t)h * cap + bi] = 1;
 }
 
 // score per hypothesis: one workgroup per hypothesis counts its flags
@@ -1101,7 +1127,7 @@ extern "C" size_t pcnn_icp_score_workspace_size(int J, int H, int W) {
   cv.take<int32_t>((size_t)kGridBuckets);      // bucket counts
   cv.take<int32_t>((size_t)kGridBuckets + 1);  // bucket starts
   cv.take<int32_t>((size_t)kGridBuckets);      // fill cursors
-  cv.take<int32_t>((size_t)kGridScanBlocks);   // bucket-scan workgroup totals
+  cv.take<int32_t>((size_t)kGridScanBlocks + 1);  // bucket-scan workgroup totals, the point count
   cv.take<int32_t>((size_t)HW);                // bucket of each depth point
   cv.take<float4>((size_t)HW);                 // depth points (+ index) by bucket
   return cv.off + 256;
@@ -1121,7 +1147,8 @@ extern "C" int pcnn_icp_score(const float* live, const int32_t* label, int obj, 
   int32_t* bcount = cv.take<int32_t>((size_t)kGridBuckets);
   int32_t* bstart = cv.take<int32_t>((size_t)kGridBuckets + 1);
   int32_t* cursor = cv.take<int32_t>((size_t)kGridBuckets);
-  int32_t* bsum = cv.take<int32_t>((size_t)kGridScanBlocks);
+  int32_t* bsum = cv.take<int32_t>((size_t)kGridScanBlocks + 1);
+  int32_t* Mdev = bsum + kGridScanBlocks;
   int32_t* bucket_of = cv.take<int32_t>((size_t)HW);
   float4* spts = cv.take<float4>((size_t)HW);
   if (workspace_bytes < cv.off) return PCNN_ECAPACITY;
@@ -1134,12 +1161,12 @@ extern "C" int pcnn_icp_score(const float* live, const int32_t* label, int obj, 
   hipLaunchKernelGGL(k_score_count, dim3(nseg), dim3(kBlk), 0, st, live, label, obj, vertmap, HW, nseg, cnt);
   hipLaunchKernelGGL(k_score_scatter, dim3(nseg), dim3(kBlk), 0, st, live, label, obj, vertmap, HW, nseg, cnt, model,
                      dpts);
-  hipLaunchKernelGGL(k_grid_count, dim3(qblocks), dim3(kBlk), 0, st, dpts, cnt, nseg, inv_s, bcount, bucket_of);
+  hipLaunchKernelGGL(k_grid_count, dim3(qblocks), dim3(kBlk), 0, st, dpts, cnt, nseg, inv_s, bcount, bucket_of, Mdev);
   hipLaunchKernelGGL(k_grid_bsum, dim3(kGridScanBlocks), dim3(256), 0, st, bcount, bsum);
   hipLaunchKernelGGL(k_grid_bscan, dim3(kGridScanBlocks), dim3(256), 0, st, bcount, bsum, bstart, cursor);
-  hipLaunchKernelGGL(k_grid_fill, dim3(qblocks), dim3(kBlk), 0, st, cnt, nseg, dpts, bucket_of, cursor, spts);
-  hipLaunchKernelGGL(k_score_nn, dim3(qblocks, J), dim3(kBlk), 0, st, model, cnt, nseg, hyps, radius * radius, inv_s,
-                     bstart, spts, flags, HW);
+  hipLaunchKernelGGL(k_grid_fill, dim3(qblocks), dim3(kBlk), 0, st, Mdev, dpts, bucket_of, cursor, spts);
+  hipLaunchKernelGGL(k_score_nn, dim3(qblocks * kNnLanes, J), dim3(kBlk), 0, st, model, Mdev, hyps, radius * radius,
+                     inv_s, bstart, spts, flags, HW);
   hipLaunchKernelGGL(k_score_count_flags, dim3(J), dim3(1024), 0, st, flags, cnt, nseg, HW, score);
   hipLaunchKernelGGL(k_score_choose, dim3(1), dim3(64), 0, st, score, cnt, nseg, J, choose);
   PCNN_CHECK_LAUNCH();
