@@ -1532,6 +1532,175 @@ __global__ void __launch_bounds__(kNmThreads / G) k_nm(const float* __restrict__
   (void)fres;
 }
 
+// The same search with speculative rounds: kNmSpecW workgroup groups per
+// problem, each of G workgroups evaluating one point of a round.  A round
+// evaluates, in one arrive-and-wait, every point the next step may need:
+// reflection, expansion and both contractions of an iteration (the sequential
+// search then takes them in its own order and counts only those it uses), up
+// to kNmSpecW points of the initial simplex or of a shrink.  optEnergy is a
+// pure function of the point, so the simplex, the evaluation count and the
+// result are those of k_nm bit for bit; an iteration costs one round (plus
+// the shrink's) instead of one to three.
+constexpr int kNmSpecW = 4;
+template <int G, int S>
+__global__ void __launch_bounds__(kNmThreads / G) k_nm_spec(const float* __restrict__ rec,
+                                                            const int32_t* __restrict__ count, int stride,
+                                                            const double* __restrict__ x0_all,
+                                                            const double* __restrict__ lb_all,
+                                                            const double* __restrict__ ub_all, int max_eval,
+                                                            float znear, float zfar, double* __restrict__ x_out,
+                                                            double* __restrict__ f_out, int32_t* __restrict__ nev_out,
+                                                            float* __restrict__ part, uint32_t* __restrict__ bar) {
+  constexpr int n = kNmDim;
+  constexpr int kT = kNmThreads / G;
+  constexpr int kW = 2 * kNmThreads / 64;  // (sum, count) per virtual wave
+  __shared__ double pts[n + 1][n], vals[n + 1], lb[n], ub[n], cen[n], xs[S][n], fs[S];
+  __shared__ int s_fail;
+  const int p = blockIdx.x / (G * S), sp = (blockIdx.x / G) % S, g = blockIdx.x % G, t = threadIdx.x;
+  const float* r = rec + (size_t)p * stride * 6;
+  const int nr = count[p];
+  int rnd = 0;  // rounds so far (the same in every thread of every workgroup of the problem)
+  if (t == 0) s_fail = 0;
+  auto round = [&](int cnt) {  // evaluate xs[0 .. cnt) -> fs[0 .. cnt), every thread
+    __syncthreads();
+    float* slot = part + ((size_t)p * 2 + (rnd & 1)) * S * kW;
+    if (sp < cnt) {
+      float P[7];
+      for (int e = 0; e < n; e++) P[e] = (float)xs[sp][e];  // the host path evaluates float32 points
+      const int vt = g * kT + t;
+      const Quat q = rec_quat(P);
+      float a, c;
+      rec_sums(r, nr, q, P, znear, zfar, vt, a, c);
+      a = pcnn::wave_sum(a);
+      c = pcnn::wave_sum(c);
+      if (pcnn::lane_id() == 0) {
+        slot[sp * kW + 2 * (vt >> 6)] = a;
+        slot[sp * kW + 2 * (vt >> 6) + 1] = c;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __syncthreads();
+    if (t == 0 && !coop_arrive_wait(bar + p, (uint32_t)(rnd + 1) * G * S)) s_fail = 1;
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    if (t < cnt) {  // value k: the 16 wave sums in order, as energy_rec
+      float S_ = 0.f, C_ = 0.f;
+      for (int w = 0; w < kNmThreads / 64; w++) {
+        S_ += slot[t * kW + 2 * w];
+        C_ += slot[t * kW + 2 * w + 1];
+      }
+      fs[t] = (double)(C_ > 0.f ? S_ / C_ : 0.f);  // distance /= c (:2520-2521)
+    }
+    rnd++;
+    __syncthreads();
+  };
+  auto clampq = [&](int e, double v) { return fmin(fmax(v, lb[e]), ub[e]); };
+  if (t == 0) {
+    for (int e = 0; e < n; e++) {
+      lb[e] = lb_all[(size_t)p * n + e];
+      ub[e] = ub_all[(size_t)p * n + e];
+      pts[0][e] = x0_all[(size_t)p * n + e];
+    }
+    for (int i = 0; i < n; i++) {
+      const double x0 = pts[0][i];
+      const double step = fmin(0.25 * (ub[i] - lb[i]), fmin(0.75 * (ub[i] - x0), 0.75 * (x0 - lb[i])));
+      for (int e = 0; e < n; e++) pts[i + 1][e] = pts[0][e] + (e == i ? step : 0.0);
+    }
+  }
+  for (int i0 = 0; i0 <= n; i0 += S) {  // the initial simplex
+    const int cnt = min(S, n + 1 - i0);
+    if (t == 0)
+      for (int k = 0; k < cnt; k++)
+        for (int e = 0; e < n; e++) xs[k][e] = pts[i0 + k][e];
+    round(cnt);
+    if (t == 0)
+      for (int k = 0; k < cnt; k++) vals[i0 + k] = fs[k];
+  }
+  int nev = n + 1;
+  while (nev < max_eval) {  // nev is identical in every thread
+    __syncthreads();
+    if (t == 0) {
+      for (int i = 1; i <= n; i++) {  // stable insertion sort (np.argsort kind="stable")
+        for (int j = i; j > 0 && vals[j] < vals[j - 1]; j--) {
+          const double tv = vals[j];
+          vals[j] = vals[j - 1];
+          vals[j - 1] = tv;
+          for (int e = 0; e < n; e++) {
+            const double tp = pts[j][e];
+            pts[j][e] = pts[j - 1][e];
+            pts[j - 1][e] = tp;
+          }
+        }
+      }
+      for (int e = 0; e < n; e++) {  // np.mean(pts[:-1], axis=0): rows added in order, then / n
+        double sm = pts[0][e];
+        for (int i = 1; i < n; i++) sm = sm + pts[i][e];
+        cen[e] = sm / (double)n;
+      }
+      for (int e = 0; e < n; e++) {
+        const double xr = clampq(e, cen[e] + (cen[e] - pts[n][e]));
+        xs[0][e] = xr;                                            // reflection
+        xs[1][e] = clampq(e, cen[e] + 2.0 * (cen[e] - pts[n][e]));  // expansion
+        xs[2][e] = clampq(e, cen[e] + 0.5 * (xr - cen[e]));        // outside contraction
+        xs[3][e] = clampq(e, cen[e] + 0.5 * (pts[n][e] - cen[e]));  // inside contraction
+      }
+    }
+    round(4);
+    const double fr = fs[0];
+    nev++;
+    const double v0 = vals[0], vn1 = vals[n - 1], vn = vals[n];
+    __syncthreads();  // every thread holds v0 / vn1 / vn before thread 0 updates the simplex
+    if (fr < v0 && nev < max_eval) {
+      nev++;
+      if (t == 0) {
+        const bool take_e = fs[1] < fr;
+        for (int e = 0; e < n; e++) pts[n][e] = take_e ? xs[1][e] : xs[0][e];
+        vals[n] = take_e ? fs[1] : fr;
+      }
+    } else if (fr < vn1) {
+      if (t == 0) {
+        for (int e = 0; e < n; e++) pts[n][e] = xs[0][e];
+        vals[n] = fr;
+      }
+    } else if (nev < max_eval) {
+      nev++;
+      const int kc = fr >= vn ? 3 : 2;
+      const double fc = fs[kc];
+      if (fc < fmin(fr, vn)) {
+        if (t == 0) {
+          for (int e = 0; e < n; e++) pts[n][e] = xs[kc][e];
+          vals[n] = fc;
+        }
+      } else {
+        const int m = min(n, max_eval - nev);
+        for (int i0 = 1; i0 <= m; i0 += S) {  // shrink toward the best
+          const int cnt = min(S, m + 1 - i0);
+          __syncthreads();
+          if (t == 0)
+            for (int k = 0; k < cnt; k++)
+              for (int e = 0; e < n; e++) xs[k][e] = clampq(e, pts[0][e] + 0.5 * (pts[i0 + k][e] - pts[0][e]));
+          round(cnt);
+          if (t == 0)
+            for (int k = 0; k < cnt; k++) {
+              for (int e = 0; e < n; e++) pts[i0 + k][e] = xs[k][e];
+              vals[i0 + k] = fs[k];
+            }
+        }
+        nev += m > 0 ? m : 0;
+      }
+    }
+  }
+  __syncthreads();
+  if (t == 0 && g == 0 && sp == 0) {
+    int b = 0;
+    for (int i = 1; i <= n; i++)
+      if (vals[i] < vals[b]) b = i;  // np.argmin: the first minimum
+    for (int e = 0; e < n; e++) x_out[(size_t)p * n + e] = pts[b][e];
+    f_out[p] = vals[b];
+    nev_out[p] = s_fail ? -1 : nev;  // -1: a cross-workgroup wait gave up (results invalid)
+  }
+}
+
 }  // namespace pcnn_refine
 
 extern "C" size_t pcnn_energy_records_workspace_size(int N, int H, int W) {
@@ -1583,11 +1752,14 @@ extern "C" int pcnn_nelder_mead_energy(const float* records, const int32_t* coun
 // records spread over kNmCoop CUs), launched cooperatively so that the
 // workgroups of a problem are resident together; bit-identical results.
 constexpr int kNmCoop = 8;
+constexpr int kNmSpecMaxN = 32;  // N x 8 x 4 workgroups of 128 threads: 1024 at N = 32
 
+static inline size_t nm_part_bytes(int N) {  // per problem: 2 parities x kNmSpecW points x the wave sums
+  return pcnn::align_up((size_t)N * 2 * kNmSpecW * (2 * kNmThreads / 64) * sizeof(float), 256);
+}
 extern "C" size_t pcnn_nelder_mead_energy_workspace_size(int N) {
   if (N <= 0) return 256;
-  return pcnn::align_up((size_t)N * 2 * (2 * kNmThreads / 64) * sizeof(float), 256) + (size_t)N * sizeof(uint32_t) +
-         256;
+  return nm_part_bytes(N) + (size_t)N * sizeof(uint32_t) + 256;
 }
 
 extern "C" int pcnn_nelder_mead_energy_coop(const float* records, const int32_t* counts, int stride, int N,
@@ -1598,15 +1770,21 @@ extern "C" int pcnn_nelder_mead_energy_coop(const float* records, const int32_t*
   PCNN_REQUIRE(max_eval >= 0 && max_eval <= (1 << 20) && N <= 128);
   if (!workspace || workspace_bytes < pcnn_nelder_mead_energy_workspace_size(N)) return PCNN_ECAPACITY;
   float* part = (float*)workspace;
-  uint32_t* bar =
-      (uint32_t*)((char*)workspace + pcnn::align_up((size_t)N * 2 * (2 * kNmThreads / 64) * sizeof(float), 256));
+  uint32_t* bar = (uint32_t*)((char*)workspace + nm_part_bytes(N));
   hipStream_t st = (hipStream_t)stream;
   if (hipMemsetAsync(bar, 0, (size_t)N * sizeof(uint32_t), st) != hipSuccess) return PCNN_EHIP;
   void* args[] = {(void*)&records, (void*)&counts, (void*)&stride, (void*)&x0, (void*)&lb, (void*)&ub,
                   (void*)&max_eval, (void*)&znear, (void*)&zfar, (void*)&x_out, (void*)&f_out, (void*)&nev_out,
                   (void*)&part, (void*)&bar};
-  if (hipLaunchCooperativeKernel((const void*)k_nm<kNmCoop>, dim3(N * kNmCoop), dim3(kNmThreads / kNmCoop), args, 0,
-                                 st) != hipSuccess) {
+  // speculative rounds while the N x kNmCoop x kNmSpecW workgroups fit the
+  // chip at once; then one evaluation per round; then one workgroup per problem
+  bool done = false;
+  if (N <= kNmSpecMaxN)
+    done = hipLaunchCooperativeKernel((const void*)k_nm_spec<kNmCoop, kNmSpecW>, dim3(N * kNmCoop * kNmSpecW),
+                                      dim3(kNmThreads / kNmCoop), args, 0, st) == hipSuccess;
+  if (!done) (void)hipGetLastError();
+  if (!done && hipLaunchCooperativeKernel((const void*)k_nm<kNmCoop>, dim3(N * kNmCoop), dim3(kNmThreads / kNmCoop),
+                                          args, 0, st) != hipSuccess) {
     (void)hipGetLastError();  // cooperative launch unavailable: the one-workgroup search (same bits)
     hipLaunchKernelGGL(k_nm<1>, dim3(N), dim3(kNmThreads), 0, st, records, counts, stride, x0, lb, ub, max_eval,
                        znear, zfar, x_out, f_out, nev_out, nullptr, nullptr);

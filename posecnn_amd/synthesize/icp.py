@@ -200,7 +200,8 @@ def pose_energy_records(records, counts, poses, pose_prob, depth_range=(0.25, 6.
 
 def nelder_mead_device(records, counts, x0, lb, ub, max_eval, depth_range=(0.25, 6.0), stream=None):
     """The bounded Nelder-Mead of nelder_mead_steps on optEnergy, for N
-    problems at once on the device (eight cooperating workgroups each, no
+    problems at once on the device (eight cooperating workgroups per
+    evaluated point, up to four points of a step per round while N <= 32; no
     host read until the end): x0 / lb / ub (N,7) float64.  Returns (x (N,7), f (N,), nev (N,))
     as device tensors; the same bits as nelder_mead over pose_energy_records."""
     _lib.require_gpu(records, counts)

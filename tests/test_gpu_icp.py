@@ -290,6 +290,36 @@ def test_nelder_mead_device_matches_host(hip, orc, max_eval):
         assert f[0] < e_rec[0]  # the search lowered the energy
 
 
+def test_nelder_mead_device_launch_paths_agree(hip, orc):
+    """The three device searches behind nelder_mead_device -- speculative
+    rounds (N <= 32: reflection, expansion and both contractions evaluated in
+    one cross-workgroup round), one evaluation per round (N <= 128), one
+    workgroup per problem (larger N) -- give the same points, values and
+    evaluation counts on the same problems."""
+    from posecnn_amd.synthesize import icp as R
+    sc = scene(7, perturb_deg=3.0, perturb_t=0.01)
+    lv = _live(sc, orc)[0]
+    lab = t(sc["live"]["label"])
+    pv = t(sc["pred"]["pred_v"])[None].expand(3, -1, -1, -1).contiguous()
+    rec, cnt = R.energy_records(lv, lab, [sc["cls"]] * 3, [0, 0, 0], pv, (0.25, 6.0))
+    x0 = np.array([[1, 0, 0, 0, 0, 0, 0], [0.99, 0.02, -0.01, 0.0, 0.002, -0.001, 0.01],
+                   [0.98, -0.03, 0.02, 0.01, -0.004, 0.003, -0.02]], np.float64)
+    r = np.array([0.1, 0.1, 0.1, 0.1, 0.01, 0.01, 0.1])
+    out = {}
+    for N in (3, 40, 130):
+        sel = torch.arange(N, device=D) % 3
+        recN, cntN = rec.index_select(0, sel).contiguous(), cnt.index_select(0, sel).contiguous()
+        xN = x0[np.arange(N) % 3]
+        x, f, nev = R.nelder_mead_device(recN, cntN, xN, xN - r, xN + r, 30)
+        out[N] = (x.cpu().numpy()[:3], f.cpu().numpy()[:3], nev.cpu().numpy()[:3])
+        del recN
+    for N in (40, 130):
+        np.testing.assert_array_equal(out[N][0], out[3][0])
+        np.testing.assert_array_equal(out[N][1], out[3][1])
+        np.testing.assert_array_equal(out[N][2], out[3][2])
+    assert (out[3][2] == 30).all()
+
+
 def test_solve_icp_device_search_matches_host_driver(hip):
     """solve_icp with the Nelder-Mead searches on the device (the default)
     against the host-driven lock-step searches (nm_device=False): identical
