@@ -76,18 +76,20 @@ def _tie_depths(n, rng):
     return d, z, ok
 
 
-@pytest.mark.parametrize("skip", [1, 2])
-def test_psum_half_ulp_ties(hip, orc, skip):
+@pytest.mark.parametrize("skip,r", [(1, 62), (2, 62), (1, 95)])
+def test_psum_half_ulp_ties(hip, orc, skip, r):
     """A disc of thousands of voters whose vectors point exactly at its centre
     and whose depths make every add in the [2048, 4096) binade a half-ulp tie
     (and cross binades on the way): the parity transducers carry the
     round-half-even choices; the sum, the pose and the box are the serial
-    chain's bits."""
+    chain's bits.  The cases take each of the peak kernel's paths: 6 k
+    voters (8 per thread), 12 k (24 per thread) and 28 k (past 24 per
+    thread: the serial chain, counted in diag[3])."""
     H, W, C = 240, 320, 4
     fr = synth.make_frames(1, H, W, num_classes=C, objects_per_image=1, seed=21)
     fr["extents"] = np.full((C, 3), 0.3, np.float32)  # T ~ 190 px at 1 m: every disc voter passes the box test
     rng = np.random.default_rng(5)
-    cy, cx, r = 120, 160, 62
+    cy, cx = 120, 160
     yy, xx = np.mgrid[0:H, 0:W]
     disc = (yy - cy) ** 2 + (xx - cx) ** 2 <= r * r
     label = np.zeros((1, H, W), np.int32)
@@ -108,3 +110,5 @@ def test_psum_half_ulp_ties(hip, orc, skip):
     fr["gt"] = fr["gt"][:0]
     res, diag = _exact(orc, fr, 0, skip)
     assert res[0].shape[0] == 1 and res[1][0, 6] > 0.9  # one maximum, its distance ~1 m
+    nv = (npx + skip - 1) // skip
+    assert (diag[3] >= 1) == (nv > 24 * 1024), (nv, diag[3])
