@@ -502,11 +502,14 @@ int pcnn_nelder_mead_energy(const float* records, const int32_t* counts, int str
                             const double* lb, const double* ub, int max_eval, float znear, float zfar, double* x_out,
                             double* f_out, int32_t* nev_out, void* stream);
 
-/* pcnn_nelder_mead_energy with 8 cooperating workgroups per problem (the
- * evaluation's records spread over 8 CUs, one arrive-and-wait per evaluation
- * through the workspace), launched cooperatively; the same bits.  N <= 128;
- * the workspace holds the wave sums and one counter per problem (zeroed by the
- * call).  nev_out = -1 marks a cross-workgroup wait that gave up. */
+/* pcnn_nelder_mead_energy with 8 cooperating workgroups per evaluated point
+ * (the evaluation's records spread over 8 CUs, one arrive-and-wait per round
+ * through the workspace), launched cooperatively; the same bits.  N <= 32:
+ * speculative rounds (an iteration's reflection, expansion and both
+ * contractions evaluated together by 4 x 8 workgroups, the search counting
+ * only those it uses); N <= 128: one point per round.  The workspace holds
+ * the wave sums and one counter per problem (zeroed by the call).
+ * nev_out = -1 marks a cross-workgroup wait that gave up. */
 size_t pcnn_nelder_mead_energy_workspace_size(int N);
 int pcnn_nelder_mead_energy_coop(const float* records, const int32_t* counts, int stride, int N, const double* x0,
                                  const double* lb, const double* ub, int max_eval, float znear, float zfar,
