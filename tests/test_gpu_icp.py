@@ -150,6 +150,25 @@ def test_icp_score_grid_ties_and_far_points(hip, orc, radius):
     assert so[0] > 0 and so[2] > 0 and so[3] == 0
 
 
+def test_icp_score_no_object_points(hip, orc):
+    """An object with no pixel in the label map (M = 0, the count every score
+    launch reads from the device): every score 0 and the choice hyps[0]
+    (synthesize.cpp:2333-2334), as the oracle."""
+    from posecnn_amd.synthesize import icp as R
+    H, W, obj = 32, 48, 2
+    rng = np.random.default_rng(3)
+    live = (rng.uniform(-0.05, 0.05, (H, W, 3)) + np.array([0, 0, 0.9])).astype(np.float32)
+    vm = rng.uniform(-0.05, 0.05, (H, W, 3)).astype(np.float32)
+    label = np.ones((H, W), np.int32)  # another class everywhere
+    hyps = np.zeros((5, 7), np.float32)
+    hyps[:, 0] = 1.0
+    hyps[:, 6] = 0.9
+    s, ch = R.icp_score(t(live), t(label), obj, t(vm), t(hyps))
+    so, cho = orc.icp_score(live, label, obj, vm, hyps)
+    np.testing.assert_array_equal(s.cpu().numpy(), so)
+    assert int(ch[0]) == cho == 0 and not so.any()
+
+
 def test_solve_icp_end_to_end(hip, orc):
     """The solveICP flow (synthesize.cpp:2052-2395) with the box ray-caster as
     the renderer: poses_new is the re-centred pose (no Nelder-Mead stage here),
