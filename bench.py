@@ -33,7 +33,7 @@ FP32_MFMA_PEAK_TFS = 157.3   # MI355X f32-input MFMA dense peak (same guide)
 BF16_MFMA_PEAK_TFS = 2500.0  # MI355X bf16 MFMA dense peak (same guide; no sparsity)
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
@@ -55,15 +55,92 @@ def parse():
                    help="dropout masks and ADD row classification on the step's stream (PoseStep side_prep=False)")
     p.add_argument("--no-fp32-leg", "--no-precision-legs", dest="no_legs", action="store_true",
                    help="skip the secondary steps at the other GEMM precisions reported beside the main line")
-    return p.parse_args()
+    p.add_argument("--global-batch", type=int, default=0,
+                   help="global batch the vote's index_size = 128 / global_batch is taken from (default: per-rank "
+                        "batch x ranks; e.g. 64 runs one rank at configs[3]'s per-rank geometry, index_size 2)")
+    p.add_argument("--pipeline", choices=["on", "off"], default="on",
+                   help="full workloads: run the next minibatch's vote + RoI-pool forward + ADD row classification "
+                        "beside the current step's loss and backward (PoseStep(pipeline=True)); two alternating "
+                        "synthetic minibatches")
+    p.add_argument("--prefetch-at", choices=["loss", "bwd", "start"], default="start",
+                   help="with --pipeline on: where the next minibatch's front chain forks off the step")
+    p.add_argument("--no-n1-reference", action="store_true",
+                   help="N > 1: skip rank 0's one-GPU run of its own shard at the same geometry")
+    return p.parse_args(argv)
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def launch_plan(n, argv, env, port):
+    """The N local rank processes `python bench.py --gpus N ...` starts when
+    no launcher set WORLD_SIZE: one process per GPU, rank r on GPU r, the
+    torch.distributed env of torch.distributed.run (127.0.0.1 rendezvous).
+    Returns [(argv, env)] -- built before anything touches a GPU."""
+    plan = []
+    for r in range(n):
+        e = dict(env)
+        e.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0",
+                 MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        plan.append(([sys.executable, os.path.abspath(__file__)] + list(argv), e))
+    return plan
+
+
+def check_world(args, env):
+    """None when this process should run a rank itself, else the number of
+    local ranks to start.  A launcher's WORLD_SIZE must equal --gpus."""
+    ws = env.get("WORLD_SIZE")
+    if ws is None:
+        return args.gpus if args.gpus > 1 else None
+    if int(ws) != args.gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={ws} from the launcher but --gpus {args.gpus}; they must agree")
+    return None
+
+
+def run_local(n, argv):
+    """Start the N rank processes (children, never an exec), wait for all,
+    stop the rest if one fails; exit status = the first failure's."""
+    import signal
+    import socket
+    import subprocess
+    try:
+        import torch  # counting devices does not initialise the GPU on this image
+        have = torch.cuda.device_count()
+    except Exception:  # pragma: no cover
+        have = n
+    if have < n:
+        raise SystemExit(f"bench.py --gpus {n}: only {have} GPU(s) visible")
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    procs = [subprocess.Popen(a, env=e) for a, e in launch_plan(n, argv, os.environ, port)]
+    rc = 0
+    try:
+        live = list(procs)
+        while live:
+            for p in list(live):
+                r = p.poll()
+                if r is None:
+                    continue
+                live.remove(p)
+                if r != 0 and rc == 0:
+                    rc = r
+                    for q in live:  # the exact PIDs this launcher started
+                        q.send_signal(signal.SIGTERM)
+            time.sleep(0.2)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    return rc if rc >= 0 else 128 - rc
+
+
 def main():
     args = parse()
+    n_local = check_world(args, os.environ)
+    if n_local:
+        sys.exit(run_local(n_local, sys.argv[1:]))
     import numpy as np
     import torch
     rank = int(os.environ.get("RANK", 0))
@@ -86,7 +163,10 @@ def main():
     B = args.batch or (8 if full else 1)
     C = 16 if linemod else args.classes
     H, W = 480, 640
-    gB = B * world
+    gB = args.global_batch or B * world
+    if gB < B * world or gB > 128:
+        raise SystemExit(f"--global-batch {gB}: needs per-rank batch x ranks ({B * world}) <= it <= MAX_ROI (128)")
+    pipelined = full and args.pipeline == "on"
     # seed = config index: configs[2] / configs[1] / configs[4]
     seed = 5 if linemod else (3 if full else 2)
     t0 = time.time()
@@ -110,12 +190,34 @@ def main():
                   conv5=torch.randn((B, H // 16, W // 16, 512), generator=g, device=dev))
     pts, sym = synth.linemod_points() if linemod else synth.rescaled_points(C)
     inputs["points"], inputs["symmetry"] = to(pts), to(sym)
+    batches = [inputs]
+    if pipelined:
+        # the second minibatch: a copy of the first in buffers of its own, so
+        # every timed step does exactly the unpipelined line's work (the same
+        # RoI rows); the parity test (tests/test_gpu_pipeline.py) runs the
+        # pipelined step over distinct minibatches
+        batches.append({k: (v.clone() if k not in ("points", "symmetry") else v) for k, v in inputs.items()})
+
+    def runner(st):
+        """One step per call; pipelined: minibatches alternate, each call
+        prefetching the next one's front chain."""
+        if not pipelined:
+            return lambda: st.step(inputs)
+        k = [0]
+
+        def go():
+            i = k[0]
+            k[0] = i + 1
+            st.step(batches[i % 2], batches[(i + 1) % 2])
+        return go
 
     if full:
         step = PoseStep(B, H, W, C, dev, is_train=1, skip_pixels=10, global_batch=gB, batch_base=rank * B,
                         dist=dist, precision=args.precision, pixel_argmax=not args.flat_argmax,
-                        side_prep=not args.prep_on_main, drop_in_reduce=not args.mask_kernel)
-        run = lambda: step.step(inputs)
+                        side_prep=not args.prep_on_main, drop_in_reduce=not args.mask_kernel,
+                        pipeline=pipelined, prefetch_at=args.prefetch_at)
+        run = runner(step)
+        step_run = run
     if linemod:  # + the depth back-projection op, forward and backward (no reference caller; SURVEY 8(d))
         from posecnn_amd.backprojecting_layer import backprojecting_op as bpo
         bp_in = dict(data=torch.randn((B, H, W, CH_BP), generator=g, device=dev),
@@ -124,7 +226,7 @@ def main():
                      grad=torch.randn((B, G_BP, G_BP, G_BP, CH_BP), generator=g, device=dev))
 
         def run():
-            step.step(inputs)
+            step_run()
             with step._t("backproject_fwd"):
                 bpo.backproject(bp_in["data"], bp_in["label"], bp_in["depth"], inputs["meta"], bp_in["label3d"],
                                 G_BP, 1, 0.02)
@@ -212,16 +314,24 @@ def main():
     # reported (both times are in the JSON line).  N > 1: eager, with the RCCL
     # collectives inside the step.
     graph_replay = None
-    if world == 1 and not args.no_graph:
+    # pipelined: one replay = two steps (both minibatches; the prefetch stream
+    # is joined at the replay's end, as capture requires), so K must be even
+    per_replay = 2 if pipelined else 1
+    if world == 1 and not args.no_graph and args.steps % per_replay == 0:
+        def run_replay_body():
+            for _ in range(per_replay):
+                run()
+            if pipelined:
+                torch.cuda.current_stream().wait_stream(step.pre_stream)
         try:
             s = torch.cuda.Stream()
             s.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(s):
-                run()
+                run_replay_body()
             torch.cuda.current_stream().wait_stream(s)
             graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(graph):
-                run()
+                run_replay_body()
             graph.replay()
             torch.cuda.synchronize()
             graph_replay = graph.replay
@@ -229,7 +339,7 @@ def main():
             log(f"graph capture failed ({e}); timing eager launches")
             torch.cuda.synchronize()
 
-    def measure(fn):
+    def measure(fn, per_call=1):
         for _ in range(2):
             fn()
         ev0 = torch.cuda.Event(enable_timing=True)
@@ -237,7 +347,7 @@ def main():
         barrier()
         w0 = time.perf_counter()
         ev0.record()
-        for _ in range(args.steps):
+        for _ in range(args.steps // per_call):
             fn()
         ev1.record()
         barrier()
@@ -251,7 +361,7 @@ def main():
 
     modes = {}
     if graph_replay is not None:
-        modes["hipgraph"] = measure(graph_replay)
+        modes["hipgraph"] = measure(graph_replay, per_replay)
     modes["eager"] = measure(run)
     mode = min(modes, key=modes.get)
     # the same step with the FC GEMMs at the other precisions, eager, reported
@@ -265,8 +375,9 @@ def main():
             if prec == args.precision:
                 continue
             step0 = PoseStep(B, H, W, C, dev, is_train=1, skip_pixels=10, global_batch=gB, batch_base=rank * B,
-                             dist=dist, precision=prec, weights=step.weights)
-            run0 = lambda: step0.step(inputs)
+                             dist=dist, precision=prec, weights=step.weights, pipeline=pipelined,
+                             prefetch_at=args.prefetch_at)
+            run0 = runner(step0)
             run0()
             t0_ = measure(run0)
             legs[key] = {"value": round(gB * args.steps / t0_, 2), "unit": "frames/s",
@@ -275,8 +386,9 @@ def main():
         # the same step without drop6 / drop7 (keep_prob 1, the test-time
         # graph's pose head): what the reference's training dropout costs
         step0 = PoseStep(B, H, W, C, dev, is_train=1, skip_pixels=10, global_batch=gB, batch_base=rank * B,
-                         dist=dist, precision=args.precision, weights=step.weights, keep_prob=1.0)
-        run0 = lambda: step0.step(inputs)
+                         dist=dist, precision=args.precision, weights=step.weights, keep_prob=1.0,
+                         pipeline=pipelined, prefetch_at=args.prefetch_at)
+        run0 = runner(step0)
         run0()
         t0_ = measure(run0)
         legs["no_dropout_step"] = {"value": round(gB * args.steps / t0_, 2), "unit": "frames/s",
@@ -290,11 +402,23 @@ def main():
     # it does not touch): one HIP event pair per step (median and
     # p10 / p90), and the practical HBM peak (device-to-device copy) beside the
     # spec peak of the roofline
-    dist_steps = distribution(graph_replay if mode == "hipgraph" else run, min(max(args.steps, 100), 200))
+    dist_steps = distribution(graph_replay if mode == "hipgraph" else run, min(max(args.steps, 100), 200),
+                              per_replay if mode == "hipgraph" else 1)
     dist_steps["mode"] = mode
     practical = d2d_gbs(dev)
     value = frames / elapsed
-    nrows = int((step.hough if step else hout["o"])["num_rois"][0].item())
+    if step is not None:  # pipelined: both minibatches' sets (the last trained and the prefetched one)
+        rows_sets = [int(st["hough"]["num_rois"][0].item()) for st in step._sets]
+    else:
+        rows_sets = [int(hout["o"]["num_rois"][0].item())]
+    nrows = rows_sets[0]
+    rows_mean = sum(rows_sets) / len(rows_sets)
+    rows_per_rank = [rows_mean]
+    if dist is not None:  # each rank's RoI row count (its shard's work), rank-major
+        t = torch.tensor([rows_mean], device=dev, dtype=torch.float64)
+        lst = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(lst, t)
+        rows_per_rank = [float(x.item()) for x in lst]
 
     # roofline objects
     C3 = 3 * C
@@ -313,9 +437,14 @@ def main():
         # dominant kernel: the slowest fc6 GEMM by its in-step HIP-event time
         # (pass 1b: the launch as it runs in the overlapped step, on its own
         # stream); algorithmic fp32 flops 2 R K N per launch
-        R = max(nrows, 1)
+        R = max(rows_mean, 1)
         K6, U = 49 * 512, 4096
-        gem = {"fc6_fwd": 2.0 * R * K6 * U, "fc6_dx": 2.0 * R * K6 * U, "fc6_dw": 2.0 * R * K6 * U}
+        # fc6 dW: one GEMM over this rank's rows, or, image-sharded, this
+        # rank's K6 / N row block of the global gradient over every rank's
+        # rows (exchange.GradShard) -- algorithmic flops count live rows only
+        dw = 2.0 * R * K6 * U if world == 1 else 2.0 * (K6 / world) * U * sum(rows_per_rank)
+        gem = {"fc6_fwd": 2.0 * R * K6 * U, "fc6_dx": 2.0 * R * K6 * U, "fc6_dw": dw}
+        gem = {k: v for k, v in gem.items() if k in gemm_in_step}
         dom = max(gem, key=lambda k: gemm_in_step.get(k, 0.0))
         tf = gem[dom] / (gemm_in_step[dom] / 1e3) / 1e12
         fam, peak, form = {2: ("k_gemm_x6", BF16_MFMA_PEAK_TFS / 6, "3-way split-bf16 x6 MFMA 32x32x16"),
@@ -323,7 +452,9 @@ def main():
                            0: ("k_gemm_f32", FP32_MFMA_PEAK_TFS, "fp32 MFMA 32x32x2")}[args.precision]
         # the split kernels' peak: the bf16 dense MFMA rate over the MFMA passes per fp32 product;
         # fc6_fwd runs split-K (+ k_gemm_reduce, inside its time)
-        kname = f"{fam} ({dom}{' + k_gemm_reduce' if dom == 'fc6_fwd' else ''}, {form}, R={R})"
+        kname = f"{fam} ({dom}{' + k_gemm_reduce' if dom == 'fc6_fwd' else ''}, {form}, R={R:g}" + \
+            (f", rank's K6/{world} row block over {sum(rows_per_rank):g} rows of {world} ranks)" if world > 1 and
+             dom == "fc6_dw" else ")")
         roof = {"bound": "mfma", "achieved": round(tf, 2), "peak": round(peak, 1), "unit": "TFLOP/s",
                 "frac": round(tf / peak, 4), "traffic": None, "kernel": kname, "flops_per_launch": gem[dom],
                 "us_per_launch_in_step": round(gemm_in_step[dom] * 1e3, 1),
@@ -334,7 +465,7 @@ def main():
     # HBM traffic of the same launches from the committed rocprofv3 FETCH_SIZE /
     # WRITE_SIZE passes (scripts/gpu.sh pmc -> scripts/pmc_traffic.py)
     pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(pmc_path):
+    if os.path.exists(pmc_path) and world == 1 and gB == B:  # the committed passes' shapes
         try:
             pmc = json.load(open(pmc_path))
             wl = pmc.get(args.workload, {})
@@ -361,6 +492,35 @@ def main():
         except Exception as e:  # pragma: no cover - a stale file must not break the bench
             log(f"pmc traffic unavailable: {e}")
 
+    # N > 1: rank 0 also times its own shard alone on its GPU at the same
+    # geometry (same frames, same index_size, no collectives), the per-GPU
+    # reference a like-for-like scaling ratio divides by; the other ranks wait
+    n1_ref = None
+    if dist is not None and full and not args.no_n1_reference:
+        if rank == 0:
+            step1 = PoseStep(B, H, W, C, dev, is_train=1, skip_pixels=10, global_batch=gB, batch_base=rank * B,
+                             dist=None, precision=args.precision, weights=step.weights, pipeline=pipelined,
+                             prefetch_at=args.prefetch_at)
+            run1 = runner(step1)
+            for _ in range(max(2, args.warmup)):
+                run1()
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            w0 = time.perf_counter()
+            e0.record()
+            for _ in range(args.steps):
+                run1()
+            e1.record()
+            torch.cuda.synchronize()
+            el1 = max(time.perf_counter() - w0, e0.elapsed_time(e1) / 1e3)
+            n1_ref = {"value": round(B * args.steps / el1, 2), "unit": "frames/s",
+                      "ms_per_step": round(el1 / args.steps * 1e3, 4), "timing": "eager", "n_gpus": 1,
+                      "per_rank_batch": B, "index_size": 128 // gB,
+                      "note": "rank 0's shard on its GPU alone at this line's geometry (no collectives, full "
+                              "local fc weight gradients): the one-GPU point of a fixed per-frame-work curve"}
+            del step1
+        dist.barrier()
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not linemod:
         cpu = cpu_baseline(fr, full, args.cpu_seconds)
@@ -368,12 +528,15 @@ def main():
     if rank == 0:
         if True:
             log(f"timed mode: {mode}; per-op ms/step (eager breakdown pass): " + json.dumps({k: round(v, 4) for k, v in sorted(ops.items(), key=lambda x: -x[1])}))
-            log(f"RoI rows per step (rank 0): {nrows}")
+            log(f"RoI rows per step (rank 0): {rows_sets}; per rank: {rows_per_rank}")
         out = {
             "metric": "frames/sec 640x480x21-class Hough-vote+RoI+ADD-loss, 1/2/4/8 MI355X",
             "value": round(value, 2),
             "unit": "frames/s",
             "n_gpus": world,
+            "ranks": {"world_size": dist.get_world_size() if dist is not None else 1,
+                      "backend": dist.get_backend() if dist is not None else None,
+                      "roi_rows_per_rank": rows_per_rank},
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
@@ -397,6 +560,13 @@ def main():
                              "configs[1]: hough_voting_gpu(test) + roi_pool x2 forward"),
                 "global_batch": gB, "per_rank_batch": B, "height": H, "width": W, "num_classes": C,
                 "skip_pixels": 10, "index_size": 128 // gB, "roi_rows_rank0": nrows,
+                "pipelined": pipelined, **({"prefetch_at": args.prefetch_at,
+                                            "minibatches": "two alternating minibatches (the second a copy of "
+                                                           "the first in its own buffers: the same work per "
+                                                           "step); the next one's vote + RoI-pool forward + ADD "
+                                                           "row classes run on a prefetch stream beside the "
+                                                           "current step; K timed steps hold K votes",
+                                            "roi_rows_minibatches_rank0": rows_sets} if pipelined else {}),
                 "fc_gemm": {2: "3-way split-bf16 x6 MFMA (fp32-faithful)", 1: "split-bf16x3 MFMA, fp32 accumulate",
                             0: "fp32 MFMA"}[args.precision],
                 "parallelism": (f"image-shard x{world} (RCCL: row-count/loss all-reduce, fc weight-gradient "
@@ -411,6 +581,7 @@ def main():
             "step_ms_distribution": dist_steps,
             "hbm_practical_peak": practical,
             "cpu_baseline": cpu,
+            "n1_same_geometry": n1_ref,
             **legs,
         }
         print(json.dumps(out), flush=True)
@@ -418,18 +589,20 @@ def main():
         dist.destroy_process_group()
 
 
-def distribution(fn, n):
-    """ms per step of n single steps, each between its own HIP event pair on
-    the current stream (the step joins its side stream before it ends)."""
+def distribution(fn, n, per_call=1):
+    """ms per step of n single steps (calls of per_call steps each, divided
+    back), each between its own HIP event pair on the current stream (the step
+    joins its side stream before it ends)."""
     import numpy as np
     import torch
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n)]
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(max(1, n // per_call))]
     for a, b in evs:
         a.record()
         fn()
         b.record()
     torch.cuda.synchronize()
-    t = np.array([a.elapsed_time(b) for a, b in evs])
+    t = np.array([a.elapsed_time(b) for a, b in evs]) / per_call
     return {"median": round(float(np.median(t)), 4), "p10": round(float(np.percentile(t, 10)), 4),
             "p90": round(float(np.percentile(t, 90)), 4), "n": n}
 

@@ -508,13 +508,25 @@ int pcnn_nelder_mead_energy(const float* records, const int32_t* counts, int str
  * speculative rounds (an iteration's reflection, expansion and both
  * contractions evaluated together by 4 x 8 workgroups, the search counting
  * only those it uses); N <= 128: one point per round.  The workspace holds
- * the wave sums and one counter per problem (zeroed by the call).
- * nev_out = -1 marks a cross-workgroup wait that gave up. */
+ * the wave sums, one arrival counter and one failure flag per problem
+ * (zeroed by the call).  nev_out = -1 marks a problem one of whose
+ * cross-workgroup waits gave up: every workgroup of it stops at its next
+ * barrier and its x / f are invalid.  max_eval >= 8 (the initial simplex;
+ * NLopt's maxeval, which poseWithOpt / refineWithOpt set, counts it too).
+ * The _path form pins the kernel (force_path 1 speculative, 2 cooperative,
+ * 3 one workgroup; 0 the first that launches) and reports the one that ran
+ * in *path_out (host int, may be NULL); PCNN_EHIP if a forced one cannot
+ * launch. */
 size_t pcnn_nelder_mead_energy_workspace_size(int N);
 int pcnn_nelder_mead_energy_coop(const float* records, const int32_t* counts, int stride, int N, const double* x0,
                                  const double* lb, const double* ub, int max_eval, float znear, float zfar,
                                  double* x_out, double* f_out, int32_t* nev_out, void* workspace,
                                  size_t workspace_bytes, void* stream);
+int pcnn_nelder_mead_energy_coop_path(const float* records, const int32_t* counts, int stride, int N,
+                                      const double* x0, const double* lb, const double* ub, int max_eval,
+                                      float znear, float zfar, double* x_out, double* f_out, int32_t* nev_out,
+                                      void* workspace, size_t workspace_bytes, int force_path, int32_t* path_out,
+                                      void* stream);
 
 /* pcnn_icp_score: the SegICP hypothesis score of solveICP (synthesize.cpp:2288-2330):
  *   over the object's pixels with depth > 0 and a finite vertmap, each model

@@ -128,6 +128,9 @@ _SIGS = {
     "pcnn_nelder_mead_energy_coop": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int,
                                              c_float, c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t,
                                              c_void_p]),
+    "pcnn_nelder_mead_energy_coop_path": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p,
+                                                  c_int, c_float, c_float, c_void_p, c_void_p, c_void_p, c_void_p,
+                                                  c_size_t, c_int, c_void_p, c_void_p]),
     "pcnn_pose_energy_batch": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_float,
                                        c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t,
                                        c_void_p]),

@@ -376,6 +376,9 @@ __host__ __device__ inline int place_queue_cap(int C, int skip) {
   const int q = kPixPerBlk / skip + C + 1;
   return q < kPixPerBlk ? q : kPixPerBlk;
 }
+// k_label_place's static LDS (its kMaxClasses / kCompactThreads tables and
+// scalars), an upper bound checked against the kernel in hough_compact.hip
+constexpr size_t kPlaceStaticLds = (7 * kMaxClasses + 2 * kCompactThreads + 16) * sizeof(int);
 __host__ __device__ inline size_t place_lds_bytes(int C, int skip) {
   return ((size_t)(kPixPerBlk / 64) * C + 3 * (size_t)place_queue_cap(C, skip)) * sizeof(int);
 }

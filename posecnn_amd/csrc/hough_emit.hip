@@ -113,7 +113,17 @@ static int hough_voting_impl(const int32_t* label, const float* prob, int32_t* l
   {
     const double c = (double)inlier_thr, co = c - kConeEps, ci = c + kConeEps;
     const double so = std::sqrt(std::max(0.0, 1.0 - co * co)), si = std::sqrt(std::max(0.0, 1.0 - ci * ci));
-    hipLaunchKernelGGL(k_label_place, dim3(ws.nblk, B), dim3(kCompactThreads), place_lds_bytes(C, skip_pixels), st,
+    // the placement's dynamic LDS grows with C and 1 / skip (57 KiB at C = 256,
+    // skip = 1): above the 64 KiB default window (with the kernel's ~9 KiB of
+    // static LDS) the launch needs the attribute raised, up to the CU's
+    // 160 KiB (such launches used to fail)
+    const size_t place_lds = place_lds_bytes(C, skip_pixels);
+    if (place_lds + kPlaceStaticLds > 160 * 1024) return PCNN_ECAPACITY;
+    if (place_lds + kPlaceStaticLds > 48 * 1024 &&
+        hipFuncSetAttribute((const void*)k_label_place, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)place_lds) != hipSuccess)
+      return PCNN_EHIP;
+    hipLaunchKernelGGL(k_label_place, dim3(ws.nblk, B), dim3(kCompactThreads), place_lds, st,
                        label, vertex, vch, extents,
                        meta, num_meta, H, W, C, skip_pixels, label_thr, index_size, nms ? 1 : 0, inlier_thr, so, si,
                        ws);

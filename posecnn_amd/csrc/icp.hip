@@ -1358,15 +1358,31 @@ __global__ void __launch_bounds__(kNmThreads) k_energy_rec(const float* __restri
 // Arrive-and-wait of the G workgroups of one problem on its counter (thread 0
 // of each): release the workgroup's partial sums, wait until every workgroup
 // of the problem has arrived for this evaluation.  Bounded: a wait that never
-// completes (not expected: the launch is cooperative) gives up and reports.
-__device__ __forceinline__ bool coop_arrive_wait(uint32_t* bar, uint32_t target) {
+// completes (not expected: the launch is cooperative) gives up and raises the
+// problem's failure flag; a workgroup waiting while the flag is up gives up at
+// once.  A workgroup whose wait fails leaves the search (the caller checks
+// s_fail after its barrier), so every workgroup of the problem stops at its
+// next barrier instead of running on with sums that were never written, and
+// the problem reports nev = -1.
+__device__ __forceinline__ bool coop_arrive_wait(uint32_t* bar, uint32_t target, uint32_t* fail) {
   __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
   uint32_t cur = __hip_atomic_load(bar, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
   for (int it = 0; cur < target && it < (1 << 24); it++) {
+    if (__hip_atomic_load(fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return false;
     __builtin_amdgcn_s_sleep(2);
     cur = __hip_atomic_load(bar, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
   }
-  return cur >= target;
+  if (cur >= target) return true;
+  __hip_atomic_fetch_or(fail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return false;
+}
+
+// nev reported by workgroup 0 of problem p: -1 when a cross-workgroup wait of
+// the problem gave up (its own or another workgroup's: results invalid)
+__device__ __forceinline__ int nm_report(int nev, int s_fail, const uint32_t* fail, int p) {
+  if (s_fail) return -1;
+  if (fail && __hip_atomic_load(fail + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return -1;
+  return nev;
 }
 
 // G workgroups per problem (G = 1: one 1024-thread workgroup; G > 1: the
@@ -1385,7 +1401,8 @@ __global__ void __launch_bounds__(kNmThreads / G) k_nm(const float* __restrict__
                                                        const double* __restrict__ ub_all, int max_eval, float znear,
                                                        float zfar, double* __restrict__ x_out,
                                                        double* __restrict__ f_out, int32_t* __restrict__ nev_out,
-                                                       float* __restrict__ part, uint32_t* __restrict__ bar) {
+                                                       float* __restrict__ part, uint32_t* __restrict__ bar,
+                                                       uint32_t* __restrict__ fail) {
   constexpr int n = kNmDim;
   constexpr int kT = kNmThreads / G;
   __shared__ double pts[n + 1][n], vals[n + 1], lb[n], ub[n], xq[n], xr[n], cen[n];
@@ -1418,7 +1435,7 @@ __global__ void __launch_bounds__(kNmThreads / G) k_nm(const float* __restrict__
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
       __syncthreads();
-      if (t == 0 && !coop_arrive_wait(bar + p, (uint32_t)(ne + 1) * G)) s_fail = 1;
+      if (t == 0 && !coop_arrive_wait(bar + p, (uint32_t)(ne + 1) * G, fail + p)) s_fail = 1;
       __syncthreads();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       float S = 0.f, Cn = 0.f;
@@ -1444,14 +1461,16 @@ __global__ void __launch_bounds__(kNmThreads / G) k_nm(const float* __restrict__
       for (int e = 0; e < n; e++) pts[i + 1][e] = pts[0][e] + (e == i ? step : 0.0);
     }
   }
-  for (int i = 0; i <= n; i++) {  // the initial simplex (one batch on the host: the same values)
+  for (int i = 0; i <= n && !s_fail; i++) {  // the initial simplex (one batch on the host: the same values)
     if (t == 0)
       for (int e = 0; e < n; e++) xq[e] = pts[i][e];
     const double v = eval();
     if (t == 0) vals[i] = v;
   }
   int nev = n + 1;
-  while (nev < max_eval) {  // nev is identical in every thread
+  // nev and s_fail (read after each evaluation's barrier) are identical in
+  // every thread; a failed wait ends the search in every workgroup
+  while (nev < max_eval && !s_fail) {
     if (t == 0) {
       for (int i = 1; i <= n; i++) {  // stable insertion sort (np.argsort kind="stable")
         for (int j = i; j > 0 && vals[j] < vals[j - 1]; j--) {
@@ -1507,7 +1526,7 @@ __global__ void __launch_bounds__(kNmThreads / G) k_nm(const float* __restrict__
         }
       } else {
         const int m = min(n, max_eval - nev);
-        for (int i = 1; i <= m; i++) {  // shrink toward the best (one batch on the host)
+        for (int i = 1; i <= m && !s_fail; i++) {  // shrink toward the best (one batch on the host)
           if (t == 0)
             for (int e = 0; e < n; e++) xq[e] = clampq(e, pts[0][e] + 0.5 * (pts[i][e] - pts[0][e]));
           const double fv = eval();
@@ -1527,7 +1546,7 @@ __global__ void __launch_bounds__(kNmThreads / G) k_nm(const float* __restrict__
       if (vals[i] < vals[b]) b = i;  // np.argmin: the first minimum
     for (int e = 0; e < n; e++) x_out[(size_t)p * n + e] = pts[b][e];
     f_out[p] = vals[b];
-    nev_out[p] = s_fail ? -1 : nev;  // -1: a cross-workgroup wait gave up (results invalid)
+    nev_out[p] = nm_report(nev, s_fail, fail, p);
   }
   (void)fres;
 }
@@ -1550,7 +1569,8 @@ __global__ void __launch_bounds__(kNmThreads / G) k_nm_spec(const float* __restr
                                                             const double* __restrict__ ub_all, int max_eval,
                                                             float znear, float zfar, double* __restrict__ x_out,
                                                             double* __restrict__ f_out, int32_t* __restrict__ nev_out,
-                                                            float* __restrict__ part, uint32_t* __restrict__ bar) {
+                                                            float* __restrict__ part, uint32_t* __restrict__ bar,
+                                                            uint32_t* __restrict__ fail) {
   constexpr int n = kNmDim;
   constexpr int kT = kNmThreads / G;
   constexpr int kW = 2 * kNmThreads / 64;  // (sum, count) per virtual wave
@@ -1580,7 +1600,7 @@ __global__ void __launch_bounds__(kNmThreads / G) k_nm_spec(const float* __restr
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     __syncthreads();
-    if (t == 0 && !coop_arrive_wait(bar + p, (uint32_t)(rnd + 1) * G * S)) s_fail = 1;
+    if (t == 0 && !coop_arrive_wait(bar + p, (uint32_t)(rnd + 1) * G * S, fail + p)) s_fail = 1;
     __syncthreads();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     if (t < cnt) {  // value k: the 16 wave sums in order, as energy_rec
@@ -1607,7 +1627,7 @@ __global__ void __launch_bounds__(kNmThreads / G) k_nm_spec(const float* __restr
       for (int e = 0; e < n; e++) pts[i + 1][e] = pts[0][e] + (e == i ? step : 0.0);
     }
   }
-  for (int i0 = 0; i0 <= n; i0 += S) {  // the initial simplex
+  for (int i0 = 0; i0 <= n && !s_fail; i0 += S) {  // the initial simplex
     const int cnt = min(S, n + 1 - i0);
     if (t == 0)
       for (int k = 0; k < cnt; k++)
@@ -1617,7 +1637,7 @@ __global__ void __launch_bounds__(kNmThreads / G) k_nm_spec(const float* __restr
       for (int k = 0; k < cnt; k++) vals[i0 + k] = fs[k];
   }
   int nev = n + 1;
-  while (nev < max_eval) {  // nev is identical in every thread
+  while (nev < max_eval && !s_fail) {  // nev and s_fail are identical in every thread (a failed wait ends all)
     __syncthreads();
     if (t == 0) {
       for (int i = 1; i <= n; i++) {  // stable insertion sort (np.argsort kind="stable")
@@ -1673,7 +1693,7 @@ __global__ void __launch_bounds__(kNmThreads / G) k_nm_spec(const float* __restr
         }
       } else {
         const int m = min(n, max_eval - nev);
-        for (int i0 = 1; i0 <= m; i0 += S) {  // shrink toward the best
+        for (int i0 = 1; i0 <= m && !s_fail; i0 += S) {  // shrink toward the best
           const int cnt = min(S, m + 1 - i0);
           __syncthreads();
           if (t == 0)
@@ -1697,7 +1717,7 @@ __global__ void __launch_bounds__(kNmThreads / G) k_nm_spec(const float* __restr
       if (vals[i] < vals[b]) b = i;  // np.argmin: the first minimum
     for (int e = 0; e < n; e++) x_out[(size_t)p * n + e] = pts[b][e];
     f_out[p] = vals[b];
-    nev_out[p] = s_fail ? -1 : nev;  // -1: a cross-workgroup wait gave up (results invalid)
+    nev_out[p] = nm_report(nev, s_fail, fail, p);
   }
 }
 
@@ -1741,9 +1761,11 @@ extern "C" int pcnn_nelder_mead_energy(const float* records, const int32_t* coun
                                        float znear, float zfar, double* x_out, double* f_out, int32_t* nev_out,
                                        void* stream) {
   PCNN_REQUIRE(records && counts && x0 && lb && ub && x_out && f_out && nev_out && N > 0 && stride > 0);
-  PCNN_REQUIRE(max_eval >= 0 && max_eval <= (1 << 20));
+  // at least the initial simplex: NLopt's maxeval also counts it, and a
+  // budget below n + 1 is refused rather than overrun
+  PCNN_REQUIRE(max_eval >= pcnn_refine::kNmDim + 1 && max_eval <= (1 << 20));
   hipLaunchKernelGGL(k_nm<1>, dim3(N), dim3(kNmThreads), 0, (hipStream_t)stream, records, counts, stride, x0, lb,
-                     ub, max_eval, znear, zfar, x_out, f_out, nev_out, nullptr, nullptr);
+                     ub, max_eval, znear, zfar, x_out, f_out, nev_out, nullptr, nullptr, nullptr);
   PCNN_CHECK_LAUNCH();
   return PCNN_OK;
 }
@@ -1759,36 +1781,56 @@ static inline size_t nm_part_bytes(int N) {  // per problem: 2 parities x kNmSpe
 }
 extern "C" size_t pcnn_nelder_mead_energy_workspace_size(int N) {
   if (N <= 0) return 256;
-  return nm_part_bytes(N) + (size_t)N * sizeof(uint32_t) + 256;
+  return nm_part_bytes(N) + 2 * (size_t)N * sizeof(uint32_t) + 256;  // + the arrival counters and failure flags
+}
+
+extern "C" int pcnn_nelder_mead_energy_coop_path(const float* records, const int32_t* counts, int stride, int N,
+                                                 const double* x0, const double* lb, const double* ub, int max_eval,
+                                                 float znear, float zfar, double* x_out, double* f_out,
+                                                 int32_t* nev_out, void* workspace, size_t workspace_bytes,
+                                                 int force_path, int32_t* path_out, void* stream) {
+  PCNN_REQUIRE(records && counts && x0 && lb && ub && x_out && f_out && nev_out && N > 0 && stride > 0);
+  PCNN_REQUIRE(max_eval >= pcnn_refine::kNmDim + 1 && max_eval <= (1 << 20) && N <= 128);
+  PCNN_REQUIRE(force_path >= 0 && force_path <= 3);
+  if (!workspace || workspace_bytes < pcnn_nelder_mead_energy_workspace_size(N)) return PCNN_ECAPACITY;
+  float* part = (float*)workspace;
+  uint32_t* bar = (uint32_t*)((char*)workspace + nm_part_bytes(N));
+  uint32_t* fail = bar + N;
+  hipStream_t st = (hipStream_t)stream;
+  if (hipMemsetAsync(bar, 0, 2 * (size_t)N * sizeof(uint32_t), st) != hipSuccess) return PCNN_EHIP;
+  void* args[] = {(void*)&records, (void*)&counts, (void*)&stride, (void*)&x0, (void*)&lb, (void*)&ub,
+                  (void*)&max_eval, (void*)&znear, (void*)&zfar, (void*)&x_out, (void*)&f_out, (void*)&nev_out,
+                  (void*)&part, (void*)&bar, (void*)&fail};
+  // speculative rounds while the N x kNmCoop x kNmSpecW workgroups fit the
+  // chip at once (path 1); then one evaluation per round (2); then one
+  // workgroup per problem (3).  force_path pins one (0: the first that
+  // launches); path_out (host int, may be null) reports the one that ran.
+  int path = 0;
+  if ((force_path == 0 || force_path == 1) && N <= kNmSpecMaxN &&
+      hipLaunchCooperativeKernel((const void*)k_nm_spec<kNmCoop, kNmSpecW>, dim3(N * kNmCoop * kNmSpecW),
+                                 dim3(kNmThreads / kNmCoop), args, 0, st) == hipSuccess)
+    path = 1;
+  if (!path) (void)hipGetLastError();
+  if (!path && (force_path == 0 || force_path == 2) &&
+      hipLaunchCooperativeKernel((const void*)k_nm<kNmCoop>, dim3(N * kNmCoop), dim3(kNmThreads / kNmCoop), args, 0,
+                                 st) == hipSuccess)
+    path = 2;
+  if (!path) (void)hipGetLastError();
+  if (!path && (force_path == 0 || force_path == 3)) {  // the one-workgroup search (same bits)
+    hipLaunchKernelGGL(k_nm<1>, dim3(N), dim3(kNmThreads), 0, st, records, counts, stride, x0, lb, ub, max_eval,
+                       znear, zfar, x_out, f_out, nev_out, nullptr, nullptr, nullptr);
+    path = 3;
+  }
+  if (path_out) *path_out = path;
+  if (!path) return PCNN_EHIP;  // the forced path could not launch
+  PCNN_CHECK_LAUNCH();
+  return PCNN_OK;
 }
 
 extern "C" int pcnn_nelder_mead_energy_coop(const float* records, const int32_t* counts, int stride, int N,
                                             const double* x0, const double* lb, const double* ub, int max_eval,
                                             float znear, float zfar, double* x_out, double* f_out, int32_t* nev_out,
                                             void* workspace, size_t workspace_bytes, void* stream) {
-  PCNN_REQUIRE(records && counts && x0 && lb && ub && x_out && f_out && nev_out && N > 0 && stride > 0);
-  PCNN_REQUIRE(max_eval >= 0 && max_eval <= (1 << 20) && N <= 128);
-  if (!workspace || workspace_bytes < pcnn_nelder_mead_energy_workspace_size(N)) return PCNN_ECAPACITY;
-  float* part = (float*)workspace;
-  uint32_t* bar = (uint32_t*)((char*)workspace + nm_part_bytes(N));
-  hipStream_t st = (hipStream_t)stream;
-  if (hipMemsetAsync(bar, 0, (size_t)N * sizeof(uint32_t), st) != hipSuccess) return PCNN_EHIP;
-  void* args[] = {(void*)&records, (void*)&counts, (void*)&stride, (void*)&x0, (void*)&lb, (void*)&ub,
-                  (void*)&max_eval, (void*)&znear, (void*)&zfar, (void*)&x_out, (void*)&f_out, (void*)&nev_out,
-                  (void*)&part, (void*)&bar};
-  // speculative rounds while the N x kNmCoop x kNmSpecW workgroups fit the
-  // chip at once; then one evaluation per round; then one workgroup per problem
-  bool done = false;
-  if (N <= kNmSpecMaxN)
-    done = hipLaunchCooperativeKernel((const void*)k_nm_spec<kNmCoop, kNmSpecW>, dim3(N * kNmCoop * kNmSpecW),
-                                      dim3(kNmThreads / kNmCoop), args, 0, st) == hipSuccess;
-  if (!done) (void)hipGetLastError();
-  if (!done && hipLaunchCooperativeKernel((const void*)k_nm<kNmCoop>, dim3(N * kNmCoop), dim3(kNmThreads / kNmCoop),
-                                          args, 0, st) != hipSuccess) {
-    (void)hipGetLastError();  // cooperative launch unavailable: the one-workgroup search (same bits)
-    hipLaunchKernelGGL(k_nm<1>, dim3(N), dim3(kNmThreads), 0, st, records, counts, stride, x0, lb, ub, max_eval,
-                       znear, zfar, x_out, f_out, nev_out, nullptr, nullptr);
-  }
-  PCNN_CHECK_LAUNCH();
-  return PCNN_OK;
+  return pcnn_nelder_mead_energy_coop_path(records, counts, stride, N, x0, lb, ub, max_eval, znear, zfar, x_out, f_out,
+                                           nev_out, workspace, workspace_bytes, 0, nullptr, stream);
 }

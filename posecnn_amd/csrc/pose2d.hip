@@ -1888,7 +1888,9 @@ extern "C" int pcnn_pose3d(const int32_t* label, const uint16_t* depth, const fl
                            void* workspace, size_t workspace_bytes, void* stream) {
   PCNN_REQUIRE(label && depth && vertmap && extents && poses_out && hyps_out && hyp_px && inl_out && final_out &&
                energy_out);
-  PCNN_REQUIRE(H > 0 && W > 0 && C > 1 && C <= 64 && n_hyp > 0 && n_hyp <= kMaxHyp && max_iter > 0 && nm_evals > 0);
+  // nm_evals >= 7: at least the six-dimensional search's initial simplex (NLopt's
+  // maxeval counts it; a smaller budget is refused rather than overrun)
+  PCNN_REQUIRE(H > 0 && W > 0 && C > 1 && C <= 64 && n_hyp > 0 && n_hyp <= kMaxHyp && max_iter > 0 && nm_evals >= 7);
   PCNN_REQUIRE((long)H * W < (1l << 28));
   const Layout3 l = layout3(H, W, C, n_hyp);
   if (!workspace || workspace_bytes < l.total) return PCNN_ECAPACITY;

@@ -24,6 +24,8 @@ RoIs/poses"): step() starts the gather right after the vote, it overlaps the
 rest of the step and is joined at the step's end (`self.detections`);
 `gather_detections()` runs the same exchange on its own.
 """
+import contextlib
+
 import torch
 
 from . import _lib
@@ -34,6 +36,7 @@ from .average_distance_loss import average_distance_loss_op as adl
 from .exchange import GradShard, RoiExchange
 
 CAP = hv.CAPACITY
+_nullctx = contextlib.nullcontext
 
 
 class PoseStep:
@@ -41,7 +44,7 @@ class PoseStep:
                  is_train=1, skip_pixels=10, vote_threshold=-1.0, vote_percentage=0.02, margin=0.01,
                  global_batch=None, batch_base=0, weights=None, dist=None, backward=True, precision=2,
                  overlap_weight_grads=True, pixel_argmax=True, keep_prob=None, drop_seed=0x5EED, side_prep=True,
-                 drop_in_reduce=True):
+                 drop_in_reduce=True, pipeline=False, prefetch_at="loss"):
         self.B, self.H, self.W, self.C = B, H, W, num_classes
         self.dev = device
         self.is_train, self.skip, self.vthr, self.vper, self.margin = is_train, skip_pixels, vote_threshold, \
@@ -62,24 +65,40 @@ class PoseStep:
         f32 = dict(dtype=torch.float32, device=device)
         i32 = dict(dtype=torch.int32, device=device)
         K6 = 49 * channels
-        self.hough = dict(box=torch.zeros((CAP, 7), **f32), pose=torch.zeros((CAP, 7), **f32),
-                          target=torch.zeros((CAP, D), **f32), weight=torch.zeros((CAP, D), **f32),
-                          domain=torch.zeros((CAP,), **i32), num_rois=torch.zeros((2,), **i32))
-        self.pool = torch.zeros((CAP, 7, 7, channels), **f32)  # pool5 + pool4 (vgg16_convs.py:184)
         # argmax as uint16 pixel indices (half the bytes of the flat int32 form,
         # written by the pool pair and re-read by both pool backwards) when
         # both maps have fewer than 0xFFFF pixels
         px = pixel_argmax and max(self.h4 * self.w4, self.h5 * self.w5) < 0xFFFF
         adt = dict(dtype=torch.int16 if px else torch.int32, device=device)
-        self.arg5 = torch.zeros((CAP, 7, 7, channels), **adt)
-        self.arg4 = torch.zeros((CAP, 7, 7, channels), **adt)
+
+        def minibatch_set():
+            """The per-minibatch buffers: the Hough outputs, pool5 + pool4
+            (vgg16_convs.py:184), both argmax maps, the ADD row classes."""
+            return dict(hough=dict(box=torch.zeros((CAP, 7), **f32), pose=torch.zeros((CAP, 7), **f32),
+                                   target=torch.zeros((CAP, D), **f32), weight=torch.zeros((CAP, D), **f32),
+                                   domain=torch.zeros((CAP,), **i32), num_rois=torch.zeros((2,), **i32)),
+                        pool=torch.zeros((CAP, 7, 7, channels), **f32),
+                        arg5=torch.zeros((CAP, 7, 7, channels), **adt),
+                        arg4=torch.zeros((CAP, 7, 7, channels), **adt),
+                        add_ws=None, prepped=False)
+        # pipeline=True: two sets; step(inputs, next_inputs) runs the forward /
+        # backward of `inputs` on one while the vote, RoI-pool forward and ADD
+        # row classification of `next_inputs` fill the other on a third stream
+        self.pipeline = bool(pipeline)
+        self._sets = [minibatch_set() for _ in range(2 if self.pipeline else 1)]
+        self._cur = 0           # the set the step's forward / backward uses (and the attributes show)
+        self._primed = None     # pipelined: (set index, inputs) voted + pooled ahead by the previous step
+        self.prefetch_at = prefetch_at  # where the next minibatch's front chain forks off: "loss" | "bwd" | "start"
+        if prefetch_at not in ("loss", "bwd", "start"):
+            raise ValueError("prefetch_at must be 'loss', 'bwd' or 'start'")
+        self.pre_stream = torch.cuda.Stream(device=device) if self.pipeline else None
+        self._next = None       # (inputs, set index) of the minibatch to prefetch during this step
         self.y6 = torch.zeros((CAP, units), **f32)
         self.y7 = torch.zeros((CAP, units), **f32)
         self.y8 = torch.zeros((CAP, D), **f32)
         self.t8 = torch.zeros((CAP, D), **f32)
         self.pred = torch.zeros((CAP, D), **f32)
         self.loss = torch.zeros((1,), **f32)
-        self.add_ws = None  # ADD-loss workspace (row classes written on the side stream after the vote)
         self.diff = torch.zeros((CAP, D), **f32)
         self.one = torch.ones((1,), **f32)
         self.dy8 = torch.zeros((CAP, D), **f32)
@@ -154,26 +173,78 @@ class PoseStep:
                     step.timer.setdefault(name, []).append((self_.e0, e1))
         return _Ctx()
 
-    def vote(self, label, vertex, extents, meta, gt):
+    # the current minibatch set's buffers (after a pipelined step: the set that
+    # step trained on, not the one its prefetch filled)
+    hough = property(lambda self: self._sets[self._cur]["hough"])
+    pool = property(lambda self: self._sets[self._cur]["pool"])
+    arg5 = property(lambda self: self._sets[self._cur]["arg5"])
+    arg4 = property(lambda self: self._sets[self._cur]["arg4"])
+    add_ws = property(lambda self: self._sets[self._cur]["add_ws"])
+
+    def vote(self, label, vertex, extents, meta, gt, s=None):
+        s = self._cur if s is None else s
+        self._sets[s]["pooled"] = False
         with self._t("hough_voting_gpu"):
             return hv.hough_voting_gpu_capacity(label, vertex, extents, meta, gt, self.is_train, self.vthr,
                                                 self.vper, self.skip, global_batch=self.global_batch,
-                                                batch_base=self.batch_base, out=self.hough)
+                                                batch_base=self.batch_base, out=self._sets[s]["hough"])
 
-    def add_prep(self, points, symmetry):
+    def add_prep(self, points, symmetry, s=None, stream=None):
         """The ADD loss's row classification (it reads only the Hough weights):
-        on the side stream right after the vote, joined before the loss."""
-        if self.add_ws is None:
-            self.add_ws = torch.empty(adl.workspace_bytes(CAP, self.C, points.shape[1]), dtype=torch.uint8,
-                                      device=self.dev)
-        h = self.hough
-        side = self.side_stream if self.timer is None and self.side_prep else None
-        if side is not None:
-            side.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(side or torch.cuda.current_stream()):
-            adl.average_distance_loss_prep(h["weight"], symmetry, points.shape[1], self.add_ws,
+        on the side stream right after the vote, joined before the loss
+        (`stream` given: on that stream, already ordered after the vote)."""
+        s = self._cur if s is None else s
+        st = self._sets[s]
+        if st["add_ws"] is None:
+            st["add_ws"] = torch.empty(adl.workspace_bytes(CAP, self.C, points.shape[1]), dtype=torch.uint8,
+                                       device=self.dev)
+        h = st["hough"]
+        side = None
+        if stream is None:
+            side = self.side_stream if self.timer is None and self.side_prep else None
+            if side is not None:
+                side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(stream or side or torch.cuda.current_stream()):
+            adl.average_distance_loss_prep(h["weight"], symmetry, points.shape[1], st["add_ws"],
                                            num_rois=h["num_rois"][1:2])
-        self._prepped = True
+        st["prepped"] = "side" if side is not None else "stream"
+
+    def pool_fwd(self, conv4, conv5, s=None):
+        """pool5 + pool4 (vgg16_convs.py:177-184) and both argmax maps, one pass."""
+        s = self._cur if s is None else s
+        st = self._sets[s]
+        with self._t("roi_pool_fwd"):
+            rp.roi_pool_pair(conv5, 1.0 / 16.0, conv4, 1.0 / 8.0, st["hough"]["box"], 7, 7,
+                             num_rois=st["hough"]["num_rois"][1:2], out=(st["pool"], st["arg5"], st["arg4"]),
+                             batch_base=self.batch_base)
+        st["pooled"] = True
+
+    def _front(self, inputs, s, stream=None):
+        """A minibatch's weight-independent front chain into set s: the vote,
+        the ADD row classification and the RoI-pool forward (`stream`: all of
+        it there, in that order)."""
+        ctx = torch.cuda.stream(stream) if stream is not None else _nullctx()
+        with ctx:
+            self.vote(inputs["label"], inputs["vertex"], inputs["extents"], inputs["meta"], inputs["gt"], s=s)
+            if stream is not None:
+                self.add_prep(inputs["points"], inputs["symmetry"], s=s, stream=stream)
+                self.pool_fwd(inputs["conv4"], inputs["conv5"], s=s)
+
+    def _prefetch(self):
+        """The next minibatch's front chain on the prefetch stream (pipelined
+        step): ordered after everything the step has issued so far on its
+        stream -- so after the previous step, which last used that set -- and
+        joined by the next step before it reads the set."""
+        if self._next is None:
+            return
+        nxt, s = self._next
+        self._next = None
+        if self.timer is not None:  # per-op timing runs the ops one by one on the step's stream
+            self._front(nxt, s, stream=torch.cuda.current_stream())
+        else:
+            self.pre_stream.wait_stream(torch.cuda.current_stream())
+            self._front(nxt, s, stream=self.pre_stream)
+        self._primed = (s, nxt)
 
     def set_drop_masks(self, m6, m7):
         """Use fixed dropout keep masks ((rows, units) 0/1, copied into the
@@ -243,9 +314,9 @@ class PoseStep:
         nr = h["num_rois"][1:2]  # output row count (incl. dummy row)
         w = self.weights
         K6 = 49 * self.Ch
-        with self._t("roi_pool_fwd"):  # pool = pool5 + pool4 (vgg16_convs.py:177-184), one pass
-            rp.roi_pool_pair(conv5, 1.0 / 16.0, conv4, 1.0 / 8.0, h["box"], 7, 7, num_rois=nr,
-                             out=(self.pool, self.arg5, self.arg4), batch_base=self.batch_base)
+        st = self._sets[self._cur]
+        if not (self.pipeline and st.get("pooled")):  # pipelined: pooled ahead by the previous step's prefetch
+            self.pool_fwd(conv4, conv5)
         x = self.pool.view(CAP, K6)
         gs = self.gshard if self.backward else None
         if gs is not None:  # fc6 input column blocks to their owners (overlaps the forward)
@@ -269,6 +340,8 @@ class PoseStep:
             if gs is not None:
                 gs.send_input("w8", self.y7)
             self._g("fc8_fwd", self.y7, w.w8, self.y8, bias=w.b8, act=0, M_dev=nr)
+        if self.prefetch_at == "loss":  # the next minibatch's vote + pool beside the loss and the backward
+            self._prefetch()
         if gen:  # the step counter moves on once both masks are drawn
             if self._in_step and self.backward:
                 self._bump_drop_step = True  # at the end of the data-gradient chain, beside the dW tail
@@ -279,17 +352,17 @@ class PoseStep:
             self.norm_rows.clamp_(min=1)
         with self._t("head_add_loss_fwd"):
             ph.head_fwd(self.y8, h["weight"], self.t8, self.pred, num_rois=nr)
-            if not getattr(self, "_prepped", False):  # forward() called without step()
+            if not st["prepped"]:  # forward() called without step()
                 self.add_prep(points, symmetry)
-            if self.timer is None and self.side_prep:
+            if st["prepped"] == "side":
                 torch.cuda.current_stream().wait_stream(self.side_stream)  # the row classes (add_prep)
-            self._prepped = False
+            st["prepped"] = False
             # the previous step's in-place loss all-reduce must be done before
             # the loss kernel rewrites self.loss (its handle orders it on this stream)
             self._wait("loss")
             adl.average_distance_loss(self.pred, h["target"], h["weight"], points, symmetry, self.margin,
                                       num_rois=nr, loss_norm_rows_dev=self.norm_rows, out=(self.loss, self.diff),
-                                      workspace=self.add_ws, prepared=True)
+                                      workspace=st["add_ws"], prepared=True)
         if self.dist is not None:  # nothing downstream reads the global loss: joined at the end of the step
             self._pending["loss"] = self.dist.all_reduce(self.loss, async_op=True)
             if not self._in_step:  # called on its own: the returned loss is the reduced one
@@ -322,7 +395,8 @@ class PoseStep:
                 gs.send_grad(name, dY, nr)
             with torch.cuda.stream(side or main):
                 if gs is not None:
-                    gs.reduce(name, g[name], g["b" + name[1:]], self._gemm, ph.colsum)
+                    gs.reduce(name, g[name], g["b" + name[1:]],
+                              lambda A, B_, C_, **kw: self._g(f"fc{name[1:]}_dw", A, B_, C_, **kw), ph.colsum)
                 else:
                     # the bias sum first: a short launch ahead of the long dW GEMM, not
                     # a tail after it (fc6: it ran 44 us behind the dW, beside the pool bwd)
@@ -333,6 +407,8 @@ class PoseStep:
             # average_distance_loss_grad (top_diff[0] * bottom_diff) folded into
             # the head backward: one pass over the (R, 4C) rows instead of two
             ph.head_bwd(self.diff, self.t8, h["weight"], self.pred, self.dy8, num_rois=nr, d_pred_scale=self.one)
+        if self.prefetch_at == "bwd":
+            self._prefetch()
         with self._t("gemm_fc8_fc7_dw_bias"):  # fc8 weight / bias gradients
             weight_grads("w8", self.y7, self.dy8, CAP, w.units, self.D)
         dk = dict(keep_prob=self.keep) if self.keep < 1.0 else {}  # relu + dropout backward: kept grads / keep_prob
@@ -373,11 +449,46 @@ class PoseStep:
         self.gemm_timer.setdefault(name, []).append((e0, e1))
         return C
 
-    def step(self, inputs):
+    def step(self, inputs, next_inputs=None):
+        """One training step over the minibatch `inputs`.
+
+        Pipelined (PoseStep(pipeline=True)): the vote, ADD row classification
+        and RoI-pool forward of `next_inputs` (the minibatch of the following
+        call) run on the prefetch stream beside this step's loss and backward
+        (`prefetch_at`), into the other buffer set; the following step(
+        next_inputs, ...) starts from them.  They depend only on a minibatch's
+        inputs, not on the weights (vgg16_convs.py:167-184: the Hough op and
+        the RoI pools read the network's label / vertex / conv maps), so every
+        output is the unpipelined step's, bit for bit.  A call whose inputs
+        were not prefetched runs its own front chain first."""
+        if self.pipeline:
+            return self._step_pipelined(inputs, next_inputs)
+        if next_inputs is not None:
+            raise ValueError("next_inputs needs PoseStep(pipeline=True)")
         self.vote(inputs["label"], inputs["vertex"], inputs["extents"], inputs["meta"], inputs["gt"])
         self.draw_drop_masks()
         if self.side_prep:  # else forward() classifies the rows right before the loss
             self.add_prep(inputs["points"], inputs["symmetry"])
+        return self._train(inputs)
+
+    def _step_pipelined(self, inputs, next_inputs):
+        main = torch.cuda.current_stream()
+        if self._primed is not None and self._primed[1] is inputs:
+            self._cur = self._primed[0]
+            main.wait_stream(self.pre_stream)  # this minibatch's vote / prep / pool (previous step's prefetch)
+        else:  # not prefetched (first step, or other inputs): its front chain here, on the step's stream
+            self._front(inputs, self._cur, stream=main)
+        self._primed = None
+        self._next = (next_inputs, 1 - self._cur) if next_inputs is not None else None
+        self.draw_drop_masks()
+        if self.prefetch_at == "start":
+            self._prefetch()
+        loss = self._train(inputs)
+        self._prefetch()  # (no-op unless the fork point was never reached)
+        return loss
+
+    def _train(self, inputs):
+        """Forward + backward of the minibatch whose vote is in the current set."""
         self.exchange()
         if self.dist is not None:  # the RoI / pose all-gather: started here, joined at the end of the step
             with self._t("allgather_rois"):

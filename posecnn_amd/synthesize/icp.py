@@ -14,6 +14,9 @@ pose_energy(live, label, obj, pred_vertices, poses, ...)   -> (K,)
 Poses are (qw, qx, qy, qz, tx, ty, tz) float32 rows; camera = (fx, fy, px, py).
 The rendered maps (the reference's OpenGL pass) are inputs.
 """
+import ctypes
+import os
+
 import numpy as np
 import torch
 
@@ -198,13 +201,28 @@ def pose_energy_records(records, counts, poses, pose_prob, depth_range=(0.25, 6.
     return energy
 
 
-def nelder_mead_device(records, counts, x0, lb, ub, max_eval, depth_range=(0.25, 6.0), stream=None):
+NM_PATHS = {0: "auto", 1: "k_nm_spec (speculative rounds, cooperative)", 2: "k_nm<8> (cooperative)",
+            3: "k_nm<1> (one workgroup per problem)"}
+
+
+def nelder_mead_device(records, counts, x0, lb, ub, max_eval, depth_range=(0.25, 6.0), stream=None, force_path=None,
+                       return_path=False):
     """The bounded Nelder-Mead of nelder_mead_steps on optEnergy, for N
     problems at once on the device (eight cooperating workgroups per
     evaluated point, up to four points of a step per round while N <= 32; no
     host read until the end): x0 / lb / ub (N,7) float64.  Returns (x (N,7), f (N,), nev (N,))
-    as device tensors; the same bits as nelder_mead over pose_energy_records."""
+    as device tensors; the same bits as nelder_mead over pose_energy_records.
+    nev[i] = -1: a cross-workgroup wait of problem i gave up (results invalid).
+    max_eval must cover the initial simplex (>= 8; NLopt's maxeval counts it).
+    force_path (or env PCNN_NM_PATH) pins the kernel (NM_PATHS: 1 speculative,
+    2 cooperative, 3 one workgroup); return_path adds the path that ran."""
     _lib.require_gpu(records, counts)
+    if int(max_eval) < 8:
+        raise ValueError("nelder_mead_device: max_eval must be >= 8 (the 7-D initial simplex)")
+    if force_path is None:
+        force_path = int(os.environ.get("PCNN_NM_PATH", "0") or 0)
+    if force_path not in NM_PATHS:
+        raise ValueError(f"nelder_mead_device: force_path in {sorted(NM_PATHS)}")
     dev = records.device
     d64 = dict(dtype=torch.float64, device=dev)
     x0_, lb_, ub_ = (torch.as_tensor(a).to(**d64).contiguous() for a in (x0, lb, ub))
@@ -215,19 +233,24 @@ def nelder_mead_device(records, counts, x0, lb, ub, max_eval, depth_range=(0.25,
     f = torch.empty((N,), **d64)
     nev = torch.empty((N,), dtype=torch.int32, device=dev)
     L = _lib.load()
+    path = ctypes.c_int32(0)
     if N <= 128:  # kNmCoop workgroups per problem, launched cooperatively (same bits as one workgroup)
         ws = _lib.workspace(L.pcnn_nelder_mead_energy_workspace_size(N), dev, "nelder_mead", stream)
-        rc = L.pcnn_nelder_mead_energy_coop(_lib.ptr(records), _lib.ptr(counts), records.shape[1], N, _lib.ptr(x0_),
-                                            _lib.ptr(lb_), _lib.ptr(ub_), int(max_eval), float(depth_range[0]),
-                                            float(depth_range[1]), _lib.ptr(x), _lib.ptr(f), _lib.ptr(nev),
-                                            _lib.ptr(ws), ws.numel(), _lib.stream_ptr(stream))
+        rc = L.pcnn_nelder_mead_energy_coop_path(_lib.ptr(records), _lib.ptr(counts), records.shape[1], N,
+                                                 _lib.ptr(x0_), _lib.ptr(lb_), _lib.ptr(ub_), int(max_eval),
+                                                 float(depth_range[0]), float(depth_range[1]), _lib.ptr(x),
+                                                 _lib.ptr(f), _lib.ptr(nev), _lib.ptr(ws), ws.numel(), int(force_path),
+                                                 ctypes.byref(path), _lib.stream_ptr(stream))
     else:
+        if force_path not in (0, 3):
+            raise ValueError("nelder_mead_device: more than 128 problems run on the one-workgroup path only")
         rc = L.pcnn_nelder_mead_energy(_lib.ptr(records), _lib.ptr(counts), records.shape[1], N, _lib.ptr(x0_),
                                        _lib.ptr(lb_), _lib.ptr(ub_), int(max_eval), float(depth_range[0]),
                                        float(depth_range[1]), _lib.ptr(x), _lib.ptr(f), _lib.ptr(nev),
                                        _lib.stream_ptr(stream))
+        path.value = 3
     _lib.check(rc, "nelder_mead_device")
-    return x, f, nev
+    return (x, f, nev, int(path.value)) if return_path else (x, f, nev)
 
 
 def icp_score(live, label, obj, vertmap, hyps, radius=0.01, stream=None):
@@ -387,6 +410,8 @@ def solve_icp(labelmap, depth, parameters, rois, poses, render, max_error=0.01, 
     bit for bit); the eight
     depth hypotheses of every RoI refined by one 8-iteration ICP launch; the
     SegICP score per RoI, its choice read once at the end."""
+    if nm_evals and int(nm_evals) < 8:
+        raise ValueError("solve_icp: nm_evals must be 0 (no search) or >= 8 (the 7-D initial simplex)")
     import numpy as np
     fx, fy, px, py, znear, zfar, factor = (float(v) for v in parameters)
     cam = (fx, fy, px, py)
@@ -431,10 +456,15 @@ def solve_icp(labelmap, depth, parameters, rois, poses, render, max_error=0.01, 
         r = np.array([0.1, 0.1, 0.1, 0.1, 0.01, 0.01, 0.1])  # poseWithOpt's bounds (:2535-2558)
         rec, cnt = energy_records(live, lab, [objs[k] for k in nm], nm, pv0, (znear, zfar), stream)
         X0 = np.repeat(x0[None], len(nm), 0)
+        res = None
         if nm_device:
-            xs, _, _ = nelder_mead_device(rec, cnt, X0, X0 - r, X0 + r, nm_evals, (znear, zfar), stream)
-            res = [(x, None) for x in xs.cpu().numpy()]
-        else:
+            xs, _, nev = nelder_mead_device(rec, cnt, X0, X0 - r, X0 + r, nm_evals, (znear, zfar), stream)
+            xn = torch.cat([xs, nev.view(-1, 1).double()], 1).cpu().numpy()  # one host read
+            if (xn[:, -1] >= 0).all():
+                res = [(x, None) for x in xn[:, :-1]]
+            # else: a cross-workgroup wait gave up (nev -1): the host-driven
+            # search below, which gives the same bits when the device one works
+        if res is None:
             def energies(items):  # every search's pending points: one launch, one host read
                 P = np.concatenate([pts for _, pts in items]).astype(np.float32)
                 who = np.concatenate([np.full(len(pts), j, np.int32) for j, pts in items])

@@ -30,17 +30,35 @@ def estimate_poses_3d(labels, depth, vertmap, extents, poses, num_classes, fx, f
         raise _lib.PcnnError("posecnn_amd ops run only on an AMD GPU (HIP); none is visible")
     dev = vertmap.device if torch.is_tensor(vertmap) and vertmap.is_cuda else torch.device("cuda")
     lab = _dev_tensor(labels, torch.int32, dev)
-    # the raw uint16 depth travels as int16 of the same bits (the kernel reads uint16)
+    # the raw uint16 depth travels as int16 of the same bits (the kernel reads
+    # uint16).  Only integer raw units are accepted: a float map (e.g. depth
+    # already in metres) would truncate to holes / single units,
+    # and values outside 0..65535 would wrap
     if torch.is_tensor(depth):
         d = depth
+        if d.dtype.is_floating_point or d.dtype.is_complex or d.dtype == torch.bool:
+            raise ValueError("estimate_poses_3d: depth must hold raw integer sensor units (uint16 / int16 / "
+                             "int32), not %s; convert metres with round(depth * factor) first" % d.dtype)
         if d.dtype == torch.uint16:
             d = d.view(torch.int16)
-        elif d.dtype != torch.int16:
-            d = d.to(torch.int32).clamp(0, 65535)
+        elif d.dtype == torch.int16:
+            if bool((d < 0).any()):
+                raise ValueError("estimate_poses_3d: negative raw depth (int16 is read as uint16 bits only for "
+                                 "torch.uint16 inputs)")
+        else:
+            d = d.to(torch.int64)
+            if bool(((d < 0) | (d > 65535)).any()):
+                raise ValueError("estimate_poses_3d: raw depth outside 0..65535")
             d = torch.where(d > 32767, d - 65536, d).to(torch.int16)
         dep = d.to(dev).contiguous()
     else:
-        dep = torch.from_numpy(np.ascontiguousarray(depth, np.uint16).view(np.int16)).to(dev)
+        a = np.asarray(depth)
+        if a.dtype.kind not in "ui":
+            raise ValueError("estimate_poses_3d: depth must hold raw integer sensor units (uint16 / int16 / int32), "
+                             "not %s; convert metres with round(depth * factor) first" % a.dtype)
+        if a.size and (int(a.min()) < 0 or int(a.max()) > 65535):
+            raise ValueError("estimate_poses_3d: raw depth outside 0..65535")
+        dep = torch.from_numpy(np.ascontiguousarray(a, np.uint16).view(np.int16)).to(dev)
     vm = _dev_tensor(vertmap, torch.float32, dev)
     ext = _dev_tensor(extents, torch.float32, dev)
     C = int(num_classes)
@@ -57,6 +75,8 @@ def estimate_poses_3d(labels, depth, vertmap, extents, poses, num_classes, fx, f
         raise ValueError("estimate_poses_3d: n_hyp in 1..256")
     if not float(factor) > 0:
         raise ValueError("estimate_poses_3d: factor must be positive")
+    if int(nm_evals) < 7:  # the 6-D search's initial simplex; NLopt's maxeval counts it too
+        raise ValueError("estimate_poses_3d: nm_evals must be >= 7 (the initial simplex)")
     f32 = dict(dtype=torch.float32, device=dev)
     i32 = dict(dtype=torch.int32, device=dev)
     out = torch.zeros((3, 4, C), **f32)

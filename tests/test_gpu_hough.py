@@ -55,6 +55,16 @@ def test_hough_full_frame_skip1(hip, orc):
     assert _check(orc, fr, 0, skip=1) > 0
 
 
+def test_hough_max_classes_skip1(hip, orc):
+    """C = kMaxClasses (256) at skip 1: the placement pass's LDS (57 KiB of
+    queue and group counts + its static tables) is past the 64 KiB default
+    window, so the launch raises the limit (it used to fail)."""
+    C = 256
+    ext = np.random.default_rng(3).uniform(0.08, 0.25, size=(C, 3)).astype(np.float32)
+    fr = synth.make_frames(1, H=96, W=128, num_classes=C, objects_per_image=5, seed=21, extents=ext)
+    assert _check(orc, fr, 1, skip=1) > 0
+
+
 def test_hough_counts_map_exact(hip, orc):
     """The whole per-class Hough space (reference hough_space) matches exactly."""
     fr = synth.make_frames(1, H=120, W=160, seed=7, objects_per_image=3)

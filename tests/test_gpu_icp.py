@@ -263,14 +263,15 @@ def test_solve_icp_batched_over_rois(hip):
         assert np.linalg.norm(picp[i, 4:] - trues[c][4:]) < 5e-3
 
 
-@pytest.mark.parametrize("max_eval", [5, 12, 50])
+@pytest.mark.parametrize("max_eval", [8, 12, 50])
 def test_nelder_mead_device_matches_host(hip, orc, max_eval):
     """refinePose's Nelder-Mead (poseWithOpt, synthesize.cpp:2529-2573) run
     wholly on the device, one workgroup per problem (pcnn_nelder_mead_energy),
     against the host search (icp.py nelder_mead) over the same record-based
     optEnergy (pcnn_energy_rec): the same points, values and evaluation counts,
-    bit for bit, for max_eval below the initial simplex (5), with shrinks (12)
-    and at solveICP's 50.  The record energy is optEnergy over the pixels of
+    bit for bit, for max_eval equal to the initial simplex (8), with shrinks
+    (12) and at solveICP's 50 (budgets below the simplex are refused: NLopt's
+    maxeval counts it, test_nelder_mead_device_refuses_small_budget).  The record energy is optEnergy over the pixels of
     the full-frame kernel (pcnn_pose_energy, parity-tested against the
     oracle), summed in another fixed order."""
     from posecnn_amd.synthesize import icp as R
@@ -325,18 +326,37 @@ def test_nelder_mead_device_launch_paths_agree(hip, orc):
                    [0.98, -0.03, 0.02, 0.01, -0.004, 0.003, -0.02]], np.float64)
     r = np.array([0.1, 0.1, 0.1, 0.1, 0.01, 0.01, 0.1])
     out = {}
-    for N in (3, 40, 130):
+    ran = {}
+    for N, force in ((3, 0), (40, 0), (130, 0), (3, 2), (3, 3), (40, 3)):
         sel = torch.arange(N, device=D) % 3
         recN, cntN = rec.index_select(0, sel).contiguous(), cnt.index_select(0, sel).contiguous()
         xN = x0[np.arange(N) % 3]
-        x, f, nev = R.nelder_mead_device(recN, cntN, xN, xN - r, xN + r, 30)
-        out[N] = (x.cpu().numpy()[:3], f.cpu().numpy()[:3], nev.cpu().numpy()[:3])
+        x, f, nev, path = R.nelder_mead_device(recN, cntN, xN, xN - r, xN + r, 30, force_path=force,
+                                               return_path=True)
+        out[(N, force)] = (x.cpu().numpy()[:3], f.cpu().numpy()[:3], nev.cpu().numpy()[:3])
+        ran[(N, force)] = path
         del recN
-    for N in (40, 130):
-        np.testing.assert_array_equal(out[N][0], out[3][0])
-        np.testing.assert_array_equal(out[N][1], out[3][1])
-        np.testing.assert_array_equal(out[N][2], out[3][2])
-    assert (out[3][2] == 30).all()
+    # the comparison must not be one kernel against itself -- the
+    # speculative and cooperative paths (and their barriers) really ran
+    assert ran[(3, 0)] == 1 and ran[(40, 0)] == 2 and ran[(130, 0)] == 3, ran
+    assert ran[(3, 2)] == 2 and ran[(3, 3)] == 3 and ran[(40, 3)] == 3, ran
+    for key in out:
+        for a, b in zip(out[key], out[(3, 0)]):
+            np.testing.assert_array_equal(a, b)
+    assert (out[(3, 0)][2] == 30).all()
+
+
+def test_nelder_mead_device_refuses_small_budget(hip):
+    """max_eval below the 7-D initial simplex is refused (the
+    device search used to evaluate all 8 points and report nev 8 anyway)."""
+    from posecnn_amd.synthesize import icp as R
+    rec = torch.zeros((1, 16, 6), device=D)
+    cnt = torch.ones((1,), dtype=torch.int32, device=D)
+    x0 = np.array([[1, 0, 0, 0, 0, 0, 0]], np.float64)
+    with pytest.raises(ValueError):
+        R.nelder_mead_device(rec, cnt, x0, x0 - 0.1, x0 + 0.1, 5)
+    with pytest.raises(ValueError):
+        R.solve_icp(None, None, None, None, None, None, nm_evals=5)
 
 
 def test_solve_icp_device_search_matches_host_driver(hip):

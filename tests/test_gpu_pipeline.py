@@ -1,0 +1,85 @@
+"""The pipelined pose step (PoseStep(pipeline=True)): the next minibatch's
+vote, ADD row classification and RoI-pool forward run on the prefetch stream
+beside the current step's loss and backward, into a second buffer set.  These
+depend only on a minibatch's inputs (vgg16_convs.py:167-184), so every output
+of every step must be bit-identical to the unpipelined step on the same
+minibatch -- checked over three consecutive steps with different frames, at
+each fork point, plus the fallback for inputs that were not prefetched."""
+import numpy as np
+import pytest
+import torch
+
+from posecnn_amd import synth
+from posecnn_amd.pipeline import PoseStep
+
+pytestmark = pytest.mark.gpu
+D = torch.device("cuda")
+B, H, W, C, CH, UNITS = 2, 120, 160, 22, 64, 256
+
+
+def _batches(n):
+    pts, sym = synth.rescaled_points(C)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(D)
+    out = []
+    for k in range(n):
+        fr = synth.make_frames(B, H=H, W=W, num_classes=C, objects_per_image=4, seed=120 + k)
+        g = torch.Generator().manual_seed(40 + k)
+        out.append(dict(label=t(fr["label"]), vertex=t(fr["vertex"]), extents=t(fr["extents"]), meta=t(fr["meta"]),
+                        gt=t(fr["gt"]), conv4=torch.randn((B, H // 8, W // 8, CH), generator=g).to(D),
+                        conv5=torch.randn((B, H // 16, W // 16, CH), generator=g).to(D), points=t(pts),
+                        symmetry=t(sym)))
+    return out
+
+
+def _snap(step):
+    n = int(step.hough["num_rois"][1].item())
+    h = step.hough
+    return dict(n=n, box=h["box"][:n].clone(), pose=h["pose"][:n].clone(), target=h["target"][:n].clone(),
+                weight=h["weight"][:n].clone(), pool=step.pool[:n].clone(), arg5=step.arg5[:n].clone(),
+                arg4=step.arg4[:n].clone(), loss=step.loss.clone(), diff=step.diff[:n].clone(),
+                drop6=step.drop6[:n].clone() if step.drop6 is not None else None, y7=step.y7[:n].clone(), dx=step.dx[:n].clone(),
+                dconv4=step.dconv4.clone(), dconv5=step.dconv5.clone(),
+                **{"g_" + k: v.clone() for k, v in step.grads.items()})
+
+
+def _run(batches, weights, **kw):
+    step = PoseStep(B, H, W, C, D, channels=CH, units=UNITS, is_train=1, skip_pixels=3, weights=weights, **kw)
+    res = []
+    for k, inp in enumerate(batches):
+        nxt = batches[k + 1] if kw.get("pipeline") and k + 1 < len(batches) else None
+        step.step(inp, nxt) if kw.get("pipeline") else step.step(inp)
+        torch.cuda.synchronize()
+        res.append(_snap(step))
+    return step, res
+
+
+@pytest.mark.parametrize("fork", ["loss", "bwd", "start"])
+def test_pipelined_steps_bit_identical(hip, fork):
+    batches = _batches(3)
+    ref_step, ref = _run(batches, None)
+    assert len({r["n"] for r in ref}) > 1 or not torch.equal(ref[0]["box"], ref[1]["box"])  # distinct minibatches
+    _, got = _run(batches, ref_step.weights, pipeline=True, prefetch_at=fork)
+    for k, (a, b) in enumerate(zip(ref, got)):
+        assert a["n"] == b["n"] > 8, (k, a["n"], b["n"])
+        for key in a:
+            if key == "n" or a[key] is None:
+                continue
+            assert torch.equal(a[key], b[key]), f"step {k}: {key} differs (fork {fork})"
+
+
+def test_pipelined_step_without_prefetch_and_mismatched_inputs(hip):
+    """A call whose inputs are not the previous call's next_inputs runs its
+    own front chain (no stale prefetched set is used)."""
+    batches = _batches(3)
+    ref_step, ref = _run(batches, None, keep_prob=1.0)  # no dropout: step 2 here is the reference's step 3
+    step = PoseStep(B, H, W, C, D, channels=CH, units=UNITS, is_train=1, skip_pixels=3, weights=ref_step.weights,
+                    pipeline=True, keep_prob=1.0)
+    step.step(batches[0], batches[1])  # prefetches batch 1 ...
+    torch.cuda.synchronize()
+    step.step(batches[2])  # ... but batch 2 comes: voted here
+    torch.cuda.synchronize()
+    got = _snap(step)
+    for key in ("box", "pool", "loss", "dconv4", "g_w6"):
+        assert torch.equal(ref[2][key], got[key]), key
+    with pytest.raises(ValueError):
+        PoseStep(B, H, W, C, D, channels=CH, units=UNITS, weights=ref_step.weights).step(batches[0], batches[1])

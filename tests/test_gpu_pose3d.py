@@ -135,6 +135,19 @@ def test_pose3d_device_inputs_and_errors(hip):
     with pytest.raises(ValueError):
         pose3d.estimate_poses_3d(sc["label"], sc["depth"][:5], sc["vertmap"], sc["extents"], p2, sc["C"],
                                  *sc["camera"], sc["depth_factor"])
+    # depth must be raw integer units (a float map in metres used
+    # to truncate silently), within 0..65535; nm_evals must cover the simplex
+    for bad in (sc["depth"].astype(np.float32) / sc["depth_factor"],
+                torch.from_numpy(sc["depth"].astype(np.float32)),
+                np.where(np.arange(sc["depth"].size).reshape(sc["depth"].shape) == 0, -1,
+                         sc["depth"].astype(np.int32)),
+                sc["depth"].astype(np.int32) + 70000):
+        with pytest.raises(ValueError):
+            pose3d.estimate_poses_3d(sc["label"], bad, sc["vertmap"], sc["extents"], p2, sc["C"], *sc["camera"],
+                                     sc["depth_factor"])
+    with pytest.raises(ValueError):
+        pose3d.estimate_poses_3d(sc["label"], sc["depth"], sc["vertmap"], sc["extents"], p2, sc["C"], *sc["camera"],
+                                 sc["depth_factor"], nm_evals=6)
 
 
 def _mat2quat(R):
