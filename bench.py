@@ -64,6 +64,8 @@ def parse(argv=None):
                         "synthetic minibatches")
     p.add_argument("--prefetch-at", choices=["loss", "bwd", "start"], default="start",
                    help="with --pipeline on: where the next minibatch's front chain forks off the step")
+    p.add_argument("--no-fuse-loss-tail", action="store_true",
+                   help="ADD loss row tail and pose-head backward as separate launches (PoseStep fuse_loss_tail=False)")
     p.add_argument("--no-n1-reference", action="store_true",
                    help="N > 1: skip rank 0's one-GPU run of its own shard at the same geometry")
     return p.parse_args(argv)
@@ -215,7 +217,7 @@ def main():
         step = PoseStep(B, H, W, C, dev, is_train=1, skip_pixels=10, global_batch=gB, batch_base=rank * B,
                         dist=dist, precision=args.precision, pixel_argmax=not args.flat_argmax,
                         side_prep=not args.prep_on_main, drop_in_reduce=not args.mask_kernel,
-                        pipeline=pipelined, prefetch_at=args.prefetch_at)
+                        pipeline=pipelined, prefetch_at=args.prefetch_at, fuse_loss_tail=not args.no_fuse_loss_tail)
         run = runner(step)
         step_run = run
     if linemod:  # + the depth back-projection op, forward and backward (no reference caller)

@@ -196,10 +196,38 @@ int pcnn_add_loss_fwd(const float* pred, const float* target, const float* weigh
  * prep by the caller). */
 int pcnn_add_loss_prep(const float* weight, const float* symmetry, int R_cap, const int32_t* num_rois_dev, int C,
                        int P, void* workspace, size_t workspace_bytes, void* stream);
+/* pcnn_add_loss_prep with the model points (C, P, 3): when the environment
+ * sets PCNN_ADD_SEARCH=pruned (P <= 4096) it also builds each symmetric
+ * class's Morton order in the workspace, which the ADD-S nearest-point search
+ * then prunes with (the same bits as the default full O(P^2) scan). */
+/* Byte offset in the loss workspace of the pruned search's diagnostics
+ * (what = 0: the Morton orders, C x P int32; 1: int32 [blocks scanned, blocks
+ * held] of the last search), -1 when P is past the pruned search's limit. */
+long pcnn_add_loss_ws_offset(int R_cap, int C, int P, int what);
+int pcnn_add_loss_prep_points(const float* weight, const float* symmetry, const float* points, int R_cap,
+                              const int32_t* num_rois_dev, int C, int P, void* workspace, size_t workspace_bytes,
+                              void* stream);
 int pcnn_add_loss_fwd_prepared(const float* pred, const float* target, const float* weight, const float* points,
                                const float* symmetry, int R_cap, const int32_t* num_rois_dev, int C, int P,
                                float margin, int loss_norm_rows, const int32_t* loss_norm_rows_dev, float* loss,
                                float* bottom_diff, void* workspace, size_t workspace_bytes, void* stream);
+
+/* The fused pose step's loss tail (posecnn_amd/pipeline.py): the prepared
+ * loss's per-point sums, then one pass that finishes each row's bottom_diff
+ * and runs the pose head's backward on it (pcnn_pose_head_bwd with
+ * d_pred = bottom_diff, scaled by d_pred_scale[0] -- the ADD gradient op,
+ * cu.cc:346-354; tanh_out and poses_weight = weight as pcnn_pose_head_fwd
+ * used them) into d_y8 (R, 4C): the same bits as pcnn_add_loss_fwd_prepared
+ * + pcnn_pose_head_bwd.  The scalar loss is left to pcnn_add_loss_total on
+ * the same workspace, which the caller may order on another stream (nothing
+ * on the backward chain reads it).  4C <= 256. */
+int pcnn_add_loss_fwd_head_bwd(const float* pred, const float* target, const float* weight, const float* points,
+                               const float* symmetry, int R_cap, const int32_t* num_rois_dev, int C, int P,
+                               float margin, int loss_norm_rows, const int32_t* loss_norm_rows_dev,
+                               float* bottom_diff, void* workspace, size_t workspace_bytes, const float* tanh_out,
+                               const float* d_pred_scale, float* d_y8, void* stream);
+int pcnn_add_loss_total(int R_cap, const int32_t* num_rois_dev, int C, int P, const void* workspace,
+                        size_t workspace_bytes, float* loss, void* stream);
 
 /* out[i] = top_diff[0] * bottom_diff[i], n = rows * 4C */
 int pcnn_add_loss_bwd(const float* top_diff, const float* bottom_diff, int n, const int32_t* num_rois_dev,

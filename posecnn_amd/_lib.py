@@ -62,6 +62,13 @@ _SIGS = {
     "pcnn_add_loss_fwd_prepared": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int, c_int,
                                   c_float, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
     "pcnn_add_loss_prep": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_size_t, c_void_p]),
+    "pcnn_add_loss_ws_offset": (ctypes.c_long, [c_int, c_int, c_int, c_int]),
+    "pcnn_add_loss_prep_points": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_void_p,
+                                          c_size_t, c_void_p]),
+    "pcnn_add_loss_fwd_head_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int,
+                                           c_int, c_float, c_int, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p,
+                                           c_void_p, c_void_p, c_void_p]),
+    "pcnn_add_loss_total": (c_int, [c_int, c_void_p, c_int, c_int, c_void_p, c_size_t, c_void_p, c_void_p]),
     "pcnn_add_loss_bwd": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p]),
     "pcnn_div_rn_check": (c_int, [c_void_p, c_float, c_int, c_int, c_void_p, c_void_p]),
     "pcnn_backproject_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_int,

@@ -19,7 +19,10 @@
 // (deterministic; fp32 sums agree with the reference's sequential sums to
 // ~1e-6 relative).
 #include "pcnn_common.h"
+#include "head_common.h"
 #include <cfloat>
+#include <cstdlib>
+#include <cstring>
 #include <type_traits>
 
 namespace {
@@ -204,7 +207,9 @@ __global__ void __launch_bounds__(kSymThreads) k_add_rows(const float* __restric
                                                            const int32_t* __restrict__ sym_rows,
                                                            const int32_t* __restrict__ nsym,
                                                            int32_t* __restrict__ queue,
-                                                           float* __restrict__ partial) {
+                                                           float* __restrict__ partial,
+                                                           const int32_t* __restrict__ nearest_in,
+                                                           const int32_t* __restrict__ perm_ok) {
   extern __shared__ __attribute__((aligned(16))) float4 gpts[];  // [P] GT-rotated points
   __shared__ float mdist[kSymGroups - 1][kPts];                   // range minima of groups 1..kSymGroups-1
   __shared__ int midx[kSymGroups - 1][kPts];
@@ -213,6 +218,8 @@ __global__ void __launch_bounds__(kSymThreads) k_add_rows(const float* __restric
   const int R = rows_of(num_rois_dev, R_cap);
   const int sym_items = *nsym * nchunk;
   const int items = sym_items + R;  // then one plain item per row (add_plain_row)
+  // nearest indices from k_add_search when its Morton orders exist (else the full scan here)
+  const int32_t* nearest = nearest_in && *perm_ok ? nearest_in : nullptr;
   const int grp = threadIdx.x / kSymLanes, lt = threadIdx.x % kSymLanes;
   const int quarter = ((P + kSymGroups - 1) / kSymGroups + kBlk - 1) / kBlk * kBlk;
   const int c0 = grp * quarter, c1 = min(P, c0 + quarter);
@@ -235,14 +242,15 @@ __global__ void __launch_bounds__(kSymThreads) k_add_rows(const float* __restric
   // ones fill the tail of the queue instead of opening a second round of
   // full-cost items
   const int nfull = P / kPts, nsym_rows = *nsym;
-  int n, chunk;
+  int n, chunk, slot;
   if (item < nsym_rows * nfull) {
-    n = sym_rows[item / nfull];
+    slot = item / nfull;
     chunk = item % nfull;
   } else {
-    n = sym_rows[item - nsym_rows * nfull];
+    slot = item - nsym_rows * nfull;
     chunk = nfull;
   }
+  n = sym_rows[slot];
   const int PC = 4 * C;
   const int cls = rcls[n];
   float* out = partial + ((size_t)n * nchunk + chunk) * 5;
@@ -253,6 +261,13 @@ __global__ void __launch_bounds__(kSymThreads) k_add_rows(const float* __restric
   const float s = pq[0], u = pq[1], v = pq[2], w = pq[3];
   quat2rot(s, u, v, w, Rp);
   const float* pts = points + (size_t)cls * P * 3;
+  if (nearest) {  // the nearest points come from k_add_search (pruned search): no staging, no scan
+    for (int jj = threadIdx.x; jj < kPts; jj += blockDim.x) {
+      const int p = chunk * kPts + jj;
+      s_imin[jj] = p < P ? nearest[(size_t)slot * P + p] : -1;
+    }
+    __syncthreads();
+  } else {
   for (int i = threadIdx.x; i < P; i += blockDim.x) {
     const float X0 = pts[i * 3 + 0], X1 = pts[i * 3 + 1], X2 = pts[i * 3 + 2];
     gpts[i] = make_float4(Rg[0] * X0 + Rg[1] * X1 + Rg[2] * X2, Rg[3] * X0 + Rg[4] * X1 + Rg[5] * X2,
@@ -366,6 +381,7 @@ __global__ void __launch_bounds__(kSymThreads) k_add_rows(const float* __restric
     }
   }
   __syncthreads();
+  }  // full scan
   // per-point loss and gradient terms (cu.cc:174-203), one point per thread
   // over the whole workgroup
   float acc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
@@ -377,8 +393,16 @@ __global__ void __launch_bounds__(kSymThreads) k_add_rows(const float* __restric
     const float x1 = Rp[0] * X0 + Rp[1] * X1 + Rp[2] * X2;  // = the scan's query point, same expression
     const float y1 = Rp[3] * X0 + Rp[4] * X1 + Rp[5] * X2;
     const float z1 = Rp[6] * X0 + Rp[7] * X1 + Rp[8] * X2;
-    const float4 cm = gpts[im];
-    const float x2 = cm.x, y2 = cm.y, z2 = cm.z;
+    float x2, y2, z2;
+    if (nearest) {  // the GT-rotated point by the staging's expression (the same bits as gpts[im])
+      const float Y0 = pts[im * 3 + 0], Y1 = pts[im * 3 + 1], Y2 = pts[im * 3 + 2];
+      x2 = Rg[0] * Y0 + Rg[1] * Y1 + Rg[2] * Y2;
+      y2 = Rg[3] * Y0 + Rg[4] * Y1 + Rg[5] * Y2;
+      z2 = Rg[6] * Y0 + Rg[7] * Y1 + Rg[8] * Y2;
+    } else {
+      const float4 cm = gpts[im];
+      x2 = cm.x, y2 = cm.y, z2 = cm.z;
+    }
     const int Rn = norm_rows_dev ? *norm_rows_dev : (norm_rows > 0 ? norm_rows : R);
     const float bn = (float)(Rn * P), rbn = 1.f / bn;
     const double ln = 2.0 * (double)Rn * (double)P, rln = 1.0 / ln;
@@ -419,12 +443,311 @@ __global__ void __launch_bounds__(kSymThreads) k_add_rows(const float* __restric
   }
 }
 
+// ---------------------------------------------------------------------------
+// Pruned ADD-S nearest-point search (symmetric rows).  The reference scans
+// all P GT-rotated model points for each of the P predicted points
+// (cu.cc:150-172: O(P^2) per row, the loss's whole cost).  Rotations keep
+// distances, so the model's points are grouped ONCE per call, in model space:
+// a Morton order per symmetric class (k_add_order, beside the row
+// classification), blocks of kPrBlk consecutive points and super-blocks of
+// kPrSup blocks.  Per row the blocks' bounding spheres are taken in the
+// rotated frame (centre = mean, radius = the largest point distance, padded);
+// each lane owns one query point (queries in the same Morton order, so a
+// wave's 64 queries are close together), seeds its minimum with the block
+// nearest it, then visits the blocks and skips -- wave-uniformly -- every
+// super-block / block whose sphere lies farther than the current minimum
+// from all 64 queries.  Candidates that are
+// visited get the reference's exact fp32 distance expression and the
+// first-minimum rule (lowest point index among equal minima, NaN never
+// wins), so the result is the full scan's index bit for bit; the bounds
+// carry 1e-4 relative + 1e-18 absolute slack (far above fp32 rounding), and a
+// non-finite sphere is never skipped.
+constexpr int kPrBlk = 8;       // candidates per block
+constexpr int kPrSup = 8;       // blocks per super-block
+constexpr int kPrThreads = 512;  // queries per search item (one per lane, 8 waves)
+constexpr int kPrMaxP = 4096;   // Morton sort of <= 4096 keys in LDS
+#ifndef ADD_PR_GRID
+#define ADD_PR_GRID 768
+#endif
+
+__device__ __forceinline__ float fl_dist(float ax, float ay, float az, float bx, float by, float bz) {
+  return (ax - bx) * (ax - bx) + (ay - by) * (ay - by) + (az - bz) * (az - bz);  // dist_to's expression
+}
+
+// Morton order of each symmetric class's model points (10 bits per axis of
+// the class's bounding box; ties by index): perm[c][i] = the i-th point.
+__global__ void __launch_bounds__(1024) k_add_order(const float* __restrict__ points,
+                                                     const float* __restrict__ symmetry, int P,
+                                                     int32_t* __restrict__ perm) {
+  __shared__ unsigned long long key[kPrMaxP];
+  __shared__ float red[6][16];
+  const int c = blockIdx.x, t = threadIdx.x;
+  if (!(symmetry[c] > 0)) return;
+  const float* pts = points + (size_t)c * P * 3;
+  float lo[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, hi[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+  for (int i = t; i < P; i += blockDim.x)
+    for (int a = 0; a < 3; a++) {
+      lo[a] = fminf(lo[a], pts[i * 3 + a]);
+      hi[a] = fmaxf(hi[a], pts[i * 3 + a]);
+    }
+  for (int a = 0; a < 3; a++) {
+    for (int o = 32; o > 0; o >>= 1) {
+      lo[a] = fminf(lo[a], __shfl_xor(lo[a], o));
+      hi[a] = fmaxf(hi[a], __shfl_xor(hi[a], o));
+    }
+    if (pcnn::lane_id() == 0) {
+      red[a][t >> 6] = lo[a];
+      red[3 + a][t >> 6] = hi[a];
+    }
+  }
+  __syncthreads();
+  for (int a = 0; a < 3; a++) {
+    lo[a] = red[a][0];
+    hi[a] = red[3 + a][0];
+    for (int w = 1; w < (int)(blockDim.x >> 6); w++) {
+      lo[a] = fminf(lo[a], red[a][w]);
+      hi[a] = fmaxf(hi[a], red[3 + a][w]);
+    }
+  }
+  int n2 = 1;
+  while (n2 < P) n2 <<= 1;
+  for (int i = t; i < n2; i += blockDim.x) {
+    unsigned long long k = ~0ull;
+    if (i < P) {
+      unsigned code = 0;
+      unsigned q[3];
+      for (int a = 0; a < 3; a++) {
+        const float ext = hi[a] - lo[a];
+        const float f = ext > 0.f ? (pts[i * 3 + a] - lo[a]) / ext * 1023.f : 0.f;
+        q[a] = f > 0.f ? (f < 1023.f ? (unsigned)f : 1023u) : 0u;  // NaN -> 0
+      }
+      for (int b = 0; b < 10; b++)
+        for (int a = 0; a < 3; a++) code |= ((q[a] >> b) & 1u) << (3 * b + a);
+      k = ((unsigned long long)code << 13) | (unsigned)i;
+    }
+    key[i] = k;
+  }
+  __syncthreads();
+  for (int k = 2; k <= n2; k <<= 1)  // bitonic sort, ascending
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = t; i < n2; i += blockDim.x) {
+        const int l = i ^ j;
+        if (l > i) {
+          const unsigned long long a = key[i], b = key[l];
+          const bool up = (i & k) == 0;
+          if (up ? a > b : a < b) {
+            key[i] = b;
+            key[l] = a;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  for (int i = t; i < P; i += blockDim.x) perm[(size_t)c * P + i] = (int32_t)(key[i] & 0x1FFFull);
+}
+
+// The search: item = (symmetric row, kPrThreads queries of its Morton order);
+// nearest[slot][p] = the index of point p's nearest GT-rotated model point
+// (first minimum), -1 when no distance is finite (the reference leaves
+// index_min unset; the loss then uses p itself).
+__global__ void __launch_bounds__(kPrThreads) k_add_search(const float* __restrict__ pred,
+                                                           const float* __restrict__ target,
+                                                           const float* __restrict__ points, int C, int P,
+                                                           const int32_t* __restrict__ rcls,
+                                                           const int32_t* __restrict__ sym_rows,
+                                                           const int32_t* __restrict__ nsym,
+                                                           const int32_t* __restrict__ perm,
+                                                           const int32_t* __restrict__ perm_ok,
+                                                           int32_t* __restrict__ queue,
+                                                           int32_t* __restrict__ nearest,
+                                                           int32_t* __restrict__ stats) {
+  extern __shared__ __attribute__((aligned(16))) float4 plds[];
+  const int nb = (P + kPrBlk - 1) / kPrBlk, nsb = (nb + kPrSup - 1) / kPrSup;
+  float4* gp = plds;        // [P] GT-rotated points in Morton order, w = the point's index (int bits)
+  float4* blk = gp + P;     // [nb] block spheres (centre, radius)
+  float4* sup = blk + nb;   // [nsb] super-block spheres
+  __shared__ int s_item;
+  const int nqi = (P + kPrThreads - 1) / kPrThreads;
+  const int items = *perm_ok ? *nsym * nqi : 0;  // no Morton orders: k_add_rows scans in full
+  const int t = threadIdx.x;
+  for (;;) {
+    __syncthreads();
+    if (t == 0) s_item = atomicAdd(queue, 1);
+    __syncthreads();
+    const int item = s_item;
+    if (item >= items) break;
+    const int slot = item / nqi, qi = item % nqi;
+    const int n = sym_rows[slot];
+    const int cls = rcls[n];
+    const int PC = 4 * C;
+    const float* tq = target + (size_t)n * PC + 4 * cls;
+    const float* pq = pred + (size_t)n * PC + 4 * cls;
+    float Rg[9], Rp[9];
+    quat2rot(tq[0], tq[1], tq[2], tq[3], Rg);
+    quat2rot(pq[0], pq[1], pq[2], pq[3], Rp);
+    const float* pts = points + (size_t)cls * P * 3;
+    const int32_t* pm = perm + (size_t)cls * P;
+#pragma unroll 4
+    for (int i = t; i < P; i += kPrThreads) {
+      const int j = pm[i];
+      const float X0 = pts[j * 3 + 0], X1 = pts[j * 3 + 1], X2 = pts[j * 3 + 2];
+      gp[i] = make_float4(Rg[0] * X0 + Rg[1] * X1 + Rg[2] * X2, Rg[3] * X0 + Rg[4] * X1 + Rg[5] * X2,
+                          Rg[6] * X0 + Rg[7] * X1 + Rg[8] * X2, __int_as_float(j));
+    }
+    __syncthreads();
+    for (int b = t; b < nb; b += blockDim.x) {  // block spheres
+      const int j0 = b * kPrBlk, j1 = min(j0 + kPrBlk, P);
+      float sx = 0.f, sy = 0.f, sz = 0.f;
+      for (int j = j0; j < j1; j++) {
+        sx += gp[j].x;
+        sy += gp[j].y;
+        sz += gp[j].z;
+      }
+      const float inv = 1.f / (float)(j1 - j0);
+      const float mx = sx * inv, my = sy * inv, mz = sz * inv;
+      float r = INFINITY;  // a non-finite point (or an overflowing sum): never skipped
+      if (isfinite(mx) && isfinite(my) && isfinite(mz)) {
+        float r2 = 0.f;
+        for (int j = j0; j < j1; j++) r2 = fmaxf(r2, fl_dist(gp[j].x, gp[j].y, gp[j].z, mx, my, mz));
+        if (isfinite(r2)) r = sqrtf(r2) * 1.0001f + 1e-18f;
+      }
+      blk[b] = make_float4(mx, my, mz, r);
+    }
+    __syncthreads();
+    for (int sb = t; sb < nsb; sb += blockDim.x) {  // super-block spheres over the blocks' spheres
+      const int b0 = sb * kPrSup, b1 = min(b0 + kPrSup, nb);
+      float sx = 0.f, sy = 0.f, sz = 0.f;
+      for (int b = b0; b < b1; b++) {
+        sx += blk[b].x;
+        sy += blk[b].y;
+        sz += blk[b].z;
+      }
+      const float inv = 1.f / (float)(b1 - b0);
+      const float mx = sx * inv, my = sy * inv, mz = sz * inv;
+      float r = 0.f;
+      for (int b = b0; b < b1; b++)
+        r = fmaxf(r, sqrtf(fl_dist(blk[b].x, blk[b].y, blk[b].z, mx, my, mz)) * 1.0001f + blk[b].w);
+      if (!(isfinite(mx) && isfinite(my) && isfinite(mz) && isfinite(r))) r = INFINITY;
+      for (int b = b0; b < b1; b++)
+        if (!(blk[b].w < INFINITY)) r = INFINITY;  // (fmaxf would drop a NaN radius)
+      sup[sb] = make_float4(mx, my, mz, r + 1e-18f);
+    }
+    __syncthreads();
+    const int qpos = qi * kPrThreads + t;
+    const bool valid = qpos < P;
+    if (__ballot(valid) == 0ull) continue;  // a wave with no query of this item (the loop head syncs)
+    const int p = pm[valid ? qpos : 0];
+    const float X0 = pts[p * 3 + 0], X1 = pts[p * 3 + 1], X2 = pts[p * 3 + 2];
+    const float qx = Rp[0] * X0 + Rp[1] * X1 + Rp[2] * X2;  // k_add_rows' query expression
+    const float qy = Rp[3] * X0 + Rp[4] * X1 + Rp[5] * X2;
+    const float qz = Rp[6] * X0 + Rp[7] * X1 + Rp[8] * X2;
+    float dmin = FLT_MAX;  // k_add_rows' start value: strict <, so a distance of FLT_MAX never wins
+    int best = -1;         // the model index of the nearest point so far
+    // exact distances to block b's points, first-minimum update (lowest model
+    // index among equal minima: the blocks arrive out of index order)
+    auto scan_block = [&](int b) {
+      const int j0 = b * kPrBlk;
+      float4 c[kPrBlk];
+      float d[kPrBlk];
+#pragma unroll
+      for (int e = 0; e < kPrBlk; e++) {
+        c[e] = gp[min(j0 + e, P - 1)];
+        d[e] = j0 + e < P ? fl_dist(qx, qy, qz, c[e].x, c[e].y, c[e].z) : INFINITY;
+      }
+      float bm = fminf(d[0], d[1]);  // NaN never wins (fminf drops it, the strict < below too)
+#pragma unroll
+      for (int e = 2; e < kPrBlk; e += 2) bm = fminf(bm, fminf(d[e], d[e + 1]));
+      if (bm < dmin || (bm == dmin && best >= 0)) {
+        int bi = 0x7fffffff;
+#pragma unroll
+        for (int e = 0; e < kPrBlk; e++) {
+          const int j = __float_as_int(c[e].w);
+          if (d[e] == bm && j < bi) bi = j;
+        }
+        if (bm < dmin) {
+          dmin = bm;
+          best = bi;
+        } else if (bi < best) {
+          best = bi;
+        }
+      }
+    };
+    // seed: the block nearest the query (by centre) inside the super-block
+    // nearest the query, scanned exactly -- dmin starts near its final value
+    {
+      float bd = INFINITY;
+      int bsel = 0;
+      for (int sb = 0; sb < nsb; sb++) {
+        const float4 m = sup[sb];
+        const float d2 = fl_dist(qx, qy, qz, m.x, m.y, m.z);
+        if (d2 < bd) {
+          bd = d2;
+          bsel = sb;
+        }
+      }
+      bd = INFINITY;
+      int b0 = bsel * kPrSup, bpick = b0;
+      for (int b = b0; b < min(b0 + kPrSup, nb); b++) {  // per-lane reads (each lane its own super-block)
+        const float4 m = blk[b];
+        const float d2 = fl_dist(qx, qy, qz, m.x, m.y, m.z);
+        if (d2 < bd) {
+          bd = d2;
+          bpick = b;
+        }
+      }
+      if (valid) scan_block(bpick);
+    }
+    // s = sqrt(dmin) padded: a sphere (centre at fl_dist d2, radius r) can
+    // hold no point at a distance <= dmin when d2 (1 - 3e-4) > ((r + s +
+    // 1e-18)^2 (1 + 1e-4)) -- sqrt-free, with slack far above fp32 rounding;
+    // an infinite radius or s (no finite distance yet) and a NaN never skip
+    float dlast = dmin, s_ = sqrtf(dmin) * 1.0001f;
+    int nscan = 0;
+    auto far_from = [&](const float4& m) {
+#ifdef ADD_PR_NOPRUNE  // timing ablation: visit every block
+      return m.w < -1.f;
+#endif
+      const float d2 = fl_dist(qx, qy, qz, m.x, m.y, m.z);
+      const float rr = m.w + s_ + 1e-18f;
+      return d2 * 0.9997f > rr * rr * 1.0001f;
+    };
+#ifdef ADD_PR_STAGE_ONLY  // timing ablation (wrong results): staging and seeding only
+    if (valid) nearest[(size_t)slot * P + p] = best;
+    continue;
+#endif
+    for (int sb = 0; sb < nsb; sb++) {
+      if (dmin != dlast) {
+        dlast = dmin;
+        s_ = sqrtf(dmin) * 1.0001f;
+      }
+      if (__ballot(valid && !far_from(sup[sb])) == 0ull) continue;
+      const int b1 = min(sb * kPrSup + kPrSup, nb);
+      for (int b = sb * kPrSup; b < b1; b++) {
+        if (dmin != dlast) {
+          dlast = dmin;
+          s_ = sqrtf(dmin) * 1.0001f;
+        }
+        if (__ballot(valid && !far_from(blk[b])) == 0ull) continue;
+        scan_block(b);
+        nscan++;
+      }
+    }
+    if (pcnn::lane_id() == 0) {  // per wave: blocks scanned of the blocks held (a no-op for the result)
+      atomicAdd(stats, nscan);
+      atomicAdd(stats + 1, nb);
+    }
+    if (valid) nearest[(size_t)slot * P + p] = best;
+  }
+}
+
 // Row classes once (first class with weight > 0, cu.cc:47-52) and the
 // ascending list of symmetric rows (ballot scan, one workgroup: deterministic).
 __global__ void __launch_bounds__(1024) k_add_prep(const float* __restrict__ weight, const float* __restrict__ symmetry,
                                                     int R_cap, const int32_t* __restrict__ num_rois_dev, int C,
                                                     int32_t* __restrict__ rcls, int32_t* __restrict__ sym_rows,
-                                                    int32_t* __restrict__ nsym, int32_t* __restrict__ queue) {
+                                                    int32_t* __restrict__ nsym, int32_t* __restrict__ queue,
+                                                    int32_t* __restrict__ squeue, int32_t* __restrict__ perm_ok,
+                                                    int order, int32_t* __restrict__ stats) {
   __shared__ int wcount[16];
   __shared__ int base;
   const int R = rows_of(num_rois_dev, R_cap);
@@ -456,6 +779,9 @@ __global__ void __launch_bounds__(1024) k_add_prep(const float* __restrict__ wei
   if (threadIdx.x == 0) {
     *nsym = base;
     *queue = 0;
+    *squeue = 0;
+    *perm_ok = order;
+    stats[0] = stats[1] = 0;
   }
 }
 
@@ -491,6 +817,45 @@ __global__ void __launch_bounds__(256) k_add_finish_rows(int R_cap, const int32_
   const int R = rows_of(num_rois_dev, R_cap);
   const int n = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   finish_row(n, R, C, nchunk, rcls, partial, row_loss, bottom_diff, pcnn::lane_id());
+}
+
+// k_add_finish_rows + the pose head's backward in one pass (the step's fused
+// tail, pcnn_add_loss_fwd_head_bwd): the row's four gradient sums go straight
+// into d pred (times the ADD gradient op's top_diff[0], cu.cc:346-354) and on
+// through tanh * poses_weight -> l2_normalize (pose_head.hip k_head_bwd, the
+// same helper), so the d_pred row is never re-read.  4 C <= 256.
+__global__ void __launch_bounds__(256) k_add_finish_head(int R_cap, const int32_t* __restrict__ num_rois_dev, int C,
+                                                          int nchunk, const int32_t* __restrict__ rcls,
+                                                          const float* __restrict__ partial,
+                                                          float* __restrict__ row_loss,
+                                                          float* __restrict__ bottom_diff,
+                                                          const float* __restrict__ t_in,
+                                                          const float* __restrict__ pw,
+                                                          const float* __restrict__ pred,
+                                                          const float* __restrict__ dscale, float* __restrict__ dy8) {
+  const int R = rows_of(num_rois_dev, R_cap);
+  const int n = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = pcnn::lane_id();
+  if (n >= R) return;
+  const int cls = rcls[n];
+  float s[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int k = lane; k < nchunk; k += 64)
+    for (int q = 0; q < 5; q++) s[q] += partial[((size_t)n * nchunk + k) * 5 + q];
+#pragma unroll
+  for (int q = 0; q < 5; q++) s[q] = pcnn::wave_sum(s[q]);
+  const int PC = 4 * C;
+  const float g = dscale ? dscale[0] : 1.f;
+  float dp[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const int col = lane + 64 * k;
+    float vv = 0.f;
+    if (cls >= 0 && col >= 4 * cls && col < 4 * cls + 4) vv = s[1 + col - 4 * cls];
+    if (col < PC) bottom_diff[(size_t)n * PC + col] = vv;
+    dp[k] = col < PC ? g * vv : 0.f;
+  }
+  if (lane == 0) row_loss[n] = cls >= 0 ? s[0] : 0.f;
+  pcnn_head::head_bwd_row(dp, t_in, pw, pred, n, PC, lane, dy8);
 }
 
 // Scalar loss: fixed-order sum of the row losses (thrust::reduce, cu.cc:333-334).
@@ -534,12 +899,106 @@ extern "C" int pcnn_div_rn_check(const float* x, float b, int n, int dbl, float*
   return PCNN_OK;
 }
 
-extern "C" size_t pcnn_add_loss_workspace_size(int R_cap, int C, int P) {
-  (void)C;
+// The loss's workspace, carved the same way by every entry point.  The
+// pruned search's Morton orders (C x P) and nearest indices (R_cap x P) are
+// there whenever P <= kPrMaxP.
+struct AddWs {
+  float* partial;
+  int32_t *rcls, *sym_rows, *nsym, *queue, *squeue;
+  float* row_loss;
+  int32_t *perm, *nearest;
+  int32_t* perm_ok;  // device flag: the Morton orders were built by this call's prep
+  int32_t* stats;    // the search's [blocks scanned, blocks held] over the call's queries (diagnostics)
+};
+static AddWs add_carve(void* workspace, int R_cap, int C, int P, size_t* bytes) {
   const int nchunk = (P + kPts - 1) / kPts;
   const size_t R = (size_t)(R_cap > 0 ? R_cap : 1);
-  return pcnn::align_up(R * nchunk * 5 * sizeof(float), 256) + 2 * pcnn::align_up(R * sizeof(int32_t), 256) +
-         pcnn::align_up(R * sizeof(float), 256) + 3 * 256;
+  pcnn::Carve cv(workspace);
+  AddWs w;
+  w.partial = cv.take<float>(R * nchunk * 5);
+  w.rcls = cv.take<int32_t>(R);
+  w.sym_rows = cv.take<int32_t>(R);
+  w.nsym = cv.take<int32_t>(1);
+  w.queue = cv.take<int32_t>(1);
+  w.row_loss = cv.take<float>(R);
+  w.squeue = cv.take<int32_t>(1);
+  w.perm_ok = cv.take<int32_t>(1);
+  w.stats = cv.take<int32_t>(2);
+  const bool pr = P <= kPrMaxP;
+  w.perm = pr ? cv.take<int32_t>((size_t)(C > 0 ? C : 1) * P) : nullptr;
+  w.nearest = pr ? cv.take<int32_t>(R * P) : nullptr;
+  if (bytes) *bytes = cv.off + 256;
+  return w;
+}
+
+// Which nearest-point search the symmetric rows use: the full O(P^2) scan
+// (the default) or the pruned one (PCNN_ADD_SEARCH=pruned, P <= kPrMaxP; the
+// same bits).  Measured on the bench's rows (round 6, scripts/add_bench.py):
+// the pruned search visits 16 % of the blocks (13 % for near-correct
+// predictions) but its per-block sphere tests are a latency-bound chain of
+// LDS read -> distance -> ballot -> branch, so the op runs 314 us against the
+// full scan's 212 us (and 132 us with the search ablated): not the default.
+static bool add_pruned(int P) {
+  if (P > kPrMaxP) return false;
+  const char* e = getenv("PCNN_ADD_SEARCH");
+  return e && strcmp(e, "pruned") == 0;
+}
+
+// Byte offsets inside the workspace of the search's diagnostics (tests and
+// benches): what = 0 the Morton orders (C x P int32), 1 the [scanned, held]
+// block counters of the last search.  -1 when the pruned search is off (P > kPrMaxP).
+extern "C" long pcnn_add_loss_ws_offset(int R_cap, int C, int P, int what) {
+  char* const base = (char*)(uintptr_t)4096;  // any aligned non-null base: only the offsets are used
+  const AddWs w = add_carve(base, R_cap, C, P, nullptr);
+  const int32_t* q = what == 0 ? w.perm : what == 1 ? w.stats : nullptr;
+  if (!q || !w.perm) return -1;
+  return (long)((const char*)q - base);
+}
+
+extern "C" size_t pcnn_add_loss_workspace_size(int R_cap, int C, int P) {
+  size_t b = 0;
+  (void)add_carve(nullptr, R_cap, C, P, &b);
+  return b;
+}
+
+// the row classification, and the symmetric classes' Morton orders (pruned search)
+static void add_launch_prep(const AddWs& w, const float* weight, const float* symmetry, const float* points,
+                            int R_cap, const int32_t* num_rois_dev, int C, int P, hipStream_t st) {
+  const int order = w.perm && points && add_pruned(P) ? 1 : 0;
+  hipLaunchKernelGGL(k_add_prep, dim3(1), dim3(1024), 0, st, weight, symmetry, R_cap, num_rois_dev, C, w.rcls,
+                     w.sym_rows, w.nsym, w.queue, w.squeue, w.perm_ok, order, w.stats);
+  if (order) hipLaunchKernelGGL(k_add_order, dim3(C), dim3(1024), 0, st, points, symmetry, P, w.perm);
+}
+
+// the per-point sums: the symmetric rows' pruned nearest-point search first
+// (when selected), then the persistent (row, chunk) queue of k_add_rows
+static int add_launch_rows(const AddWs& w, const float* pred, const float* target, const float* weight,
+                           const float* points, const float* symmetry, int R_cap, const int32_t* num_rois_dev,
+                           int C, int P, float margin, int loss_norm_rows, const int32_t* loss_norm_rows_dev,
+                           hipStream_t st) {
+  const int nchunk = (P + kPts - 1) / kPts;
+  const bool pr = add_pruned(P);
+  if (pr) {
+    const int nb = (P + kPrBlk - 1) / kPrBlk, nsb = (nb + kPrSup - 1) / kPrSup;
+    const size_t lds = (size_t)(P + nb + nsb) * sizeof(float4);
+    if (lds > 64 * 1024 && hipFuncSetAttribute((const void*)k_add_search, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                               (int)lds) != hipSuccess)
+      return PCNN_EHIP;
+    const long items = (long)R_cap * ((P + kPrThreads - 1) / kPrThreads);
+    const int grid = (int)(items < ADD_PR_GRID ? items : ADD_PR_GRID);
+    hipLaunchKernelGGL(k_add_search, dim3(grid), dim3(kPrThreads), lds, st, pred, target, points, C, P, w.rcls,
+                       w.sym_rows, w.nsym, w.perm, w.perm_ok, w.squeue, w.nearest, w.stats);
+  }
+  // one persistent grid: symmetric (row, chunk) items of the device-side list, then the plain rows
+  const long sym_items = (long)R_cap * nchunk + R_cap;
+  const int sym_grid = (int)(sym_items < ADD_GRID ? sym_items : ADD_GRID);
+  // (dynamic LDS for the full scan's staging either way: a prep without the
+  // points leaves perm_ok 0 and k_add_rows then scans)
+  hipLaunchKernelGGL(k_add_rows, dim3(sym_grid), dim3(kSymThreads), (size_t)P * sizeof(float4), st, pred,
+                     target, weight, points, symmetry, R_cap, num_rois_dev, C, P, margin, loss_norm_rows,
+                     loss_norm_rows_dev, nchunk, w.rcls, w.sym_rows, w.nsym, w.queue, w.partial,
+                     pr ? w.nearest : nullptr, w.perm_ok);
+  return PCNN_OK;
 }
 
 static int add_loss_fwd(const float* pred, const float* target, const float* weight, const float* points,
@@ -551,25 +1010,14 @@ static int add_loss_fwd(const float* pred, const float* target, const float* wei
   if (workspace_bytes < pcnn_add_loss_workspace_size(R_cap, C, P)) return PCNN_ECAPACITY;
   hipStream_t st = (hipStream_t)stream;
   const int nchunk = (P + kPts - 1) / kPts;
-  pcnn::Carve cv(workspace);
-  float* partial = cv.take<float>((size_t)R_cap * nchunk * 5);
-  int32_t* rcls = cv.take<int32_t>(R_cap);
-  int32_t* sym_rows = cv.take<int32_t>(R_cap);
-  int32_t* nsym = cv.take<int32_t>(1);
-  int32_t* queue = cv.take<int32_t>(1);
-  float* row_loss = cv.take<float>(R_cap);
-  if (!prepared)
-    hipLaunchKernelGGL(k_add_prep, dim3(1), dim3(1024), 0, st, weight, symmetry, R_cap, num_rois_dev, C, rcls,
-                       sym_rows, nsym, queue);
-  // one persistent grid: symmetric (row, chunk) items of the device-side list, then the plain rows
-  const long sym_items = (long)R_cap * nchunk + R_cap;  // symmetric (row, chunk) items, then plain rows
-  const int sym_grid = (int)(sym_items < ADD_GRID ? sym_items : ADD_GRID);
-  hipLaunchKernelGGL(k_add_rows, dim3(sym_grid), dim3(kSymThreads), (size_t)P * sizeof(float4), st, pred,
-                     target, weight, points, symmetry, R_cap, num_rois_dev, C, P, margin, loss_norm_rows,
-                     loss_norm_rows_dev, nchunk, rcls, sym_rows, nsym, queue, partial);
+  const AddWs w = add_carve(workspace, R_cap, C, P, nullptr);
+  if (!prepared) add_launch_prep(w, weight, symmetry, points, R_cap, num_rois_dev, C, P, st);
+  const int rc = add_launch_rows(w, pred, target, weight, points, symmetry, R_cap, num_rois_dev, C, P, margin,
+                                 loss_norm_rows, loss_norm_rows_dev, st);
+  if (rc != PCNN_OK) return rc;
   hipLaunchKernelGGL(k_add_finish_rows, dim3((R_cap + 3) / 4), dim3(256), 0, st, R_cap, num_rois_dev, C, nchunk,
-                     rcls, partial, row_loss, bottom_diff);
-  hipLaunchKernelGGL(k_add_total, dim3(1), dim3(1024), 0, st, R_cap, num_rois_dev, row_loss, loss);
+                     w.rcls, w.partial, w.row_loss, bottom_diff);
+  hipLaunchKernelGGL(k_add_total, dim3(1), dim3(1024), 0, st, R_cap, num_rois_dev, w.row_loss, loss);
   PCNN_CHECK_LAUNCH();
   return PCNN_OK;
 }
@@ -582,22 +1030,30 @@ extern "C" int pcnn_add_loss_fwd(const float* pred, const float* target, const f
                       loss_norm_rows_dev, loss, bottom_diff, workspace, workspace_bytes, false, stream);
 }
 
+extern "C" int pcnn_add_loss_prep_points(const float* weight, const float* symmetry, const float* points, int R_cap,
+                                         const int32_t* num_rois_dev, int C, int P, void* workspace,
+                                         size_t workspace_bytes, void* stream);
+
 // The row classification of pcnn_add_loss_fwd on its own: it reads only the
-// weights (the Hough op's targets), so a caller can run it as soon as they
-// exist, on another stream, off the chain that produces the predictions.
+// weights (the Hough op's targets) and the model points, so a caller can run
+// it as soon as they exist, on another stream, off the chain that produces
+// the predictions.
 extern "C" int pcnn_add_loss_prep(const float* weight, const float* symmetry, int R_cap, const int32_t* num_rois_dev,
                                   int C, int P, void* workspace, size_t workspace_bytes, void* stream) {
+  return pcnn_add_loss_prep_points(weight, symmetry, nullptr, R_cap, num_rois_dev, C, P, workspace, workspace_bytes,
+                                   stream);
+}
+
+// ... with the model points: the symmetric classes' Morton orders for the
+// pruned search are built here too (without the points, the prepared loss
+// uses the full scan).
+extern "C" int pcnn_add_loss_prep_points(const float* weight, const float* symmetry, const float* points, int R_cap,
+                                         const int32_t* num_rois_dev, int C, int P, void* workspace,
+                                         size_t workspace_bytes, void* stream) {
   PCNN_REQUIRE(weight && symmetry && workspace && R_cap > 0 && C > 0 && P > 0 && P <= kMaxPointsLds);
   if (workspace_bytes < pcnn_add_loss_workspace_size(R_cap, C, P)) return PCNN_ECAPACITY;
-  const int nchunk = (P + kPts - 1) / kPts;
-  pcnn::Carve cv(workspace);
-  (void)cv.take<float>((size_t)R_cap * nchunk * 5);
-  int32_t* rcls = cv.take<int32_t>(R_cap);
-  int32_t* sym_rows = cv.take<int32_t>(R_cap);
-  int32_t* nsym = cv.take<int32_t>(1);
-  int32_t* queue = cv.take<int32_t>(1);
-  hipLaunchKernelGGL(k_add_prep, dim3(1), dim3(1024), 0, (hipStream_t)stream, weight, symmetry, R_cap, num_rois_dev,
-                     C, rcls, sym_rows, nsym, queue);
+  const AddWs w = add_carve(workspace, R_cap, C, P, nullptr);
+  add_launch_prep(w, weight, symmetry, points, R_cap, num_rois_dev, C, P, (hipStream_t)stream);
   PCNN_CHECK_LAUNCH();
   return PCNN_OK;
 }
@@ -610,6 +1066,48 @@ extern "C" int pcnn_add_loss_fwd_prepared(const float* pred, const float* target
                                           void* stream) {
   return add_loss_fwd(pred, target, weight, points, symmetry, R_cap, num_rois_dev, C, P, margin, loss_norm_rows,
                       loss_norm_rows_dev, loss, bottom_diff, workspace, workspace_bytes, true, stream);
+}
+
+// The loss with the step's backward tail fused in (prepared rows only): the
+// per-point sums (k_add_rows), then one pass that finishes each row's
+// bottom_diff and runs the pose head's backward on it into d_y8
+// (pcnn_pose_head_bwd with d_pred = bottom_diff, d_pred_scale the ADD
+// gradient op's top_diff[0]: the same bits as the two separate launches).
+// The scalar loss is left to pcnn_add_loss_total on the same workspace --
+// nothing on the backward chain reads it, so a caller can run it on another
+// stream after this call.  4 C <= 256.
+extern "C" int pcnn_add_loss_fwd_head_bwd(const float* pred, const float* target, const float* weight,
+                                          const float* points, const float* symmetry, int R_cap,
+                                          const int32_t* num_rois_dev, int C, int P, float margin,
+                                          int loss_norm_rows, const int32_t* loss_norm_rows_dev, float* bottom_diff,
+                                          void* workspace, size_t workspace_bytes, const float* tanh_out,
+                                          const float* d_pred_scale, float* d_y8, void* stream) {
+  PCNN_REQUIRE(pred && target && weight && points && symmetry && bottom_diff && workspace && tanh_out && d_y8);
+  PCNN_REQUIRE(R_cap > 0 && C > 0 && 4 * C <= 256 && P > 0 && P <= kMaxPointsLds);
+  if (workspace_bytes < pcnn_add_loss_workspace_size(R_cap, C, P)) return PCNN_ECAPACITY;
+  hipStream_t st = (hipStream_t)stream;
+  const int nchunk = (P + kPts - 1) / kPts;
+  const AddWs w = add_carve(workspace, R_cap, C, P, nullptr);
+  const int rc = add_launch_rows(w, pred, target, weight, points, symmetry, R_cap, num_rois_dev, C, P, margin,
+                                 loss_norm_rows, loss_norm_rows_dev, st);
+  if (rc != PCNN_OK) return rc;
+  hipLaunchKernelGGL(k_add_finish_head, dim3((R_cap + 3) / 4), dim3(256), 0, st, R_cap, num_rois_dev, C, nchunk,
+                     w.rcls, w.partial, w.row_loss, bottom_diff, tanh_out, weight, pred, d_pred_scale, d_y8);
+  PCNN_CHECK_LAUNCH();
+  return PCNN_OK;
+}
+
+// The scalar loss of a pcnn_add_loss_fwd_head_bwd call (the row losses it left
+// in the workspace, summed in the fixed order of pcnn_add_loss_fwd).
+extern "C" int pcnn_add_loss_total(int R_cap, const int32_t* num_rois_dev, int C, int P, const void* workspace,
+                                   size_t workspace_bytes, float* loss, void* stream) {
+  PCNN_REQUIRE(workspace && loss && R_cap > 0 && C > 0 && P > 0);
+  if (workspace_bytes < pcnn_add_loss_workspace_size(R_cap, C, P)) return PCNN_ECAPACITY;
+  const AddWs w = add_carve(const_cast<void*>(workspace), R_cap, C, P, nullptr);
+  hipLaunchKernelGGL(k_add_total, dim3(1), dim3(1024), 0, (hipStream_t)stream, R_cap, num_rois_dev, w.row_loss,
+                     loss);
+  PCNN_CHECK_LAUNCH();
+  return PCNN_OK;
 }
 
 extern "C" int pcnn_add_loss_bwd(const float* top_diff, const float* bottom_diff, int n,

@@ -16,6 +16,7 @@
 // fixed order by a second kernel that also applies the epilogue (bit-stable
 // across runs).  The pool5 + pool4 addition is fused into the A-tile load.
 #include "gemm_common.h"
+#include "head_common.h"
 #include "pcnn_philox.h"
 #include <math.h>
 #include <stdlib.h>
@@ -701,33 +702,13 @@ __global__ void __launch_bounds__(256) k_head_bwd(const float* __restrict__ dpre
   const int row = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int lane = pcnn::lane_id();
   if (row >= R) return;
-  float ss = 0.f, dot = 0.f;
+  float dp[4];
 #pragma unroll
   for (int k = 0; k < 4; k++) {
     const int c = lane + 64 * k;
-    if (c < D) {
-      const float mv = t_in[(size_t)row * D + c] * pw[(size_t)row * D + c];
-      ss += mv * mv;
-      dot += pred[(size_t)row * D + c] * (g * dpred[(size_t)row * D + c]);
-    }
+    dp[k] = c < D ? g * dpred[(size_t)row * D + c] : 0.f;
   }
-  ss = pcnn::wave_sum(ss);
-  dot = pcnn::wave_sum(dot);
-  const bool clamp = !(ss > 1e-12f);
-  const float inv = 1.f / sqrtf(fmaxf(ss, 1e-12f));
-#pragma unroll
-  for (int k = 0; k < 4; k++) {
-    const int c = lane + 64 * k;
-    if (c < D) {
-      const size_t o = (size_t)row * D + c;
-      // d/dm of m * rsqrt(max(sum m^2, eps))
-      const float dp = g * dpred[o];
-      const float dm = clamp ? dp * inv : (dp - pred[o] * dot) * inv;
-      const float dt = dm * pw[o];
-      const float t = t_in[o];
-      dy8[o] = dt * (1.f - t * t);
-    }
-  }
+  pcnn_head::head_bwd_row(dp, t_in, pw, pred, row, D, lane, dy8);
 }
 
 }  // namespace

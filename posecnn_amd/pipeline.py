@@ -44,7 +44,7 @@ class PoseStep:
                  is_train=1, skip_pixels=10, vote_threshold=-1.0, vote_percentage=0.02, margin=0.01,
                  global_batch=None, batch_base=0, weights=None, dist=None, backward=True, precision=2,
                  overlap_weight_grads=True, pixel_argmax=True, keep_prob=None, drop_seed=0x5EED, side_prep=True,
-                 drop_in_reduce=True, pipeline=False, prefetch_at="loss"):
+                 drop_in_reduce=True, pipeline=False, prefetch_at="loss", fuse_loss_tail=True):
         self.B, self.H, self.W, self.C = B, H, W, num_classes
         self.dev = device
         self.is_train, self.skip, self.vthr, self.vper, self.margin = is_train, skip_pixels, vote_threshold, \
@@ -84,6 +84,9 @@ class PoseStep:
         # pipeline=True: two sets; step(inputs, next_inputs) runs the forward /
         # backward of `inputs` on one while the vote, RoI-pool forward and ADD
         # row classification of `next_inputs` fill the other on a third stream
+        # the loss's row tail + the pose head's backward in one pass, the scalar
+        # loss on the side stream (step() only; False: separate launches, A/B)
+        self.fuse_loss_tail = fuse_loss_tail
         self.pipeline = bool(pipeline)
         self._sets = [minibatch_set() for _ in range(2 if self.pipeline else 1)]
         self._cur = 0           # the set the step's forward / backward uses (and the attributes show)
@@ -206,7 +209,7 @@ class PoseStep:
                 side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(stream or side or torch.cuda.current_stream()):
             adl.average_distance_loss_prep(h["weight"], symmetry, points.shape[1], st["add_ws"],
-                                           num_rois=h["num_rois"][1:2])
+                                           num_rois=h["num_rois"][1:2], points=points)
         st["prepped"] = "side" if side is not None else "stream"
 
     def pool_fwd(self, conv4, conv5, s=None):
@@ -360,6 +363,23 @@ class PoseStep:
             # the previous step's in-place loss all-reduce must be done before
             # the loss kernel rewrites self.loss (its handle orders it on this stream)
             self._wait("loss")
+            side = self.side_stream
+            self._head_bwd_done = fuse = (self.fuse_loss_tail and self._in_step and self.backward and
+                                          self.timer is None and side is not None and self.D <= 256)
+            if fuse:
+                # the loss's row tail and the pose head's backward in one pass
+                # (dY8 straight from the row sums), the scalar loss beside the
+                # backward on the side stream: nothing on the chain reads it
+                adl.average_distance_loss_head_bwd(self.pred, h["target"], h["weight"], points, symmetry,
+                                                   self.margin, self.t8, self.one, self.diff, self.dy8, st["add_ws"],
+                                                   num_rois=nr, loss_norm_rows_dev=self.norm_rows)
+                side.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(side):
+                    adl.average_distance_loss_total(CAP, self.C, points.shape[1], st["add_ws"], self.loss,
+                                                    num_rois=nr)
+                    if self.dist is not None:  # joined at the end of the step
+                        self._pending["loss"] = self.dist.all_reduce(self.loss, async_op=True)
+                return self.loss
             adl.average_distance_loss(self.pred, h["target"], h["weight"], points, symmetry, self.margin,
                                       num_rois=nr, loss_norm_rows_dev=self.norm_rows, out=(self.loss, self.diff),
                                       workspace=st["add_ws"], prepared=True)
@@ -403,10 +423,13 @@ class PoseStep:
                     ph.colsum(dY, g["b" + name[1:]], M_dev=nr)
                     self._g(f"fc{name[1:]}_dw", X, dY, g[name], a_trans=1, K_dev=nr, M=M, N=N, K=K_loc)
 
-        with self._t("add_loss_head_bwd"):
-            # average_distance_loss_grad (top_diff[0] * bottom_diff) folded into
-            # the head backward: one pass over the (R, 4C) rows instead of two
-            ph.head_bwd(self.diff, self.t8, h["weight"], self.pred, self.dy8, num_rois=nr, d_pred_scale=self.one)
+        if not getattr(self, "_head_bwd_done", False):  # (fused into the loss's row tail inside step())
+            with self._t("add_loss_head_bwd"):
+                # average_distance_loss_grad (top_diff[0] * bottom_diff) folded into
+                # the head backward: one pass over the (R, 4C) rows instead of two
+                ph.head_bwd(self.diff, self.t8, h["weight"], self.pred, self.dy8, num_rois=nr,
+                            d_pred_scale=self.one)
+        self._head_bwd_done = False
         if self.prefetch_at == "bwd":
             self._prefetch()
         with self._t("gemm_fc8_fc7_dw_bias"):  # fc8 weight / bias gradients

@@ -1,5 +1,7 @@
 """GPU parity for RoI pooling, ADD loss, backprojection and the pose-head GEMM
 against the oracle (or an fp64 numpy reference for the GEMM)."""
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -580,3 +582,132 @@ def test_add_loss_division_correctly_rounded(hip, dbl):
         assert rc == 0
         ref = (x.astype(np.float64) / np.float64(b)).astype(np.float32) if dbl else x / b
         np.testing.assert_array_equal(out.cpu().numpy(), ref, err_msg=f"R={R}")
+
+
+def _add_modes(args, **kw):
+    """The loss with the pruned ADD-S search (default) and the full scan
+    (PCNN_ADD_SEARCH=full), on the same inputs."""
+    out = []
+    for mode in ("pruned", "full"):
+        os.environ["PCNN_ADD_SEARCH"] = mode
+        try:
+            loss, diff = adl.average_distance_loss(*args, **kw)
+            torch.cuda.synchronize()
+            out.append((loss.cpu().numpy(), diff.cpu().numpy()))
+        finally:
+            os.environ.pop("PCNN_ADD_SEARCH", None)
+    return out
+
+
+@pytest.mark.parametrize("case", ["random", "near", "ties", "small_p", "p4096", "p4100", "nonfinite", "scaled"])
+def test_add_s_pruned_search_matches_full_scan(hip, case):
+    """The pruned nearest-point search (PCNN_ADD_SEARCH=pruned: Morton-ordered
+    blocks with bounding spheres, wave-uniform skips; k_add_search) against
+    the reference's full O(P^2) scan (the default): loss and bottom_diff bit for bit -- random and near-correct
+    predictions, exact distance ties on a lattice, P below one block row and
+    at / past the pruned path's 4096 limit, non-finite rows and points, and
+    unnormalised quaternions."""
+    rng = np.random.default_rng({"random": 1, "near": 2, "ties": 3, "small_p": 4, "p4096": 5, "p4100": 6,
+                                 "nonfinite": 7, "scaled": 8}[case])
+    C, R = 4, 37
+    P = {"small_p": 13, "p4096": 4096, "p4100": 4100}.get(case, 2620)
+    if case == "ties":
+        pts = rng.integers(-3, 4, size=(C, P, 3)).astype(np.float32)
+    else:
+        pts = (rng.normal(size=(C, P, 3)) * np.array([1.0, 2.0, 0.5])).astype(np.float32)
+    sym = np.array([0, 1, 1, 0], np.float32)
+    pred = np.zeros((R, 4 * C), np.float32)
+    target = np.zeros((R, 4 * C), np.float32)
+    weight = np.zeros((R, 4 * C), np.float32)
+    for r in range(R):
+        c = 1 + r % 3
+        qt = rng.normal(size=4)
+        qt /= np.linalg.norm(qt)
+        qp = rng.normal(size=4)
+        qp /= np.linalg.norm(qp)
+        if case == "near":
+            qp = qt + rng.normal(size=4) * 0.02
+            qp /= np.linalg.norm(qp)
+        if case == "ties":
+            qt = np.array([1, 0, 0, 1.0]) if r % 2 else np.array([0, 0, 1, 1.0])
+            qp = np.array([1, 0, 0, 0.0]) if r % 3 else np.array([0, 1, 0, 0.0])
+        if case == "scaled":
+            qp *= 1.0 + r * 0.3
+            qt *= 0.7
+        pred[r, 4 * c:4 * c + 4] = qp
+        target[r, 4 * c:4 * c + 4] = qt
+        weight[r, 4 * c:4 * c + 4] = 1
+    if case == "nonfinite":
+        pred[4, 4 * 2] = np.nan       # symmetric rows (class 1 + r % 3) with a non-finite prediction
+        pred[6, 4 * 1 + 2] = np.inf
+        pts[2, 17] = np.nan
+        pts[1, 100] = np.inf
+    args = (T(pred), T(target), T(weight), T(pts), T(sym), 0.01)
+    (lp, dp), (lf, df) = _add_modes(args)
+    np.testing.assert_array_equal(lp, lf)
+    np.testing.assert_array_equal(dp, df)
+    # and through the prepared path (prep with the points on another stream)
+    ws = torch.empty(adl.workspace_bytes(R, C, P), dtype=torch.uint8, device=D)
+    side = torch.cuda.Stream()
+    os.environ["PCNN_ADD_SEARCH"] = "pruned"
+    try:
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            adl.average_distance_loss_prep(args[2], args[4], P, ws, points=args[3])
+        torch.cuda.current_stream().wait_stream(side)
+        l2, d2 = adl.average_distance_loss(*args, workspace=ws, prepared=True)
+        torch.cuda.synchronize()
+    finally:
+        os.environ.pop("PCNN_ADD_SEARCH", None)
+    np.testing.assert_array_equal(l2.cpu().numpy(), lf)
+    np.testing.assert_array_equal(d2.cpu().numpy(), df)
+
+
+def _morton_np(X):
+    """numpy restatement of k_add_order: 10-bit per-axis cell of the class's
+    bounding box, interleaved x0 y0 z0 x1 ..., ties by point index."""
+    lo, hi = X.min(0), X.max(0)
+    ext = (hi - lo).astype(np.float32)
+    f = np.where(ext > 0, (X - lo) / np.where(ext > 0, ext, 1) * np.float32(1023), 0).astype(np.float32)
+    q = np.where(f > 0, np.where(f < 1023, f.astype(np.int64), 1023), 0)
+    code = np.zeros(len(X), np.int64)
+    for b in range(10):
+        for a in range(3):
+            code |= ((q[:, a] >> b) & 1) << (3 * b + a)
+    return np.argsort(code * 8192 + np.arange(len(X)), kind="stable").astype(np.int32)
+
+
+def test_add_s_search_order_and_pruning(hip):
+    """The symmetric classes' Morton orders match the numpy restatement, and
+    on the bench's model points (YCB rescaled, random unit predictions) the
+    search scans a small part of the blocks -- the pruning is real."""
+    rng = np.random.default_rng(31)
+    C = 22
+    pts, sym = synth.rescaled_points(C)
+    P = pts.shape[1]
+    R = 40
+    pred = np.zeros((R, 4 * C), np.float32)
+    target = np.zeros((R, 4 * C), np.float32)
+    weight = np.zeros((R, 4 * C), np.float32)
+    scls = np.nonzero(sym)[0]
+    for r in range(R):
+        c = int(scls[r % len(scls)])
+        for arr in (pred, target):
+            q = rng.normal(size=4)
+            arr[r, 4 * c:4 * c + 4] = q / np.linalg.norm(q)
+        weight[r, 4 * c:4 * c + 4] = 1
+    args = (T(pred), T(target), T(weight), T(pts), T(sym), 0.01)
+    ws = torch.empty(adl.workspace_bytes(R, C, P), dtype=torch.uint8, device=D)
+    os.environ["PCNN_ADD_SEARCH"] = "pruned"
+    try:
+        adl.average_distance_loss_prep(args[2], args[4], P, ws, points=args[3])
+        adl.average_distance_loss(*args, workspace=ws, prepared=True)
+        torch.cuda.synchronize()
+    finally:
+        os.environ.pop("PCNN_ADD_SEARCH", None)
+    perm, stat = adl.search_diagnostics(ws, R, C, P)
+    for c in scls:
+        np.testing.assert_array_equal(perm[c].cpu().numpy(), _morton_np(pts[c]))
+    scanned, held = (int(v) for v in stat.cpu().numpy())
+    assert held == R * ((P + 63) // 64) * ((P + 7) // 8)
+    assert scanned < 0.35 * held, (scanned, held)

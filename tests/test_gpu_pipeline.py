@@ -38,7 +38,7 @@ def _snap(step):
                 weight=h["weight"][:n].clone(), pool=step.pool[:n].clone(), arg5=step.arg5[:n].clone(),
                 arg4=step.arg4[:n].clone(), loss=step.loss.clone(), diff=step.diff[:n].clone(),
                 drop6=step.drop6[:n].clone() if step.drop6 is not None else None, y7=step.y7[:n].clone(), dx=step.dx[:n].clone(),
-                dconv4=step.dconv4.clone(), dconv5=step.dconv5.clone(),
+                dconv4=step.dconv4.clone(), dconv5=step.dconv5.clone(), dy8=step.dy8[:n].clone(),
                 **{"g_" + k: v.clone() for k, v in step.grads.items()})
 
 
@@ -83,3 +83,19 @@ def test_pipelined_step_without_prefetch_and_mismatched_inputs(hip):
         assert torch.equal(ref[2][key], got[key]), key
     with pytest.raises(ValueError):
         PoseStep(B, H, W, C, D, channels=CH, units=UNITS, weights=ref_step.weights).step(batches[0], batches[1])
+
+
+def test_fused_loss_tail_bit_identical(hip):
+    """The loss's row tail fused with the pose head's backward (dY8 straight
+    from the row sums; the scalar loss on the side stream) against the
+    separate launches (pcnn_add_loss_fwd_prepared + pcnn_pose_head_bwd):
+    every output of two steps bit-identical."""
+    batches = _batches(2)
+    ref_step, ref = _run(batches, None, fuse_loss_tail=False)
+    _, got = _run(batches, ref_step.weights, fuse_loss_tail=True)
+    for k, (a, b) in enumerate(zip(ref, got)):
+        for key in a:
+            if key == "n" or a[key] is None:
+                assert a[key] == b[key]
+                continue
+            assert torch.equal(a[key], b[key]), f"step {k}: {key} differs"
