@@ -64,6 +64,9 @@ def parse(argv=None):
                         "synthetic minibatches")
     p.add_argument("--prefetch-at", choices=["loss", "bwd", "start"], default="start",
                    help="with --pipeline on: where the next minibatch's front chain forks off the step")
+    p.add_argument("--step-priority", choices=["normal", "high"], default="normal",
+                   help="run the step's own stream at high HIP stream priority (its side / prefetch streams stay "
+                        "normal), so the dispatcher serves the critical chain first")
     p.add_argument("--no-fuse-loss-tail", action="store_true",
                    help="ADD loss row tail and pose-head backward as separate launches (PoseStep fuse_loss_tail=False)")
     p.add_argument("--no-n1-reference", action="store_true",
@@ -150,6 +153,8 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", 0))
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
+    if args.step_priority == "high":  # every launch of this thread on a high-priority stream
+        torch.cuda.set_stream(torch.cuda.Stream(device=dev, priority=-1))
     dist = None
     if world > 1:
         import torch.distributed as dist
@@ -562,6 +567,7 @@ def main():
                              "configs[1]: hough_voting_gpu(test) + roi_pool x2 forward"),
                 "global_batch": gB, "per_rank_batch": B, "height": H, "width": W, "num_classes": C,
                 "skip_pixels": 10, "index_size": 128 // gB, "roi_rows_rank0": nrows,
+                "step_stream_priority": args.step_priority,
                 "pipelined": pipelined, **({"prefetch_at": args.prefetch_at,
                                             "minibatches": "two alternating minibatches (the second a copy of "
                                                            "the first in its own buffers: the same work per "

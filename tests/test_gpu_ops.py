@@ -585,8 +585,8 @@ def test_add_loss_division_correctly_rounded(hip, dbl):
 
 
 def _add_modes(args, **kw):
-    """The loss with the pruned ADD-S search (default) and the full scan
-    (PCNN_ADD_SEARCH=full), on the same inputs."""
+    """The loss with the pruned ADD-S search (PCNN_ADD_SEARCH=pruned) and the
+    full scan (the default), on the same inputs."""
     out = []
     for mode in ("pruned", "full"):
         os.environ["PCNN_ADD_SEARCH"] = mode
