@@ -62,7 +62,7 @@ def parse(argv=None):
                    help="full workloads: run the next minibatch's vote + RoI-pool forward + ADD row classification "
                         "beside the current step's loss and backward (PoseStep(pipeline=True)); two alternating "
                         "synthetic minibatches")
-    p.add_argument("--prefetch-at", choices=["loss", "bwd", "start"], default="start",
+    p.add_argument("--prefetch-at", choices=["start", "loss", "bwd", "tail"], default="start",
                    help="with --pipeline on: where the next minibatch's front chain forks off the step")
     p.add_argument("--step-priority", choices=["normal", "high"], default="normal",
                    help="run the step's own stream at high HIP stream priority (its side / prefetch streams stay "

@@ -91,9 +91,13 @@ class PoseStep:
         self._sets = [minibatch_set() for _ in range(2 if self.pipeline else 1)]
         self._cur = 0           # the set the step's forward / backward uses (and the attributes show)
         self._primed = None     # pipelined: (set index, inputs) voted + pooled ahead by the previous step
-        self.prefetch_at = prefetch_at  # where the next minibatch's front chain forks off: "loss" | "bwd" | "start"
-        if prefetch_at not in ("loss", "bwd", "start"):
-            raise ValueError("prefetch_at must be 'loss', 'bwd' or 'start'")
+        # where the next minibatch's front chain forks off: "start" (beside the
+        # fc6 forward), "loss" (after fc8's forward), "bwd" (after the head
+        # backward) or "tail" (after fc6 dX is launched: beside fc6 dW and the
+        # RoI-pool backward)
+        self.prefetch_at = prefetch_at
+        if prefetch_at not in ("loss", "bwd", "start", "tail"):
+            raise ValueError("prefetch_at must be 'start', 'loss', 'bwd' or 'tail'")
         self.pre_stream = torch.cuda.Stream(device=device) if self.pipeline else None
         self._next = None       # (inputs, set index) of the minibatch to prefetch during this step
         self.y6 = torch.zeros((CAP, units), **f32)
@@ -445,6 +449,8 @@ class PoseStep:
             weight_grads("w6", x, self.dy6, CAP, K6, w.units)
         with self._t("gemm_fc6_dx"):
             self._g("fc6_dx", self.dy6, w.w6, self.dx, b_trans=1, M_dev=nr)
+        if self.prefetch_at == "tail":
+            self._prefetch()
         dxp = self.dx.view(CAP, 7, 7, self.Ch)
         with self._t("roi_pool_bwd"):  # both pools receive d(pool5 + pool4) = dx
             rp.roi_pool_grad(conv5, h["box"], self.arg5, dxp, 7, 7, 1.0 / 16.0, 0, num_rois=nr, out=self.dconv5,

@@ -53,7 +53,7 @@ def _run(batches, weights, **kw):
     return step, res
 
 
-@pytest.mark.parametrize("fork", ["loss", "bwd", "start"])
+@pytest.mark.parametrize("fork", ["start", "loss", "bwd", "tail"])
 def test_pipelined_steps_bit_identical(hip, fork):
     batches = _batches(3)
     ref_step, ref = _run(batches, None)
