@@ -32,7 +32,7 @@ namespace {
 #endif
 constexpr int kSymLanes = ADD_LANES;           // symmetric rows: lanes per candidate group
 #ifndef ADD_GRID
-#define ADD_GRID 768
+#define ADD_GRID 1024
 #endif
 #ifndef ADD_PPL
 #define ADD_PPL 4
@@ -176,17 +176,20 @@ __device__ __forceinline__ void add_plain_row(int n, const float* __restrict__ p
   }
 }
 
-// Symmetric rows: a 512-thread workgroup owns (row, chunk of kPts = 256 query
-// points); its eight one-wave groups scan disjoint eighths of the candidate
-// list for the same query points (the first-minimum update is a dependent
-// chain, so latency, not issue, bounds a lone wave: 8 waves per item, kPPL = 4
-// chains per lane — each broadcast candidate read serves four distances: 155
-// -> 148 us against kPPL = 2 on the bench rows — three items per CU), then
-// merge in LDS in group order with a strict < —
-// a later range wins only with a strictly smaller distance, which is exactly
-// the reference's sequential first minimum (cu.cc:150-172).
+// Symmetric rows: a 256-thread workgroup owns (row, chunk of kPts = 256 query
+// points); its four one-wave groups scan disjoint quarters of the candidate
+// list for the same query points (kPPL = 4 chains per lane: each broadcast
+// candidate read serves four distances), then merge in LDS in group order
+// with a strict < — a later range wins only with a strictly smaller
+// distance, which is exactly the reference's sequential first minimum
+// (cu.cc:150-172).  Round 6 geometry sweep of the whole op on the bench's
+// rows (scripts/add_bench.py, one box, profiles/r06/add_geometry_sweep.log):
+// 8 groups / 768 workgroups 143-148 us; 4 groups 126-130 us (kept, with a
+// 1024-workgroup grid: 124-130 us); kPPL 2 129-134 us; 16 groups, kPPL 8,
+// blocks of 16: slower.  Half the workgroup, twice as many in flight: the
+// merge and per-item staging cost less, and more items overlap the scans.
 #ifndef ADD_GROUPS
-#define ADD_GROUPS 8
+#define ADD_GROUPS 4
 #endif
 constexpr int kSymGroups = ADD_GROUPS;
 constexpr int kSymThreads = kSymLanes * kSymGroups;

@@ -30,7 +30,7 @@ while [ $# -gt 0 ]; do
   case $task in
     test)
       args=(tests)
-      if [ $# -gt 0 ] && [[ $1 != test && $1 != smoke && $1 != bench && $1 != prof && $1 != pmc && $1 != sq && $1 != ab && $1 != micro && $1 != microab && $1 != sqmicro && $1 != bppmc && $1 != pose ]]; then
+      if [ $# -gt 0 ] && [[ $1 != test && $1 != smoke && $1 != bench && $1 != prof && $1 != pmc && $1 != sq && $1 != ab && $1 != micro && $1 != microab && $1 != sqmicro && $1 != bppmc && $1 != pose && $1 != dram ]]; then
         args=($1); shift
       fi
       timeout -k 10 900 python -u -m pytest "${args[@]}" -m gpu -x -v --timeout 120 --timeout-method thread \
@@ -53,6 +53,9 @@ while [ $# -gt 0 ]; do
       PMC=(--pmc VALUBusy); prof pmc_valu 4 2 --no-graph || exit 1
       PMC=(--pmc VALUBusy); prof pmc_valu_vr 20 2 --workload vote_roi --no-graph || exit 1
       python scripts/pmc_traffic.py gpurun_out > $O/pmc_traffic.txt && cp profiles/pmc_traffic.json $O/ || exit 1 ;;
+    dram)  # L2-miss reads split into MALL hits and HBM reads (the fc6 dW over-fetch question)
+      PMC=(--pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_DRAM_sum); prof pmc_dram 4 2 --no-graph || exit 1
+      python scripts/dram_split.py $O/pmc_dram > $O/dram_split.json || exit 1 ;;
     sq)
       PMC=(--pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM)
       prof sq1 2 1 --no-graph || exit 1
