@@ -193,6 +193,15 @@ __global__ void __launch_bounds__(X6Tile<T>::threads, T == 256 ? 1 : 2) k_gemm_x
     for (int i = 0; i < AM; i++)
 #pragma unroll
       for (int j = 0; j < 2; j++) acc[i][j] = (f32x16){};
+#ifdef PCNN_X6_M16ABL
+    f32x4 a16[AM][2][4];
+#pragma unroll
+    for (int i = 0; i < AM; i++)
+#pragma unroll
+      for (int j = 0; j < 2; j++)
+#pragma unroll
+        for (int p = 0; p < 4; p++) a16[i][j][p] = (f32x4){};
+#endif
     if (nsteps > 0) {
       float va[8], vb[8];
       // prologue: stage 0 -> LDS buffer 0, stage 1 -> registers
@@ -280,6 +289,18 @@ __global__ void __launch_bounds__(X6Tile<T>::threads, T == 256 ? 1 : 2) k_gemm_x
 #pragma unroll
                 for (int p = i * 4 / AMW; p < (i + 1) * 4 / AMW; p++) stage_part(p, nxt, kn);
               }
+#ifdef PCNN_X6_M16ABL  // timing ablation (wrong results): the same MFMA work as 16x16x32 instructions
+#pragma unroll
+              for (int j = 0; j < 2; j++) {
+                const bf16x8 fa[6] = {al[c], ah[c], am[c], am[c], ah[c], ah[c]};
+                const bf16x8 fb[6] = {bh[j], bl[j], bm[j], bh[j], bm[j], bh[j]};
+#pragma unroll
+                for (int p = 0; p < 12; p++)
+                  a16[i][j][p & 3] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[p >> 1], fb[p >> 1], a16[i][j][p & 3],
+                                                                             0, 0, 0);
+              }
+              if (false)
+#endif
 #pragma unroll
               for (int j = 0; j < 2; j++) {
                 acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[c], bh[j], acc[i][j], 0, 0, 0);
@@ -330,6 +351,16 @@ __global__ void __launch_bounds__(X6Tile<T>::threads, T == 256 ? 1 : 2) k_gemm_x
         else kloop_w(IC<3>{});
       }
     }
+#ifdef PCNN_X6_M16ABL
+#pragma unroll
+    for (int i = 0; i < AM; i++)
+#pragma unroll
+      for (int j = 0; j < 2; j++)
+#pragma unroll
+        for (int p = 0; p < 4; p++)
+#pragma unroll
+          for (int e = 0; e < 4; e++) acc[i][j][4 * p + e] = a16[i][j][p][e];
+#endif
     x_epilogue<T, AM>(g, pl, acc, m0, n0, rl, z, wm, wn, r, hsel);
   };
 

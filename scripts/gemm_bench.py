@@ -15,6 +15,7 @@ p.add_argument("--rows", type=int, default=405)
 p.add_argument("--precision", default="2")
 p.add_argument("--iters", type=int, default=20)
 p.add_argument("--only", default="")
+p.add_argument("--kc", action="store_true", help="also fc6 dW from k-contiguous (transposed) copies of X / dY")
 a = p.parse_args()
 D = torch.device("cuda")
 CAP, K6, U, O = 1152, 25088, 4096, 88
@@ -40,6 +41,20 @@ def cases_for(P):
         ("fc6_dw", 2 * R * K6 * U, lambda: ph.gemm(x5, dy6, gw6, a_trans=1, K_dev=nr, M=K6, N=U, K=CAP,
                                                    precision=P)),
         ("fc6_dx", 2 * R * K6 * U, lambda: ph.gemm(dy6, w6, dx, b_trans=1, M_dev=nr, precision=P)),
+    ]
+
+
+def kc_cases(P):
+    """fc6 dW with one or both operands stored k-contiguous (the transposes timed on their own)."""
+    x5t, dy6t = x5.t().contiguous(), dy6.t().contiguous()  # (K6, CAP), (U, CAP)
+    return [
+        ("tr_x5", 0, lambda: x5t.copy_(x5.t())),
+        ("tr_dy6", 0, lambda: dy6t.copy_(dy6.t())),
+        ("fc6_dw_akc", 2 * R * K6 * U, lambda: ph.gemm(x5t, dy6, gw6, K_dev=nr, M=K6, N=U, K=CAP, precision=P)),
+        ("fc6_dw_bkc", 2 * R * K6 * U, lambda: ph.gemm(x5, dy6t, gw6, a_trans=1, b_trans=1, K_dev=nr, M=K6, N=U,
+                                                       K=CAP, precision=P)),
+        ("fc6_dw_kc", 2 * R * K6 * U, lambda: ph.gemm(x5t, dy6t, gw6, b_trans=1, K_dev=nr, M=K6, N=U, K=CAP,
+                                                      precision=P)),
     ]
 
 
@@ -72,7 +87,7 @@ def tp_cases():
 for P in [int(v) for v in a.precision.split(",")]:
     print(f"precision {P}", flush=True)
     tot = 0.0
-    for name, flops, fn in (cases_for(P) if P >= 0 else tp_cases()):
+    for name, flops, fn in (cases_for(P) + (kc_cases(P) if a.kc else []) if P >= 0 else tp_cases()):
         if a.only and name not in a.only.split(","):
             continue
         for _ in range(3):

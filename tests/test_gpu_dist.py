@@ -102,10 +102,10 @@ class _HostStagedAsync(_HostStaged):
         return self._go(lambda: self.d.all_to_all_single(h, src, async_op=True), out, h, async_op)
 
 
-def _inputs(world):
+def _inputs(world, seed=77):
     from posecnn_amd import synth
-    fr = synth.make_frames(B_RANK * world, H=H, W=W, num_classes=C, objects_per_image=4, seed=77)
-    g = torch.Generator().manual_seed(5)
+    fr = synth.make_frames(B_RANK * world, H=H, W=W, num_classes=C, objects_per_image=4, seed=seed)
+    g = torch.Generator().manual_seed(5 + seed - 77)
     fr["conv4"] = torch.randn((B_RANK * world, H // 8, W // 8, CH), generator=g).numpy()
     fr["conv5"] = torch.randn((B_RANK * world, H // 16, W // 16, CH), generator=g).numpy()
     fr["points"], fr["symmetry"] = synth.rescaled_points(C)
@@ -133,15 +133,54 @@ def _run(fr, sl, global_batch, batch_base, d):
     return out
 
 
+def _device_inputs(fr, sl):
+    dev = torch.device("cuda", 0)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    inputs = {k: t(fr[k][sl]) for k in ("label", "vertex", "meta", "conv4", "conv5")}
+    inputs.update(extents=t(fr["extents"]), gt=t(fr["gt"]), points=t(fr["points"]), symmetry=t(fr["symmetry"]))
+    return inputs
+
+
+def _run_pipelined(frs, sl, global_batch, batch_base, d, pipeline):
+    """Three consecutive sharded steps over distinct minibatches; pipelined:
+    each step is handed the next minibatch, whose vote and RoI-pool forward run
+    on the prefetch stream beside the current step's collectives."""
+    from posecnn_amd.pipeline import PoseStep
+    batches = [_device_inputs(fr, sl) for fr in frs]
+    step = PoseStep(B_RANK, H, W, C, torch.device("cuda", 0), channels=CH, units=UNITS, is_train=1, skip_pixels=3,
+                    global_batch=global_batch, batch_base=batch_base, dist=d, keep_prob=1.0, pipeline=pipeline)
+    out = {}
+    for k, inp in enumerate(batches):
+        if pipeline:
+            step.step(inp, batches[k + 1] if k + 1 < len(batches) else None)
+        else:
+            step.step(inp)
+        torch.cuda.synchronize()
+        n = int(step.hough["num_rois"][0].item())
+        out[f"n{k}"] = np.array(n)
+        for name, v in (("pool", step.pool[:n]), ("loss", step.loss), ("dconv4", step.dconv4),
+                        ("dconv5", step.dconv5), ("box", step.hough["box"][:n])):
+            out[f"{name}{k}"] = v.cpu().numpy()
+        for gk, v in step.grads.items():
+            out[f"g_{gk}{k}"] = v.cpu().numpy()
+    return out
+
+
 def _worker(rank, world, port, out_dir, mode="sync"):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        fr = _inputs(world)
-        wrap = _HostStagedAsync(dist) if mode == "async" else _HostStaged(dist)
-        o = _run(fr, slice(rank * B_RANK, (rank + 1) * B_RANK), B_RANK * world, rank * B_RANK, wrap)
+        wrap = _HostStagedAsync(dist) if mode in ("async", "pipelined") else _HostStaged(dist)
+        sl = slice(rank * B_RANK, (rank + 1) * B_RANK)
+        if mode == "pipelined":
+            frs = [_inputs(world, 77 + k) for k in range(3)]
+            ref = _run_pipelined(frs, sl, B_RANK * world, rank * B_RANK, wrap, False)
+            o = _run_pipelined(frs, sl, B_RANK * world, rank * B_RANK, wrap, True)
+            o.update({"ref_" + k: v for k, v in ref.items()})
+        else:
+            o = _run(_inputs(world), sl, B_RANK * world, rank * B_RANK, wrap)
         np.savez(os.path.join(out_dir, f"rank{rank}.npz"), **o)
         dist.barrier()
     finally:
@@ -189,3 +228,20 @@ def test_sharded_step_matches_single_device(hip, tmp_path, mode):
             want = ref["g_" + k]
             np.testing.assert_allclose(o["g_" + k], want, rtol=1e-4, atol=1e-4 * np.abs(want).max())
         off += n[r]
+
+
+def test_sharded_pipelined_steps_bit_identical(hip, tmp_path):
+    """The bench's default N > 1 path: each rank's pipelined step (the next
+    minibatch's vote and pool on the prefetch stream while this step's loss
+    all-reduce, RoI row exchange and weight-gradient shards are in flight,
+    async collective handles) over three distinct minibatches, bit for bit the
+    unpipelined sharded step's outputs on the same rank."""
+    world = 2
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), "pipelined"), nprocs=world, join=True)
+    for r in range(world):
+        o = dict(np.load(tmp_path / f"rank{r}.npz"))
+        keys = [k for k in o if not k.startswith("ref_")]
+        assert len({int(o[f"n{k}"]) for k in range(3)}) > 1 or not np.array_equal(o["box0"], o["box1"])
+        for k in keys:
+            np.testing.assert_array_equal(o[k], o["ref_" + k], err_msg=f"rank {r} {k}")
+        assert all(int(o[f"n{k}"]) > 0 for k in range(3))
