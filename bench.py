@@ -62,8 +62,11 @@ def parse(argv=None):
                    help="full workloads: run the next minibatch's vote + RoI-pool forward + ADD row classification "
                         "beside the current step's loss and backward (PoseStep(pipeline=True)); two alternating "
                         "synthetic minibatches")
-    p.add_argument("--prefetch-at", choices=["start", "loss", "bwd", "tail"], default="start",
+    p.add_argument("--prefetch-at", choices=["start", "fwd", "loss", "bwd", "tail"], default="start",
                    help="with --pipeline on: where the next minibatch's front chain forks off the step")
+    p.add_argument("--defer-side-join", choices=["on", "off"], default="on",
+                   help="pipelined, one GPU: do not join the weight-gradient stream at the end of a step; the next "
+                        "step waits for it only where it first rewrites what that stream reads")
     p.add_argument("--step-priority", choices=["normal", "high"], default="normal",
                    help="run the step's own stream at high HIP stream priority (its side / prefetch streams stay "
                         "normal), so the dispatcher serves the critical chain first")
@@ -174,6 +177,7 @@ def main():
     if gB < B * world or gB > 128:
         raise SystemExit(f"--global-batch {gB}: needs per-rank batch x ranks ({B * world}) <= it <= MAX_ROI (128)")
     pipelined = full and args.pipeline == "on"
+    defer_join = pipelined and world == 1 and args.defer_side_join == "on"
     # seed = config index: configs[2] / configs[1] / configs[4]
     seed = 5 if linemod else (3 if full else 2)
     t0 = time.time()
@@ -222,7 +226,8 @@ def main():
         step = PoseStep(B, H, W, C, dev, is_train=1, skip_pixels=10, global_batch=gB, batch_base=rank * B,
                         dist=dist, precision=args.precision, pixel_argmax=not args.flat_argmax,
                         side_prep=not args.prep_on_main, drop_in_reduce=not args.mask_kernel,
-                        pipeline=pipelined, prefetch_at=args.prefetch_at, fuse_loss_tail=not args.no_fuse_loss_tail)
+                        pipeline=pipelined, prefetch_at=args.prefetch_at, fuse_loss_tail=not args.no_fuse_loss_tail,
+                        defer_side_join=defer_join)
         run = runner(step)
         step_run = run
     if linemod:  # + the depth back-projection op, forward and backward (no reference caller)
@@ -329,7 +334,7 @@ def main():
             for _ in range(per_replay):
                 run()
             if pipelined:
-                torch.cuda.current_stream().wait_stream(step.pre_stream)
+                step.join()  # the prefetch and weight-gradient streams, as capture requires
         try:
             s = torch.cuda.Stream()
             s.wait_stream(torch.cuda.current_stream())
@@ -383,7 +388,7 @@ def main():
                 continue
             step0 = PoseStep(B, H, W, C, dev, is_train=1, skip_pixels=10, global_batch=gB, batch_base=rank * B,
                              dist=dist, precision=prec, weights=step.weights, pipeline=pipelined,
-                             prefetch_at=args.prefetch_at)
+                             prefetch_at=args.prefetch_at, defer_side_join=defer_join)
             run0 = runner(step0)
             run0()
             t0_ = measure(run0)
@@ -394,7 +399,7 @@ def main():
         # graph's pose head): what the reference's training dropout costs
         step0 = PoseStep(B, H, W, C, dev, is_train=1, skip_pixels=10, global_batch=gB, batch_base=rank * B,
                          dist=dist, precision=args.precision, weights=step.weights, keep_prob=1.0,
-                         pipeline=pipelined, prefetch_at=args.prefetch_at)
+                         pipeline=pipelined, prefetch_at=args.prefetch_at, defer_side_join=defer_join)
         run0 = runner(step0)
         run0()
         t0_ = measure(run0)
@@ -507,7 +512,7 @@ def main():
         if rank == 0:
             step1 = PoseStep(B, H, W, C, dev, is_train=1, skip_pixels=10, global_batch=gB, batch_base=rank * B,
                              dist=None, precision=args.precision, weights=step.weights, pipeline=pipelined,
-                             prefetch_at=args.prefetch_at)
+                             prefetch_at=args.prefetch_at, defer_side_join=defer_join)
             run1 = runner(step1)
             for _ in range(max(2, args.warmup)):
                 run1()
@@ -568,7 +573,7 @@ def main():
                 "global_batch": gB, "per_rank_batch": B, "height": H, "width": W, "num_classes": C,
                 "skip_pixels": 10, "index_size": 128 // gB, "roi_rows_rank0": nrows,
                 "step_stream_priority": args.step_priority,
-                "pipelined": pipelined, **({"prefetch_at": args.prefetch_at,
+                "pipelined": pipelined, **({"prefetch_at": args.prefetch_at, "deferred_side_join": defer_join,
                                             "minibatches": "two alternating minibatches (the second a copy of "
                                                            "the first in its own buffers: the same work per "
                                                            "step); the next one's vote + RoI-pool forward + ADD "

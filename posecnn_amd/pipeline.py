@@ -44,7 +44,8 @@ class PoseStep:
                  is_train=1, skip_pixels=10, vote_threshold=-1.0, vote_percentage=0.02, margin=0.01,
                  global_batch=None, batch_base=0, weights=None, dist=None, backward=True, precision=2,
                  overlap_weight_grads=True, pixel_argmax=True, keep_prob=None, drop_seed=0x5EED, side_prep=True,
-                 drop_in_reduce=True, pipeline=False, prefetch_at="loss", fuse_loss_tail=True):
+                 drop_in_reduce=True, pipeline=False, prefetch_at="loss", fuse_loss_tail=True,
+                 defer_side_join=False):
         self.B, self.H, self.W, self.C = B, H, W, num_classes
         self.dev = device
         self.is_train, self.skip, self.vthr, self.vper, self.margin = is_train, skip_pixels, vote_threshold, \
@@ -92,12 +93,17 @@ class PoseStep:
         self._cur = 0           # the set the step's forward / backward uses (and the attributes show)
         self._primed = None     # pipelined: (set index, inputs) voted + pooled ahead by the previous step
         # where the next minibatch's front chain forks off: "start" (beside the
-        # fc6 forward), "loss" (after fc8's forward), "bwd" (after the head
-        # backward) or "tail" (after fc6 dX is launched: beside fc6 dW and the
-        # RoI-pool backward)
+        # fc6 forward), "fwd" (the same point on the device -- ordered after the
+        # step's start by an event -- but issued by the host after the fc6
+        # forward's launch, so the chain's first kernel is queued first),
+        # "loss" (after fc8's forward), "bwd" (after the head backward) or
+        # "tail" (after fc6 dX is launched: beside fc6 dW and the RoI-pool
+        # backward)
         self.prefetch_at = prefetch_at
-        if prefetch_at not in ("loss", "bwd", "start", "tail"):
-            raise ValueError("prefetch_at must be 'start', 'loss', 'bwd' or 'tail'")
+        if prefetch_at not in ("loss", "bwd", "start", "fwd", "tail"):
+            raise ValueError("prefetch_at must be 'start', 'fwd', 'loss', 'bwd' or 'tail'")
+        self._fork_ev = torch.cuda.Event() if self.pipeline else None
+        self._fork_recorded = False
         self.pre_stream = torch.cuda.Stream(device=device) if self.pipeline else None
         self._next = None       # (inputs, set index) of the minibatch to prefetch during this step
         self.y6 = torch.zeros((CAP, units), **f32)
@@ -161,6 +167,22 @@ class PoseStep:
         # beside the RoI pool (True), or on the step's stream with no fork /
         # join (False: the row classification right before the loss)
         self.side_prep = side_prep and self.side_stream is not None
+        # pipelined, single device: the weight-gradient stream is not joined at
+        # the end of the step; the next step waits for it only where it first
+        # rewrites what that stream reads (y6 before the fc6 forward: an event
+        # after fc7's weight gradient; dy6 before fc7 dX, and the other set's
+        # buffers before the prefetch or an un-prefetched front chain: the end
+        # of the stream), so the next step's fc6 forward starts beside this
+        # step's fc6 dW.  step() then returns before the weight gradients and
+        # the loss are ordered on the caller's stream: join() (or a device
+        # synchronize) before reading them there.
+        self.defer_side_join = bool(defer_side_join) and self.pipeline and dist is None and \
+            self.side_stream is not None
+        self._side_mid_ev = torch.cuda.Event() if self.defer_side_join else None
+        self._side_done_ev = torch.cuda.Event() if self.defer_side_join else None
+        self._side_pending = False
+        self._mid_covers_pre = False  # the mid event was recorded after the prefetch it follows was joined
+        self._mid_waited = False      # this step's stream already waited for the previous step's mid event
 
     # ------------------------------------------------------------------
     def _t(self, name):
@@ -179,6 +201,22 @@ class PoseStep:
                     e1.record()
                     step.timer.setdefault(name, []).append((self_.e0, e1))
         return _Ctx()
+
+    def join(self):
+        """Order everything the step's other streams issued (the deferred
+        weight-gradient stream, the prefetch stream) before the caller's
+        current stream's later work."""
+        cur = torch.cuda.current_stream()
+        for st in (self.side_stream, self.pre_stream):
+            if st is not None:
+                cur.wait_stream(st)
+        self._side_pending = False
+
+    def _side_wait(self, ev_name, stream=None):
+        """Deferred join: `stream` (default the current one) waits for the
+        previous step's weight-gradient stream up to the named event."""
+        if self._side_pending:
+            (stream or torch.cuda.current_stream()).wait_event(getattr(self, ev_name))
 
     # the current minibatch set's buffers (after a pipelined step: the set that
     # step trained on, not the one its prefetch filled)
@@ -239,18 +277,26 @@ class PoseStep:
 
     def _prefetch(self):
         """The next minibatch's front chain on the prefetch stream (pipelined
-        step): ordered after everything the step has issued so far on its
-        stream -- so after the previous step, which last used that set -- and
+        step): ordered after everything the step had issued on its stream at
+        the fork point ("fwd": at the step's start, through the event recorded
+        there) -- so after the previous step, which last used that set -- and
         joined by the next step before it reads the set."""
         if self._next is None:
             return
         nxt, s = self._next
         self._next = None
         if self.timer is not None:  # per-op timing runs the ops one by one on the step's stream
+            self._side_wait("_side_done_ev")  # the set's hough rows / pool / ADD workspace
+            self._side_pending = False
             self._front(nxt, s, stream=torch.cuda.current_stream())
         else:
-            self.pre_stream.wait_stream(torch.cuda.current_stream())
+            if self._fork_recorded:
+                self.pre_stream.wait_event(self._fork_ev)
+            else:
+                self.pre_stream.wait_stream(torch.cuda.current_stream())
+            self._side_wait("_side_done_ev", self.pre_stream)  # the set's hough rows / pool / ADD workspace
             self._front(nxt, s, stream=self.pre_stream)
+        self._fork_recorded = False
         self._primed = (s, nxt)
 
     def set_drop_masks(self, m6, m7):
@@ -338,8 +384,13 @@ class PoseStep:
         gen = self.keep < 1.0 and self.drop_in_reduce and not self._drop_external
         g6 = dict(drop_gen=(self.drop_seed, self.drop_step, 6)) if gen else {}
         g7 = dict(drop_gen=(self.drop_seed, self.drop_step, 7)) if gen else {}
+        if not self._mid_waited:
+            self._side_wait("_side_mid_ev")  # the previous step's fc7 weight gradient read y6
+        self._mid_waited = False
         with self._t("gemm_fc6_fwd"):
             self._g("fc6_fwd", x, w.w6, self.y6, bias=w.b6, act=1, M_dev=nr, drop=self.drop6, **dk, **g6)
+        if self.prefetch_at == "fwd":  # forked at the step's start (event), issued after the fc6 forward
+            self._prefetch()
         if gs is not None:
             gs.send_input("w7", self.y6)
         with self._t("gemm_fc7_fc8_fwd"):
@@ -443,6 +494,22 @@ class PoseStep:
             self._g("fc8_dx", self.dy8, w.w8, self.dy7, b_trans=1, mask=self.y7, M_dev=nr, **dk)
         with self._t("gemm_fc8_fc7_dw_bias"):  # fc7 weight / bias gradients
             weight_grads("w7", self.y6, self.dy7, CAP, w.units, w.units)
+        defer = self.defer_side_join and side is not None
+        self._side_wait("_side_done_ev")  # (deferred join) the previous step's fc6 dW / bias read dy6
+        self._side_pending = False
+        if defer:
+            # the mid event also covers the next minibatch's prefetch (when it
+            # was issued by now) and the dropout counter bump, so the next step
+            # starts behind one cross-stream wait instead of two or three
+            # (not while a HIP graph is captured: that step keeps both waits)
+            self._mid_covers_pre = self._primed is not None and not torch.cuda.is_current_stream_capturing()
+            if self._mid_covers_pre:
+                side.wait_stream(self.pre_stream)
+            if self._bump_drop_step and self._mid_covers_pre:
+                with torch.cuda.stream(side):  # after this step's fc6 / fc7 forward reduces read it (joined above)
+                    self.drop_step.add_(1)
+                self._bump_drop_step = False
+            self._side_mid_ev.record(side)  # after this step's last reader of y6 / y7 / dy7 / dy8
         with self._t("gemm_fc8_fc7_dx"):
             self._g("fc7_dx", self.dy7, w.w7, self.dy6, b_trans=1, mask=self.y6, M_dev=nr, **dk)
         with self._t("gemm_fc6_dw"):  # fc6 weight / bias gradients (A = pool5 + pool4)
@@ -460,7 +527,10 @@ class PoseStep:
         if self._bump_drop_step:  # next step's dropout draws (off the critical path: the side stream's tail runs)
             self.drop_step.add_(1)
             self._bump_drop_step = False
-        if side is not None:
+        if defer:
+            self._side_done_ev.record(side)
+            self._side_pending = True
+        elif side is not None:
             main.wait_stream(side)
 
     def _gemm(self, A, B, C, **kw):
@@ -504,14 +574,23 @@ class PoseStep:
         main = torch.cuda.current_stream()
         if self._primed is not None and self._primed[1] is inputs:
             self._cur = self._primed[0]
-            main.wait_stream(self.pre_stream)  # this minibatch's vote / prep / pool (previous step's prefetch)
+            if self._side_pending and self._mid_covers_pre:  # deferred join: one wait covers the prefetch too
+                main.wait_event(self._side_mid_ev)
+                self._mid_waited = True
+            else:
+                main.wait_stream(self.pre_stream)  # this minibatch's vote / prep / pool (previous step's prefetch)
         else:  # not prefetched (first step, or other inputs): its front chain here, on the step's stream
+            self._side_wait("_side_done_ev")  # it rewrites the set the previous step's weight gradients read
+            self._side_pending = False
             self._front(inputs, self._cur, stream=main)
         self._primed = None
         self._next = (next_inputs, 1 - self._cur) if next_inputs is not None else None
         self.draw_drop_masks()
         if self.prefetch_at == "start":
             self._prefetch()
+        elif self.prefetch_at == "fwd" and self._next is not None and self.timer is None:
+            self._fork_ev.record(main)
+            self._fork_recorded = True
         loss = self._train(inputs)
         self._prefetch()  # (no-op unless the fork point was never reached)
         return loss

@@ -53,7 +53,7 @@ def _run(batches, weights, **kw):
     return step, res
 
 
-@pytest.mark.parametrize("fork", ["start", "loss", "bwd", "tail"])
+@pytest.mark.parametrize("fork", ["start", "fwd", "loss", "bwd", "tail"])
 def test_pipelined_steps_bit_identical(hip, fork):
     batches = _batches(3)
     ref_step, ref = _run(batches, None)
@@ -65,6 +65,55 @@ def test_pipelined_steps_bit_identical(hip, fork):
             if key == "n" or a[key] is None:
                 continue
             assert torch.equal(a[key], b[key]), f"step {k}: {key} differs (fork {fork})"
+
+
+def _run_overlapped(batches, weights, **kw):
+    """Consecutive steps with no host synchronisation in between: each step's
+    outputs are copied on the stream that produced them right after step()
+    returns (the chain's on the step's stream, the loss and weight gradients on
+    the weight-gradient stream), so a deferred join's next step really runs
+    beside the previous step's weight gradients."""
+    step = PoseStep(B, H, W, C, D, channels=CH, units=UNITS, is_train=1, skip_pixels=3, weights=weights, **kw)
+    main_keys = ("box", "pose", "target", "weight")
+    res = []
+    for k, inp in enumerate(batches):
+        step.step(inp, batches[k + 1] if k + 1 < len(batches) else None)
+        h = step.hough
+        r = {key: h[key].clone() for key in main_keys}
+        r["num_rois"] = h["num_rois"].clone()
+        for key in ("pool", "arg5", "arg4", "diff", "y7", "dx", "dconv4", "dconv5", "dy8"):
+            r[key] = getattr(step, key).clone()
+        r["drop6"] = step.drop6.clone() if step.drop6 is not None else None
+        with torch.cuda.stream(step.side_stream):
+            r["loss"] = step.loss.clone()
+            for gk, v in step.grads.items():
+                r["g_" + gk] = v.clone()
+        res.append(r)
+    step.join()
+    torch.cuda.synchronize()
+    out = []
+    for r in res:
+        n = int(r.pop("num_rois")[1].item())
+        out.append({key: (v[:n] if v is not None and key not in ("loss", "dconv4", "dconv5") and
+                          not key.startswith("g_") else v) for key, v in r.items()} | {"n": n})
+    return step, out
+
+
+@pytest.mark.parametrize("fork", ["start", "fwd"])
+def test_pipelined_deferred_join_bit_identical(hip, fork):
+    """PoseStep(defer_side_join=True): the weight-gradient stream is not joined
+    at the end of a step; over three consecutive steps with no host sync, every
+    output is still the unpipelined step's, bit for bit."""
+    batches = _batches(3)
+    ref_step, ref = _run(batches, None)
+    step, got = _run_overlapped(batches, ref_step.weights, pipeline=True, prefetch_at=fork, defer_side_join=True)
+    assert step.defer_side_join
+    for k, (a, b) in enumerate(zip(ref, got)):
+        assert a["n"] == b["n"] > 8, (k, a["n"], b["n"])
+        for key in b:
+            if key == "n" or b[key] is None:
+                continue
+            assert torch.equal(a[key], b[key]), f"step {k}: {key} differs (fork {fork}, deferred join)"
 
 
 def test_pipelined_step_without_prefetch_and_mismatched_inputs(hip):
