@@ -463,8 +463,8 @@ class PoseStep:
         gs = self.gshard
         x = self.pool.view(CAP, K6)
 
-        def weight_grads(name, X, dY, K_loc, M, N):
-            if side is not None:
+        def weight_grads(name, X, dY, K_loc, M, N, fork=True):
+            if side is not None and fork:
                 side.wait_stream(main)
             if gs is not None:
                 gs.send_grad(name, dY, nr)
@@ -478,6 +478,11 @@ class PoseStep:
                     ph.colsum(dY, g["b" + name[1:]], M_dev=nr)
                     self._g(f"fc{name[1:]}_dw", X, dY, g[name], a_trans=1, K_dev=nr, M=M, N=N, K=K_loc)
 
+        # the fused loss tail already forked the side stream right after dY8
+        # (forward()) and nothing has been queued on this stream since: the
+        # fc8 weight gradient reuses that fork (each fork is a marker packet
+        # that leaves the chain's stream idle ~7 us)
+        fused_fork = getattr(self, "_head_bwd_done", False) and side is not None
         if not getattr(self, "_head_bwd_done", False):  # (fused into the loss's row tail inside step())
             with self._t("add_loss_head_bwd"):
                 # average_distance_loss_grad (top_diff[0] * bottom_diff) folded into
@@ -488,7 +493,7 @@ class PoseStep:
         if self.prefetch_at == "bwd":
             self._prefetch()
         with self._t("gemm_fc8_fc7_dw_bias"):  # fc8 weight / bias gradients
-            weight_grads("w8", self.y7, self.dy8, CAP, w.units, self.D)
+            weight_grads("w8", self.y7, self.dy8, CAP, w.units, self.D, fork=not fused_fork)
         dk = dict(keep_prob=self.keep) if self.keep < 1.0 else {}  # relu + dropout backward: kept grads / keep_prob
         with self._t("gemm_fc8_fc7_dx"):
             self._g("fc8_dx", self.dy8, w.w8, self.dy7, b_trans=1, mask=self.y7, M_dev=nr, **dk)
