@@ -415,7 +415,10 @@ def main():
     # p10 / p90), and the practical HBM peak (device-to-device copy) beside the
     # spec peak of the roofline
     dist_steps = distribution(graph_replay if mode == "hipgraph" else run, min(max(args.steps, 100), 200),
-                              per_replay if mode == "hipgraph" else 1)
+                              per_replay if mode == "hipgraph" else 1,
+                              group=2 if defer_join and mode != "hipgraph" else 1)
+    if defer_join and mode != "hipgraph":
+        dist_steps["grouping"] = "pairs of steps (deferred weight-gradient join), per step"
     dist_steps["mode"] = mode
     practical = d2d_gbs(dev)
     value = frames / elapsed
@@ -602,20 +605,23 @@ def main():
         dist.destroy_process_group()
 
 
-def distribution(fn, n, per_call=1):
-    """ms per step of n single steps (calls of per_call steps each, divided
-    back), each between its own HIP event pair on the current stream (the step
-    joins its side stream before it ends)."""
+def distribution(fn, n, per_call=1, group=1):
+    """ms per step of n steps, timed in groups of `group` calls of `per_call`
+    steps each between one HIP event pair on the current stream, divided back.
+    group 2 with the deferred weight-gradient join: a step's events on its own
+    stream close before its fc6 dW ends and the next step absorbs the rest, so
+    single-step samples alternate short / long around the same mean."""
     import numpy as np
     import torch
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(max(1, n // per_call))]
+           for _ in range(max(1, n // (per_call * group)))]
     for a, b in evs:
         a.record()
-        fn()
+        for _ in range(group):
+            fn()
         b.record()
     torch.cuda.synchronize()
-    t = np.array([a.elapsed_time(b) for a, b in evs]) / per_call
+    t = np.array([a.elapsed_time(b) for a, b in evs]) / (per_call * group)
     return {"median": round(float(np.median(t)), 4), "p10": round(float(np.percentile(t, 10)), 4),
             "p90": round(float(np.percentile(t, 90)), 4), "n": n}
 
