@@ -67,6 +67,9 @@ def parse(argv=None):
     p.add_argument("--defer-side-join", choices=["on", "off"], default="on",
                    help="pipelined, one GPU: do not join the weight-gradient stream at the end of a step; the next "
                         "step waits for it only where it first rewrites what that stream reads")
+    p.add_argument("--graph-repeat", type=int, default=1,
+                   help="HIP-graph timing: capture this many times the minimal step group (2 steps pipelined, else 1) "
+                        "in one replay (the streams are joined once per replay)")
     p.add_argument("--step-priority", choices=["normal", "high"], default="normal",
                    help="run the step's own stream at high HIP stream priority (its side / prefetch streams stay "
                         "normal), so the dispatcher serves the critical chain first")
@@ -328,7 +331,7 @@ def main():
     graph_replay = None
     # pipelined: one replay = two steps (both minibatches; the prefetch stream
     # is joined at the replay's end, as capture requires), so K must be even
-    per_replay = 2 if pipelined else 1
+    per_replay = (2 if pipelined else 1) * args.graph_repeat
     if world == 1 and not args.no_graph and args.steps % per_replay == 0:
         def run_replay_body():
             for _ in range(per_replay):

@@ -35,6 +35,17 @@ extern "C" {
 int pcnn_abi_version(void);
 const char* pcnn_strerror(int code);
 
+/* Completion event of the next op called on this thread (a created
+ * hipEvent_t): the op's last kernel records it through the kernel's own
+ * completion signal (hipExtLaunchKernel's stop event), so another stream can
+ * be forked off at that point without an event-record marker on the op's
+ * stream. Implemented by the fused ADD loss + head backward, the FC GEMMs
+ * (precision 2) and the RoI-pool backward; after any other op the event stays
+ * pending: pcnn_completion_event_pending() reports it (1) and clears it.
+ * (No reference counterpart: a host-side scheduling hook of the pose step.) */
+int pcnn_set_completion_event(void* event);
+int pcnn_completion_event_pending(void);
+
 /* ---------------------------------------------------------------------------
  * Hough voting (Houghvotinggpu).
  * Replaces HoughVotingLaucher (lib/hough_voting_gpu_layer/hough_voting_gpu_op.cu.cc:615-799)

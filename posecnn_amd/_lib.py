@@ -26,6 +26,8 @@ c_void_p = ctypes.c_void_p
 _SIGS = {
     "pcnn_abi_version": (c_int, []),
     "pcnn_strerror": (ctypes.c_char_p, [c_int]),
+    "pcnn_set_completion_event": (c_int, [c_void_p]),
+    "pcnn_completion_event_pending": (c_int, []),
     "pcnn_hough_voting_workspace_size": (c_size_t, [c_int, c_int, c_int, c_int, c_int, c_float]),
     "pcnn_hough_voting": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_int,
                                   c_int, c_int, c_int, c_int, c_int, c_float, c_int, c_float, c_float, c_int,

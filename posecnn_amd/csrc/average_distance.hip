@@ -1094,7 +1094,7 @@ extern "C" int pcnn_add_loss_fwd_head_bwd(const float* pred, const float* target
   const int rc = add_launch_rows(w, pred, target, weight, points, symmetry, R_cap, num_rois_dev, C, P, margin,
                                  loss_norm_rows, loss_norm_rows_dev, st);
   if (rc != PCNN_OK) return rc;
-  hipLaunchKernelGGL(k_add_finish_head, dim3((R_cap + 3) / 4), dim3(256), 0, st, R_cap, num_rois_dev, C, nchunk,
+  pcnn::launch_last(k_add_finish_head, dim3((R_cap + 3) / 4), dim3(256), 0, st, R_cap, num_rois_dev, C, nchunk,
                      w.rcls, w.partial, w.row_loss, bottom_diff, tanh_out, weight, pred, d_pred_scale, d_y8);
   PCNN_CHECK_LAUNCH();
   return PCNN_OK;

@@ -383,8 +383,8 @@ void launch_one(const GemmArgs& g, int grid, hipStream_t st) {
                               hipFuncAttributeMaxDynamicSharedMemorySize, X6Tile<T>::lds);
     if (dev >= 0 && dev < pcnn::kMaxDevices) attr_set[dev] = true;
   }
-  hipLaunchKernelGGL((k_gemm_x6<T, AT, BT, RG, S2, GN>), dim3(grid), dim3(X6Tile<T>::threads), X6Tile<T>::lds, st,
-                     g);
+  // the op's last launch when no reduce follows (gemm_impl holds the completion event back otherwise)
+  pcnn::launch_last(k_gemm_x6<T, AT, BT, RG, S2, GN>, dim3(grid), dim3(X6Tile<T>::threads), X6Tile<T>::lds, st, g);
 }
 
 template <bool AT, bool BT, bool RG, bool S2>

@@ -1,6 +1,7 @@
 // Shared device helpers for the PoseCNN MI355X kernels (gfx950, wave64).
 #pragma once
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <stdint.h>
 #include "../../include/posecnn_hip.h"
 
@@ -51,6 +52,24 @@ __device__ __forceinline__ T wave_sum(T v) {
 }
 
 inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+// Completion event of the next op (pcnn_set_completion_event): the op's LAST
+// kernel launch records it through the kernel's own completion signal
+// (hipExtLaunchKernel's stop event), so a stream forked off at that point
+// waits on it without an event-record marker packet on the launching stream.
+// Thread-local, consumed by the launch that takes it.
+extern thread_local hipEvent_t t_done_event;
+inline hipEvent_t take_done_event() {
+  hipEvent_t e = t_done_event;
+  t_done_event = nullptr;
+  return e;
+}
+
+// The last kernel of an op: records the pending completion event, if any.
+template <typename... KArgs, typename... Args>
+inline void launch_last(void (*k)(KArgs...), dim3 grid, dim3 block, uint32_t shmem, hipStream_t st, Args... args) {
+  hipExtLaunchKernelGGL(k, grid, block, shmem, st, nullptr, take_done_event(), 0, args...);
+}
 
 // Bump allocator over a caller-provided workspace (no allocation on the hot path).
 struct Carve {

@@ -835,6 +835,12 @@ static int gemm_impl(int M, int N, int K, const float* A, const float* A2, int l
     else if (a_trans && !b_trans) PCNN_X3_LAUNCH(true, false, RG, S2); \
     else PCNN_X3_LAUNCH(true, true, RG, S2);                       \
   } while (0)
+    // split-K slab reduction when the plan can split (a no-op launch is not
+    // free: queued behind a persistent GEMM on another stream it holds back
+    // everything after it on its own stream); the op's completion event goes
+    // to whichever launch is last
+    const bool reduce_after = may_split || drop || (keep_prob != 1.f && !keep_in_epilogue(g));
+    const hipEvent_t done_ev = reduce_after ? pcnn::take_done_event() : nullptr;
     if (precision == 2) launch_gemm_x6(g, (int)grid, a_trans, b_trans, ragged, A2 != nullptr, gen, st);
     else if (!ragged && !A2) PCNN_X3_LAYOUT(false, false);
     else if (!ragged) PCNN_X3_LAYOUT(false, true);
@@ -843,11 +849,10 @@ static int gemm_impl(int M, int N, int K, const float* A, const float* A2, int l
 #undef PCNN_X3_LAYOUT
 #undef PCNN_X3_LAUNCH_G
 #undef PCNN_X3_LAUNCH
-    // split-K slab reduction when the plan can split (a no-op launch is not
-    // free: queued behind a persistent GEMM on another stream it holds back
-    // everything after it on its own stream)
-    if (may_split || drop || (keep_prob != 1.f && !keep_in_epilogue(g)))
-      hipLaunchKernelGGL(k_gemm_reduce, dim3(1024), dim3(256), 0, st, g);
+    if (reduce_after) {
+      pcnn::t_done_event = done_ev;
+      pcnn::launch_last(k_gemm_reduce, dim3(1024), dim3(256), 0, st, g);
+    }
     PCNN_CHECK_LAUNCH();
     return PCNN_OK;
   }

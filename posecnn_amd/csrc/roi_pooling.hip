@@ -676,8 +676,8 @@ static int roi_pool_bwd(const float* top_diff, const void* argmax, bool px, int 
     const int tiles = ((H + tbh - 1) / tbh) * ((W + tbw - 1) / tbw);
     const unsigned nwg = (unsigned)((B * tiles * nchunk + 7) / 8 * 8);
 #define PCNN_RBW(TH, PXV)                                                                                  \
-  hipLaunchKernelGGL((k_roi_bwd_ent<TH, 4, PXV>), dim3(nwg), dim3(64 * kBWaves), 0, st, top_diff, argmax, B, H, W, C, \
-                     geo, lo, hi, pooled_h, pooled_w, bottom_diff)
+  pcnn::launch_last(k_roi_bwd_ent<TH, 4, PXV>, dim3(nwg), dim3(64 * kBWaves), 0, st, top_diff, argmax, B, H, W, C, \
+                    geo, lo, hi, pooled_h, pooled_w, bottom_diff)
     if (narrow) {
       if (px) PCNN_RBW(1, true); else PCNN_RBW(1, false);
     } else {

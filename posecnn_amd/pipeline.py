@@ -45,7 +45,7 @@ class PoseStep:
                  global_batch=None, batch_base=0, weights=None, dist=None, backward=True, precision=2,
                  overlap_weight_grads=True, pixel_argmax=True, keep_prob=None, drop_seed=0x5EED, side_prep=True,
                  drop_in_reduce=True, pipeline=False, prefetch_at="loss", fuse_loss_tail=True,
-                 defer_side_join=False):
+                 defer_side_join=False, signal_forks=True):
         self.B, self.H, self.W, self.C = B, H, W, num_classes
         self.dev = device
         self.is_train, self.skip, self.vthr, self.vper, self.margin = is_train, skip_pixels, vote_threshold, \
@@ -181,6 +181,18 @@ class PoseStep:
         self._side_mid_ev = torch.cuda.Event() if self.defer_side_join else None
         self._side_done_ev = torch.cuda.Event() if self.defer_side_join else None
         self._side_pending = False
+        # the chain's forks to the weight-gradient stream (after the fused loss
+        # tail, fc8 dX and fc7 dX) wait on an event the op's last kernel records
+        # through its own completion signal (pcnn_set_completion_event) instead
+        # of an event-record marker, which leaves the chain's stream idle ~7 us
+        # per fork; eager, single device (under graph capture: markers)
+        self.signal_forks = bool(signal_forks) and self.side_stream is not None and dist is None
+        self._fork_evs = {}
+        if self.signal_forks:
+            for k in ("loss", "fc8_dx", "fc7_dx"):
+                ev = torch.cuda.Event()
+                ev.record()  # creates the event (torch waits only on created events)
+                self._fork_evs[k] = ev
         self._mid_covers_pre = False  # the mid event was recorded after the prefetch it follows was joined
         self._mid_waited = False      # this step's stream already waited for the previous step's mid event
 
@@ -217,6 +229,31 @@ class PoseStep:
         previous step's weight-gradient stream up to the named event."""
         if self._side_pending:
             (stream or torch.cuda.current_stream()).wait_event(getattr(self, ev_name))
+
+    def _arm_fork(self, name):
+        """Arm the completion event `name` for the next library op on this
+        thread (eager, signal_forks); returns it, or None."""
+        if not self.signal_forks or self.timer is not None or torch.cuda.is_current_stream_capturing():
+            return None
+        ev = self._fork_evs[name]
+        _lib.load().pcnn_set_completion_event(ev.cuda_event)
+        return ev
+
+    @staticmethod
+    def _fork_taken(ev):
+        """The armed event if the op's last kernel recorded it, else None (and
+        the hook cleared): the caller then forks with a marker."""
+        if ev is None:
+            return None
+        return None if _lib.load().pcnn_completion_event_pending() else ev
+
+    def _fork_side(self, side, ev):
+        """`side` continues after the chain's last op: on its completion event
+        when it was taken, else behind an event-record marker."""
+        if ev is not None:
+            side.wait_event(ev)
+        else:
+            side.wait_stream(torch.cuda.current_stream())
 
     # the current minibatch set's buffers (after a pipelined step: the set that
     # step trained on, not the one its prefetch filled)
@@ -425,10 +462,11 @@ class PoseStep:
                 # the loss's row tail and the pose head's backward in one pass
                 # (dY8 straight from the row sums), the scalar loss beside the
                 # backward on the side stream: nothing on the chain reads it
+                ev = self._arm_fork("loss")
                 adl.average_distance_loss_head_bwd(self.pred, h["target"], h["weight"], points, symmetry,
                                                    self.margin, self.t8, self.one, self.diff, self.dy8, st["add_ws"],
                                                    num_rois=nr, loss_norm_rows_dev=self.norm_rows)
-                side.wait_stream(torch.cuda.current_stream())
+                self._fork_side(side, self._fork_taken(ev))
                 with torch.cuda.stream(side):
                     adl.average_distance_loss_total(CAP, self.C, points.shape[1], st["add_ws"], self.loss,
                                                     num_rois=nr)
@@ -463,9 +501,9 @@ class PoseStep:
         gs = self.gshard
         x = self.pool.view(CAP, K6)
 
-        def weight_grads(name, X, dY, K_loc, M, N, fork=True):
+        def weight_grads(name, X, dY, K_loc, M, N, fork=True, fork_ev=None):
             if side is not None and fork:
-                side.wait_stream(main)
+                self._fork_side(side, fork_ev)
             if gs is not None:
                 gs.send_grad(name, dY, nr)
             with torch.cuda.stream(side or main):
@@ -495,10 +533,12 @@ class PoseStep:
         with self._t("gemm_fc8_fc7_dw_bias"):  # fc8 weight / bias gradients
             weight_grads("w8", self.y7, self.dy8, CAP, w.units, self.D, fork=not fused_fork)
         dk = dict(keep_prob=self.keep) if self.keep < 1.0 else {}  # relu + dropout backward: kept grads / keep_prob
+        ev = self._arm_fork("fc8_dx") if side is not None else None
         with self._t("gemm_fc8_fc7_dx"):
             self._g("fc8_dx", self.dy8, w.w8, self.dy7, b_trans=1, mask=self.y7, M_dev=nr, **dk)
+        ev = self._fork_taken(ev)
         with self._t("gemm_fc8_fc7_dw_bias"):  # fc7 weight / bias gradients
-            weight_grads("w7", self.y6, self.dy7, CAP, w.units, w.units)
+            weight_grads("w7", self.y6, self.dy7, CAP, w.units, w.units, fork_ev=ev)
         defer = self.defer_side_join and side is not None
         self._side_wait("_side_done_ev")  # (deferred join) the previous step's fc6 dW / bias read dy6
         self._side_pending = False
@@ -515,10 +555,12 @@ class PoseStep:
                     self.drop_step.add_(1)
                 self._bump_drop_step = False
             self._side_mid_ev.record(side)  # after this step's last reader of y6 / y7 / dy7 / dy8
+        ev = self._arm_fork("fc7_dx") if side is not None else None
         with self._t("gemm_fc8_fc7_dx"):
             self._g("fc7_dx", self.dy7, w.w7, self.dy6, b_trans=1, mask=self.y6, M_dev=nr, **dk)
+        ev = self._fork_taken(ev)
         with self._t("gemm_fc6_dw"):  # fc6 weight / bias gradients (A = pool5 + pool4)
-            weight_grads("w6", x, self.dy6, CAP, K6, w.units)
+            weight_grads("w6", x, self.dy6, CAP, K6, w.units, fork_ev=ev)
         with self._t("gemm_fc6_dx"):
             self._g("fc6_dx", self.dy6, w.w6, self.dx, b_trans=1, M_dev=nr)
         if self.prefetch_at == "tail":
