@@ -665,7 +665,10 @@ static int roi_pool_bwd(const float* top_diff, const void* argmax, bool px, int 
   const int nchunk = (C + kBChunk - 1) / kBChunk;
   const long wg24 = (long)B * ((H + 1) / 2) * ((W + 3) / 4) * nchunk;
   const bool narrow = wg24 < PCNN_RBW_NARROW;
-  const int tbh = narrow ? 1 : 2, tbw = 4;
+#ifndef PCNN_RBW_TH
+#define PCNN_RBW_TH 2
+#endif
+  const int tbh = narrow ? 1 : PCNN_RBW_TH, tbw = 4;
   const bool vec = layout == 0 && !pool_channel && C % 2 == 0 && pooled_h * tbh <= 32 && pooled_w * tbw <= 32 &&
                    (long)H * W * C < (1l << 30) && (long)R_cap * pooled_h * pooled_w * C < (1l << 29) &&
                    // top_diff is read as b64 and bottom_diff written as float2 in both forms;
@@ -681,7 +684,7 @@ static int roi_pool_bwd(const float* top_diff, const void* argmax, bool px, int 
     if (narrow) {
       if (px) PCNN_RBW(1, true); else PCNN_RBW(1, false);
     } else {
-      if (px) PCNN_RBW(2, true); else PCNN_RBW(2, false);
+      if (px) PCNN_RBW(PCNN_RBW_TH, true); else PCNN_RBW(PCNN_RBW_TH, false);
     }
 #undef PCNN_RBW
   } else {
