@@ -62,7 +62,7 @@ def parse(argv=None):
                    help="full workloads: run the next minibatch's vote + RoI-pool forward + ADD row classification "
                         "beside the current step's loss and backward (PoseStep(pipeline=True)); two alternating "
                         "synthetic minibatches")
-    p.add_argument("--prefetch-at", choices=["start", "fwd", "loss", "bwd", "tail"], default="start",
+    p.add_argument("--prefetch-at", choices=["start", "fwd", "loss", "bwd", "tail"], default="loss",
                    help="with --pipeline on: where the next minibatch's front chain forks off the step")
     p.add_argument("--defer-side-join", choices=["on", "off"], default="on",
                    help="pipelined, one GPU: do not join the weight-gradient stream at the end of a step; the next "

@@ -99,7 +99,7 @@ def _run_overlapped(batches, weights, **kw):
     return step, out
 
 
-@pytest.mark.parametrize("fork", ["start", "fwd"])
+@pytest.mark.parametrize("fork", ["start", "fwd", "loss"])
 def test_pipelined_deferred_join_bit_identical(hip, fork):
     """PoseStep(defer_side_join=True): the weight-gradient stream is not joined
     at the end of a step; over three consecutive steps with no host sync, every
