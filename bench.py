@@ -64,6 +64,8 @@ def parse(argv=None):
                         "synthetic minibatches")
     p.add_argument("--prefetch-at", choices=["start", "fwd", "loss", "bwd", "tail"], default="loss",
                    help="with --pipeline on: where the next minibatch's front chain forks off the step")
+    p.add_argument("--pool-at-tail", action="store_true",
+                   help="pipelined: issue the prefetched minibatch's RoI-pool forward only once fc6 dX is launched")
     p.add_argument("--defer-side-join", choices=["on", "off"], default="on",
                    help="pipelined, one GPU: do not join the weight-gradient stream at the end of a step; the next "
                         "step waits for it only where it first rewrites what that stream reads")
@@ -230,7 +232,7 @@ def main():
                         dist=dist, precision=args.precision, pixel_argmax=not args.flat_argmax,
                         side_prep=not args.prep_on_main, drop_in_reduce=not args.mask_kernel,
                         pipeline=pipelined, prefetch_at=args.prefetch_at, fuse_loss_tail=not args.no_fuse_loss_tail,
-                        defer_side_join=defer_join)
+                        defer_side_join=defer_join, pool_at_tail=args.pool_at_tail)
         run = runner(step)
         step_run = run
     if linemod:  # + the depth back-projection op, forward and backward (no reference caller)
@@ -391,7 +393,8 @@ def main():
                 continue
             step0 = PoseStep(B, H, W, C, dev, is_train=1, skip_pixels=10, global_batch=gB, batch_base=rank * B,
                              dist=dist, precision=prec, weights=step.weights, pipeline=pipelined,
-                             prefetch_at=args.prefetch_at, defer_side_join=defer_join)
+                             prefetch_at=args.prefetch_at, defer_side_join=defer_join,
+                             pool_at_tail=args.pool_at_tail)
             run0 = runner(step0)
             run0()
             t0_ = measure(run0)
@@ -402,7 +405,8 @@ def main():
         # graph's pose head): what the reference's training dropout costs
         step0 = PoseStep(B, H, W, C, dev, is_train=1, skip_pixels=10, global_batch=gB, batch_base=rank * B,
                          dist=dist, precision=args.precision, weights=step.weights, keep_prob=1.0,
-                         pipeline=pipelined, prefetch_at=args.prefetch_at, defer_side_join=defer_join)
+                         pipeline=pipelined, prefetch_at=args.prefetch_at, defer_side_join=defer_join,
+                         pool_at_tail=args.pool_at_tail)
         run0 = runner(step0)
         run0()
         t0_ = measure(run0)
@@ -518,7 +522,8 @@ def main():
         if rank == 0:
             step1 = PoseStep(B, H, W, C, dev, is_train=1, skip_pixels=10, global_batch=gB, batch_base=rank * B,
                              dist=None, precision=args.precision, weights=step.weights, pipeline=pipelined,
-                             prefetch_at=args.prefetch_at, defer_side_join=defer_join)
+                             prefetch_at=args.prefetch_at, defer_side_join=defer_join,
+                             pool_at_tail=args.pool_at_tail)
             run1 = runner(step1)
             for _ in range(max(2, args.warmup)):
                 run1()

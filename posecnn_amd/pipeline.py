@@ -45,7 +45,7 @@ class PoseStep:
                  global_batch=None, batch_base=0, weights=None, dist=None, backward=True, precision=2,
                  overlap_weight_grads=True, pixel_argmax=True, keep_prob=None, drop_seed=0x5EED, side_prep=True,
                  drop_in_reduce=True, pipeline=False, prefetch_at="loss", fuse_loss_tail=True,
-                 defer_side_join=False, signal_forks=True):
+                 defer_side_join=False, signal_forks=True, pool_at_tail=False):
         self.B, self.H, self.W, self.C = B, H, W, num_classes
         self.dev = device
         self.is_train, self.skip, self.vthr, self.vper, self.margin = is_train, skip_pixels, vote_threshold, \
@@ -188,6 +188,11 @@ class PoseStep:
         # per fork; eager, single device (under graph capture: markers)
         self.signal_forks = bool(signal_forks) and self.side_stream is not None and dist is None
         self._fork_evs = {}
+        # pipelined: the prefetched minibatch's RoI-pool forward issued on the
+        # prefetch stream only once fc6 dX is launched (beside the tail),
+        # its vote and ADD row classes at the fork point
+        self.pool_at_tail = bool(pool_at_tail) and self.pipeline
+        self._pool_pending = None
         if self.signal_forks:
             for k in ("loss", "fc8_dx", "fc7_dx"):
                 ev = torch.cuda.Event()
@@ -310,7 +315,20 @@ class PoseStep:
             self.vote(inputs["label"], inputs["vertex"], inputs["extents"], inputs["meta"], inputs["gt"], s=s)
             if stream is not None:
                 self.add_prep(inputs["points"], inputs["symmetry"], s=s, stream=stream)
-                self.pool_fwd(inputs["conv4"], inputs["conv5"], s=s)
+                if self.pool_at_tail and stream is self.pre_stream:
+                    self._pool_pending = (inputs, s)
+                else:
+                    self.pool_fwd(inputs["conv4"], inputs["conv5"], s=s)
+
+    def _issue_pending_pool(self):
+        """The prefetched minibatch's RoI-pool forward (pool_at_tail), on the
+        prefetch stream behind its vote."""
+        if self._pool_pending is None:
+            return
+        inputs, s = self._pool_pending
+        self._pool_pending = None
+        with torch.cuda.stream(self.pre_stream):
+            self.pool_fwd(inputs["conv4"], inputs["conv5"], s=s)
 
     def _prefetch(self):
         """The next minibatch's front chain on the prefetch stream (pipelined
@@ -547,7 +565,8 @@ class PoseStep:
             # was issued by now) and the dropout counter bump, so the next step
             # starts behind one cross-stream wait instead of two or three
             # (not while a HIP graph is captured: that step keeps both waits)
-            self._mid_covers_pre = self._primed is not None and not torch.cuda.is_current_stream_capturing()
+            self._mid_covers_pre = (self._primed is not None and self._pool_pending is None and
+                                    not torch.cuda.is_current_stream_capturing())
             if self._mid_covers_pre:
                 side.wait_stream(self.pre_stream)
             if self._bump_drop_step and self._mid_covers_pre:
@@ -565,6 +584,7 @@ class PoseStep:
             self._g("fc6_dx", self.dy6, w.w6, self.dx, b_trans=1, M_dev=nr)
         if self.prefetch_at == "tail":
             self._prefetch()
+        self._issue_pending_pool()
         dxp = self.dx.view(CAP, 7, 7, self.Ch)
         with self._t("roi_pool_bwd"):  # both pools receive d(pool5 + pool4) = dx
             rp.roi_pool_grad(conv5, h["box"], self.arg5, dxp, 7, 7, 1.0 / 16.0, 0, num_rois=nr, out=self.dconv5,
@@ -640,6 +660,7 @@ class PoseStep:
             self._fork_recorded = True
         loss = self._train(inputs)
         self._prefetch()  # (no-op unless the fork point was never reached)
+        self._issue_pending_pool()
         return loss
 
     def _train(self, inputs):

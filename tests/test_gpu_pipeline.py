@@ -99,14 +99,16 @@ def _run_overlapped(batches, weights, **kw):
     return step, out
 
 
-@pytest.mark.parametrize("fork", ["start", "fwd", "loss"])
-def test_pipelined_deferred_join_bit_identical(hip, fork):
+@pytest.mark.parametrize("fork,pool_at_tail", [("start", False), ("fwd", False), ("loss", False), ("loss", True)])
+def test_pipelined_deferred_join_bit_identical(hip, fork, pool_at_tail):
     """PoseStep(defer_side_join=True): the weight-gradient stream is not joined
     at the end of a step; over three consecutive steps with no host sync, every
-    output is still the unpipelined step's, bit for bit."""
+    output is still the unpipelined step's, bit for bit (pool_at_tail: the
+    prefetched RoI-pool forward issued beside the tail)."""
     batches = _batches(3)
     ref_step, ref = _run(batches, None)
-    step, got = _run_overlapped(batches, ref_step.weights, pipeline=True, prefetch_at=fork, defer_side_join=True)
+    step, got = _run_overlapped(batches, ref_step.weights, pipeline=True, prefetch_at=fork, defer_side_join=True,
+                                pool_at_tail=pool_at_tail)
     assert step.defer_side_join
     for k, (a, b) in enumerate(zip(ref, got)):
         assert a["n"] == b["n"] > 8, (k, a["n"], b["n"])
