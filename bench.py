@@ -72,7 +72,7 @@ def parse(argv=None):
     p.add_argument("--graph-repeat", type=int, default=1,
                    help="HIP-graph timing: capture this many times the minimal step group (2 steps pipelined, else 1) "
                         "in one replay (the streams are joined once per replay)")
-    p.add_argument("--step-priority", choices=["normal", "high"], default="high",
+    p.add_argument("--step-priority", choices=["normal", "high"], default="normal",
                    help="run the step's own stream at high HIP stream priority (its side / prefetch streams stay "
                         "normal), so the dispatcher serves the critical chain first")
     p.add_argument("--no-fuse-loss-tail", action="store_true",
