@@ -104,7 +104,10 @@ __host__ __device__ __forceinline__ int tile_x3(int M, int N, int K) {
 //  evenly over workgroup pairs, partial tiles fixed up in fixed order by the
 //  last segment to finish): fc6 dX 295 -> 343 us — the slab round trip and
 //  the per-segment fix-up cost more than the balance gains.
-constexpr int kMaxSplitX = 32;   // split-K slices
+#ifndef PCNN_MAX_SPLIT_X
+#define PCNN_MAX_SPLIT_X 32
+#endif
+constexpr int kMaxSplitX = PCNN_MAX_SPLIT_X;  // split-K slices
 struct XPlan {
   int mt, nt, ns, Tm, tiles, mode, S;
   bool m_fast;  // tile order: the dimension with fewer tiles runs fastest (its
